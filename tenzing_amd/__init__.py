@@ -1,0 +1,102 @@
+"""tenzing_amd — MI355X-native schedule search for multi-GPU HIP + RCCL programs.
+
+A program is a DAG of operations (HIP kernels, RCCL transfers, host steps). The engine turns
+"issue order x HIP-stream assignment x kernel variant x event-synchronization placement" into a
+sequential decision problem, explores it with DFS or Monte-Carlo tree search, and benchmarks every
+candidate schedule on the GPUs (eagerly or as a captured hipGraph). Same capabilities as
+sandialabs/tenzing; see SURVEY.md for the parity map.
+
+The search engine, runtime, kernels and transports are native (``tenzing_amd._tz``); this package
+adds Python-side configuration, process bootstrap and analysis.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _load_native():
+    try:
+        return importlib.import_module("tenzing_amd._tz")
+    except ImportError as first:
+        if os.environ.get("TZ_NO_AUTOBUILD"):
+            raise
+        from . import _build
+
+        sys.stderr.write("tenzing_amd: native extension missing, building (gfx950)...\n")
+        try:
+            _build.build()
+        except Exception as e:  # pragma: no cover - surfaced to the user
+            raise ImportError(f"tenzing_amd native extension could not be built: {e}") from first
+        importlib.invalidate_caches()
+        return importlib.import_module("tenzing_amd._tz")
+
+
+_tz = _load_native()
+
+from ._tz import (  # noqa: E402,F401
+    BenchOpts,
+    BenchResult,
+    BoundGpuOp,
+    BusyKernelOp,
+    CsvBenchmarker,
+    Ctrl,
+    DfsOpts,
+    DistSpmv,
+    EmptyKernelOp,
+    EmpiricalBenchmarker,
+    EventRecord,
+    EventSync,
+    ExecMode,
+    Finish,
+    Graph,
+    HaloArgs,
+    HaloExchange,
+    HipRuntime,
+    HostExecutor,
+    MctsOpts,
+    NoOp,
+    OpBase,
+    OpIndex,
+    Platform,
+    PyCpuOp,
+    PyGpuOp,
+    RcclComm,
+    SelfCtrl,
+    Sequence,
+    SimBenchmarker,
+    SimExecutor,
+    SimGpuOp,
+    SimParams,
+    SleepOp,
+    SpmvArgs,
+    Start,
+    State,
+    StaticChoiceOp,
+    StaticCompoundOp,
+    StreamSync,
+    StreamWait,
+    StreamWaitEvent,
+    TcpCtrl,
+    TzError,
+    dfs_explore,
+    get_all_sequences,
+    hip_device_count,
+    mcts_explore,
+    random_rollout,
+    remove_redundant_syncs,
+    strategy_names,
+    verify,
+)
+
+__version__ = _tz.version()
+
+NATIVE_PATH = _tz.__file__
+
+
+def native_loaded() -> str:
+    """Path of the loaded native extension (raises if the HIP path is not available)."""
+    return NATIVE_PATH

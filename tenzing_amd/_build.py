@@ -1,0 +1,144 @@
+"""Native build for tenzing_amd: generates a ninja file and builds, in-tree,
+
+* ``tenzing_amd/_tz<EXT_SUFFIX>``  – the Python extension (C++17 core + HIP runtime + gfx950
+  kernels + RCCL transport + pybind11 bindings),
+* ``tenzing_amd/bin/tz-search``    – the standalone search CLI (no Python needed),
+* ``tenzing_amd/bin/tz-unit``      – native unit tests of the core.
+
+Host C++ is compiled with amdclang++, device code (``*.hip``) with ``hipcc --offload-arch=gfx950``
+(cross-compiles without a GPU). Reference build: CMakeLists.txt + src/CMakeLists.txt (object
+library + static lib + doctest binaries); here a single ninja graph.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = ROOT / "build"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("TZ_OFFLOAD_ARCH", "gfx950")
+
+CORE = ["json", "numeric", "ops", "graph", "state", "serdes", "ctrl", "benchmark", "solve"]
+HIP_HOST = ["hip_runtime", "rccl_comm"]
+WORKLOADS = ["halo", "spmv", "workloads_common"]
+KERNELS = ["halo_kernels", "spmv_kernels"]
+
+
+def _git_hash() -> str:
+    try:
+        return subprocess.check_output(["git", "-C", str(ROOT), "rev-parse", "--short", "HEAD"],
+                                       stderr=subprocess.DEVNULL, text=True).strip() or "unknown"
+    except Exception:
+        return "unknown"
+
+
+def ext_path() -> Path:
+    return PKG / ("_tz" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _ninja_file(debug: bool) -> str:
+    import pybind11
+
+    py_inc = sysconfig.get_paths()["include"]
+    opt = "-O0 -g" if debug else "-O3 -g1"
+    common = (f"-std=c++17 -fPIC {opt} -Wall -Wextra -Wno-unused-parameter "
+              f"-DTZ_GIT_HASH=\\\"{_git_hash()}\\\" -I{CSRC}")
+    hipdefs = f"-D__HIP_PLATFORM_AMD__ -I{ROCM}/include"
+    cxx = f"{ROCM}/lib/llvm/bin/clang++"
+    hipcc = f"{ROCM}/bin/hipcc"
+    lines = [
+        "ninja_required_version = 1.5",
+        f"cxx = {cxx}",
+        f"hipcc = {hipcc}",
+        f"cflags = {common}",
+        f"hipflags = {common} {hipdefs}",
+        f"devflags = {common} --offload-arch={ARCH} -munsafe-fp-atomics -ffp-contract=fast",
+        f"pyflags = -I{pybind11.get_include()} -I{py_inc}",
+        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lpthread",
+        "rule cxx",
+        "  command = $cxx $cflags $extra -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX $out",
+        "rule hipdev",
+        "  command = $hipcc $devflags -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = HIPCC $out",
+        "rule link_so",
+        "  command = $hipcc -shared -o $out $in $ldflags",
+        "  description = LINK $out",
+        "rule link_exe",
+        "  command = $hipcc -o $out $in $ldflags",
+        "  description = LINK $out",
+    ]
+    objs_core, objs_rt = [], []
+    for n in CORE:
+        o = f"{BUILD}/core/{n}.o"
+        lines.append(f"build {o}: cxx {CSRC}/core/{n}.cpp")
+        objs_core.append(o)
+    for n in HIP_HOST:
+        o = f"{BUILD}/hip/{n}.o"
+        lines.append(f"build {o}: cxx {CSRC}/hip/{n}.cpp")
+        lines.append(f"  extra = {hipdefs}")
+        objs_rt.append(o)
+    for n in WORKLOADS:
+        o = f"{BUILD}/workloads/{n}.o"
+        lines.append(f"build {o}: cxx {CSRC}/workloads/{n}.cpp")
+        lines.append(f"  extra = {hipdefs}")
+        objs_rt.append(o)
+    for n in KERNELS:
+        o = f"{BUILD}/kernels/{n}.o"
+        lines.append(f"build {o}: hipdev {CSRC}/kernels/{n}.hip")
+        objs_rt.append(o)
+    bind = f"{BUILD}/bind/module.o"
+    lines.append(f"build {bind}: cxx {CSRC}/bind/module.cpp")
+    lines.append(f"  extra = {hipdefs} $pyflags -fvisibility=hidden")
+    allobjs = " ".join(objs_core + objs_rt)
+    lines.append(f"build {ext_path()}: link_so {allobjs} {bind}")
+    for tool in ("tz_search", "tz_unit"):
+        o = f"{BUILD}/tools/{tool}.o"
+        lines.append(f"build {o}: cxx {CSRC}/tools/{tool}.cpp")
+        lines.append(f"  extra = {hipdefs}")
+        exe = PKG / "bin" / tool.replace("_", "-")
+        lines.append(f"build {exe}: link_exe {allobjs} {o}")
+    lines.append(f"default {ext_path()} {PKG / 'bin' / 'tz-search'} {PKG / 'bin' / 'tz-unit'}")
+    return "\n".join(lines) + "\n"
+
+
+def build(jobs: int | None = None, debug: bool = False, verbose: bool = False) -> Path:
+    """Compile everything (idempotent, incremental). Returns the extension path."""
+    BUILD.mkdir(parents=True, exist_ok=True)
+    (PKG / "bin").mkdir(exist_ok=True)
+    nf = BUILD / "build.ninja"
+    content = _ninja_file(debug)
+    if not nf.exists() or nf.read_text() != content:
+        nf.write_text(content)
+    ninja = shutil.which("ninja") or "ninja"
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    cmd = [ninja, "-C", str(BUILD), f"-j{jobs}"]
+    if verbose:
+        cmd.append("-v")
+    r = subprocess.run(cmd, text=True, capture_output=not verbose)
+    if r.returncode != 0:
+        sys.stderr.write((r.stdout or "") + (r.stderr or ""))
+        raise RuntimeError("tenzing_amd native build failed")
+    return ext_path()
+
+
+if __name__ == "__main__":
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    print(build(a.j, a.debug, a.verbose))

@@ -1,0 +1,635 @@
+// Python bindings (pybind11) for the native core, HIP runtime, RCCL transport and workloads.
+// The reference listed Python bindings as a roadmap item (README.md:56-58); here they are the
+// primary scripting surface, while the search engine itself stays native.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "core/benchmark.hpp"
+#include "core/solve.hpp"
+#include "hip/hip_runtime.hpp"
+#include "hip/rccl_comm.hpp"
+#include "kernels/kernels.hpp"
+#include "workloads/workloads.hpp"
+
+#include <sstream>
+
+namespace py = pybind11;
+using namespace tz;
+
+namespace {
+
+// ---- Python-defined ops
+
+class PyCpuOp : public CpuOp {
+public:
+  PyCpuOp(std::string name, py::function fn, double cost) : name_(std::move(name)), fn_(std::move(fn)), cost_(cost) {}
+  ~PyCpuOp() override {
+    py::gil_scoped_acquire g;
+    fn_ = py::function();
+  }
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "PyCpuOp"; }
+  double cost_us() const override { return cost_; }
+  void run(Executor &ex) const override {
+    if (!fn_) {
+      ex.host_busy(cost_);
+      return;
+    }
+    py::gil_scoped_acquire g;
+    fn_();
+  }
+
+private:
+  std::string name_;
+  py::function fn_;
+  double cost_;
+};
+
+class PyGpuOp : public GpuOp {
+public:
+  PyGpuOp(std::string name, py::function fn, double cost, bool capturable)
+      : name_(std::move(name)), fn_(std::move(fn)), cost_(cost), capturable_(capturable) {}
+  ~PyGpuOp() override {
+    py::gil_scoped_acquire g;
+    fn_ = py::function();
+  }
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "PyGpuOp"; }
+  double cost_us() const override { return cost_; }
+  bool capturable() const override { return capturable_; }
+  void launch(void *stream, Executor &) const override {
+    py::gil_scoped_acquire g;
+    fn_(reinterpret_cast<uintptr_t>(stream));
+  }
+
+private:
+  std::string name_;
+  py::function fn_;
+  double cost_;
+  bool capturable_;
+};
+
+py::dict counters_dict(const Counters &c) {
+  py::dict d;
+  for (const auto &kv : c.seconds) d[py::str(kv.first)] = kv.second;
+  return d;
+}
+
+kern::BoxDesc box_from_dict(const py::dict &d) {
+  kern::BoxDesc b;
+  b.buf = reinterpret_cast<double *>(d["buf"].cast<uintptr_t>());
+  b.grid_off = d["grid_off"].cast<int64_t>();
+  b.s1 = d["s1"].cast<int64_t>();
+  b.s2 = d["s2"].cast<int64_t>();
+  b.s3 = d["s3"].cast<int64_t>();
+  b.len = d["len"].cast<int>();
+  b.n1 = d["n1"].cast<int>();
+  b.n2 = d["n2"].cast<int>();
+  b.n3 = d["n3"].cast<int>();
+  return b;
+}
+
+py::dict box_to_dict(const kern::BoxDesc &b) {
+  py::dict d;
+  d["buf"] = reinterpret_cast<uintptr_t>(b.buf);
+  d["grid_off"] = b.grid_off;
+  d["s1"] = b.s1;
+  d["s2"] = b.s2;
+  d["s3"] = b.s3;
+  d["len"] = b.len;
+  d["n1"] = b.n1;
+  d["n2"] = b.n2;
+  d["n3"] = b.n3;
+  return d;
+}
+
+void *P(uintptr_t p) { return reinterpret_cast<void *>(p); }
+
+} // namespace
+
+PYBIND11_MODULE(_tz, m) {
+  m.doc() = "tenzing_amd native core: schedule search over HIP streams / RCCL on MI355X";
+
+  py::register_exception<tz::Error>(m, "TzError");
+  m.def("version", &version_string);
+  m.def("reproduce_json", [](const std::vector<std::string> &a) { return reproduce_json(a).dump(); });
+  m.def("set_log_level", [](int l) { set_log_level(LogLevel(l)); });
+  m.def("set_log_rank", [](int r) { log_rank() = r; });
+  m.def("hip_device_count", &hip_device_count);
+  m.def("rccl_version", &RcclComm::version);
+  m.def("strategy_names", &strategy_names);
+  m.def("prime_factors", &prime_factors);
+  m.def("runs_test", [](const std::vector<double> &v, bool rejectSmall) {
+    return runs_test(v, rejectSmall ? RunsTestSmall::Reject : RunsTestSmall::Accept);
+  }, py::arg("v"), py::arg("reject_small") = false);
+
+  // ------------------------------------------------------------------ ops
+  py::class_<OpBase, std::shared_ptr<OpBase>>(m, "OpBase")
+      .def_property_readonly("name", &OpBase::name)
+      .def_property_readonly("kind", &OpBase::kind)
+      .def_property_readonly("op_class", [](const OpBase &o) { return std::string(op_class_name(o.op_class())); })
+      .def("json", [](const OpBase &o) { return o.json().dump(); })
+      .def("desc", &OpBase::desc)
+      .def("eq", &OpBase::eq)
+      .def_property_readonly("cost_us", &OpBase::cost_us)
+      .def_property_readonly("bytes", &OpBase::bytes)
+      .def("__repr__", [](const OpBase &o) { return "<" + o.kind() + " " + o.desc() + ">"; });
+  py::class_<BoundOp, OpBase, std::shared_ptr<BoundOp>>(m, "BoundOp");
+  py::class_<CpuOp, BoundOp, std::shared_ptr<CpuOp>>(m, "CpuOp");
+  py::class_<GpuOp, OpBase, std::shared_ptr<GpuOp>>(m, "GpuOp");
+  py::class_<Start, CpuOp, std::shared_ptr<Start>>(m, "Start").def(py::init<>());
+  py::class_<Finish, CpuOp, std::shared_ptr<Finish>>(m, "Finish").def(py::init<>());
+  py::class_<NoOp, CpuOp, std::shared_ptr<NoOp>>(m, "NoOp")
+      .def(py::init<std::string, double>(), py::arg("name"), py::arg("cost_us") = 0.0);
+  py::class_<SleepOp, CpuOp, std::shared_ptr<SleepOp>>(m, "SleepOp").def(py::init<std::string, double>());
+  py::class_<PyCpuOp, CpuOp, std::shared_ptr<PyCpuOp>>(m, "PyCpuOp")
+      .def(py::init<std::string, py::function, double>(), py::arg("name"), py::arg("fn"), py::arg("cost_us") = 0.0);
+  py::class_<SimGpuOp, GpuOp, std::shared_ptr<SimGpuOp>>(m, "SimGpuOp").def(py::init<std::string, double>());
+  py::class_<PyGpuOp, GpuOp, std::shared_ptr<PyGpuOp>>(m, "PyGpuOp")
+      .def(py::init<std::string, py::function, double, bool>(), py::arg("name"), py::arg("fn"),
+           py::arg("cost_us") = 0.0, py::arg("capturable") = true);
+  py::class_<EmptyKernelOp, GpuOp, std::shared_ptr<EmptyKernelOp>>(m, "EmptyKernelOp").def(py::init<std::string>());
+  py::class_<BusyKernelOp, GpuOp, std::shared_ptr<BusyKernelOp>>(m, "BusyKernelOp")
+      .def(py::init<std::string, double, int>(), py::arg("name"), py::arg("us"), py::arg("blocks") = 1);
+  py::class_<BoundGpuOp, BoundOp, std::shared_ptr<BoundGpuOp>>(m, "BoundGpuOp")
+      .def(py::init([](std::shared_ptr<GpuOp> op, int s) { return std::make_shared<BoundGpuOp>(op, s); }))
+      .def_property_readonly("stream", &BoundGpuOp::stream)
+      .def_property_readonly("unbound", [](const BoundGpuOp &b) { return std::const_pointer_cast<GpuOp>(b.unbound()); });
+  py::class_<SyncOp, BoundOp, std::shared_ptr<SyncOp>>(m, "SyncOp")
+      .def_property_readonly("stream", &SyncOp::stream)
+      .def_property_readonly("event", &SyncOp::event);
+  py::class_<EventRecord, SyncOp, std::shared_ptr<EventRecord>>(m, "EventRecord")
+      .def(py::init<int, int, std::string>(), py::arg("event"), py::arg("stream"), py::arg("name") = "");
+  py::class_<StreamWaitEvent, SyncOp, std::shared_ptr<StreamWaitEvent>>(m, "StreamWaitEvent")
+      .def(py::init<int, int, std::string>(), py::arg("stream"), py::arg("event"), py::arg("name") = "");
+  py::class_<EventSync, SyncOp, std::shared_ptr<EventSync>>(m, "EventSync")
+      .def(py::init<int, std::string>(), py::arg("event"), py::arg("name") = "");
+  py::class_<StreamSync, SyncOp, std::shared_ptr<StreamSync>>(m, "StreamSync")
+      .def(py::init<int, std::string>(), py::arg("stream"), py::arg("name") = "");
+  py::class_<StreamWait, SyncOp, std::shared_ptr<StreamWait>>(m, "StreamWait")
+      .def(py::init<int, int, std::string>(), py::arg("waiter"), py::arg("waitee"), py::arg("name") = "");
+  py::class_<ChoiceOp, OpBase, std::shared_ptr<ChoiceOp>>(m, "ChoiceOp")
+      .def("choices", [](const ChoiceOp &c) {
+        std::vector<std::shared_ptr<OpBase>> out;
+        for (auto &x : c.choices()) out.push_back(std::const_pointer_cast<OpBase>(x));
+        return out;
+      });
+  py::class_<StaticChoiceOp, ChoiceOp, std::shared_ptr<StaticChoiceOp>>(m, "StaticChoiceOp")
+      .def(py::init([](std::string name, std::vector<std::shared_ptr<OpBase>> ch) {
+        std::vector<OpPtr> c(ch.begin(), ch.end());
+        return std::make_shared<StaticChoiceOp>(name, c);
+      }));
+  py::class_<CompoundOp, OpBase, std::shared_ptr<CompoundOp>>(m, "CompoundOp")
+      .def("graph", [](const CompoundOp &c) { return std::const_pointer_cast<Graph>(c.graph()); });
+  py::class_<StaticCompoundOp, CompoundOp, std::shared_ptr<StaticCompoundOp>>(m, "StaticCompoundOp")
+      .def(py::init([](std::string name, std::shared_ptr<Graph> g) {
+        return std::make_shared<StaticCompoundOp>(name, std::make_shared<Graph>(*g));
+      }));
+
+  auto cop = [](const std::shared_ptr<OpBase> &o) { return std::const_pointer_cast<const OpBase>(o); };
+
+  // ------------------------------------------------------------------ graph
+  py::class_<Graph, std::shared_ptr<Graph>>(m, "Graph")
+      .def(py::init<>())
+      .def("add", [cop](Graph &g, std::shared_ptr<OpBase> o) { return g.add(cop(o)); })
+      .def("then", [cop](Graph &g, std::shared_ptr<OpBase> a, std::shared_ptr<OpBase> b) { g.then(cop(a), cop(b)); })
+      .def("start_then", [cop](Graph &g, std::shared_ptr<OpBase> a) { g.start_then(cop(a)); })
+      .def("then_finish", [cop](Graph &g, std::shared_ptr<OpBase> a) { g.then_finish(cop(a)); })
+      .def("add_edge", &Graph::add_edge)
+      .def("normalize", &Graph::normalize)
+      .def("__len__", &Graph::size)
+      .def_property_readonly("capacity", &Graph::capacity)
+      .def("vertices", &Graph::vertices)
+      .def("op", [](const Graph &g, int i) { return std::const_pointer_cast<OpBase>(g.op(i)); })
+      .def("preds", &Graph::preds)
+      .def("succs", &Graph::succs)
+      .def("find", &Graph::find)
+      .def("contains", &Graph::contains)
+      .def("topo_order", &Graph::topo_order)
+      .def("num_edges", &Graph::num_edges)
+      .def("clone", [](const Graph &g) { return g.clone(); })
+      .def("clone_but_replace", [cop](const Graph &g, int id, std::shared_ptr<OpBase> o) { return g.clone_but_replace(id, cop(o)); })
+      .def("clone_but_expand", &Graph::clone_but_expand)
+      .def("dump_graphviz", &Graph::dump_graphviz, py::arg("title") = "")
+      .def("json", [](const Graph &g) { return g.json().dump(); });
+
+  // ------------------------------------------------------------------ SDP
+  py::class_<Platform>(m, "Platform")
+      .def(py::init([](int n, bool sym, bool ss) {
+        Platform p;
+        p.n_streams = n;
+        p.symmetric_streams = sym;
+        p.offer_stream_sync = ss;
+        return p;
+      }), py::arg("n_streams") = 2, py::arg("symmetric_streams") = true, py::arg("offer_stream_sync") = false)
+      .def_readwrite("n_streams", &Platform::n_streams)
+      .def_readwrite("symmetric_streams", &Platform::symmetric_streams)
+      .def_readwrite("offer_stream_sync", &Platform::offer_stream_sync);
+
+  py::class_<Sequence>(m, "Sequence")
+      .def(py::init<>())
+      .def("__len__", &Sequence::size)
+      .def("__getitem__", [](const Sequence &s, size_t i) {
+        if (i >= s.size()) throw py::index_error();
+        return std::const_pointer_cast<BoundOp>(s[i]);
+      })
+      .def("append", [](Sequence &s, std::shared_ptr<BoundOp> o) { s.push_back(o, -1); })
+      .def("ops", [](const Sequence &s) {
+        std::vector<std::shared_ptr<BoundOp>> v;
+        for (auto &e : s.entries) v.push_back(std::const_pointer_cast<BoundOp>(e.op));
+        return v;
+      })
+      .def("json", [](const Sequence &s, bool ig) { return s.json(ig).dump(); }, py::arg("in_graph") = false)
+      .def("desc", &Sequence::desc, py::arg("delim") = ", ")
+      .def("canonical_key", &Sequence::canonical_key)
+      .def("num_events", &Sequence::num_events)
+      .def("num_streams", &Sequence::num_streams)
+      .def("count_sync_ops", &Sequence::count_sync_ops)
+      .def("equivalent", [](const Sequence &a, const Sequence &b) { return equivalent(a, b); });
+
+  py::class_<Decision>(m, "Decision")
+      .def_property_readonly("kind", [](const Decision &d) {
+        switch (d.kind) {
+        case Decision::Kind::Execute: return "Execute";
+        case Decision::Kind::Expand: return "Expand";
+        case Decision::Kind::Choose: return "Choose";
+        default: return "Assign";
+        }
+      })
+      .def_property_readonly("op", [](const Decision &d) { return std::const_pointer_cast<BoundOp>(d.op); })
+      .def_readonly("node", &Decision::node)
+      .def_readonly("stream", &Decision::stream)
+      .def_readonly("choice", &Decision::choice)
+      .def("desc", &Decision::desc)
+      .def("__repr__", &Decision::desc);
+
+  py::class_<State>(m, "State")
+      .def(py::init([](std::shared_ptr<Graph> g, const Platform &p) { return State(g, p); }),
+           py::arg("graph"), py::arg("platform") = Platform())
+      .def_property_readonly("sequence", &State::sequence)
+      .def_property_readonly("graph", [](const State &s) { return std::const_pointer_cast<Graph>(s.graph_ptr()); })
+      .def("frontier", &State::frontier)
+      .def("get_decisions", &State::get_decisions)
+      .def("apply", &State::apply)
+      .def("complete", &State::complete)
+      .def("stream_of", &State::stream_of)
+      .def("executed", &State::executed)
+      .def("canonical_key", &State::canonical_key)
+      .def("equivalent", [](const State &a, const State &b) { return equivalent(a, b); });
+
+  m.def("verify", [](const Sequence &s, const Graph &g, int n) {
+    std::vector<std::string> out;
+    for (auto &v : verify(s, g, n)) out.push_back(v.desc());
+    return out;
+  });
+  m.def("remove_redundant_syncs", [](Sequence s, const Graph &g, int n) {
+    int k = remove_redundant_syncs(s, g, n);
+    return py::make_tuple(s, k);
+  });
+  m.def("random_rollout", [](const State &s, uint64_t seed) {
+    std::mt19937_64 rng(seed);
+    return random_rollout(s, rng);
+  });
+
+  py::class_<OpIndex>(m, "OpIndex")
+      .def(py::init<const Graph &>())
+      .def("from_json", [](const OpIndex &i, const std::string &j) { return std::const_pointer_cast<BoundOp>(i.from_json(Json::parse(j))); })
+      .def("sequence_from_json", [](const OpIndex &i, const std::string &j) { return i.sequence_from_json(Json::parse(j)); });
+
+  // ------------------------------------------------------------------ benchmark
+  py::class_<BenchOpts>(m, "BenchOpts")
+      .def(py::init([](int64_t n, int r, double t, bool rs) {
+        BenchOpts o;
+        o.n_iters = n;
+        o.max_retries = r;
+        o.target_secs = t;
+        o.small_sample = rs ? RunsTestSmall::Reject : RunsTestSmall::Accept;
+        return o;
+      }), py::arg("n_iters") = 1000, py::arg("max_retries") = 10, py::arg("target_secs") = 0.01,
+         py::arg("reject_small_samples") = false)
+      .def_readwrite("n_iters", &BenchOpts::n_iters)
+      .def_readwrite("max_retries", &BenchOpts::max_retries)
+      .def_readwrite("target_secs", &BenchOpts::target_secs);
+
+  py::class_<BenchResult>(m, "BenchResult")
+      .def(py::init<>())
+      .def_readwrite("pct01", &BenchResult::pct01)
+      .def_readwrite("pct10", &BenchResult::pct10)
+      .def_readwrite("pct50", &BenchResult::pct50)
+      .def_readwrite("pct90", &BenchResult::pct90)
+      .def_readwrite("pct99", &BenchResult::pct99)
+      .def_readwrite("stddev", &BenchResult::stddev)
+      .def_readonly("samples_per_measurement", &BenchResult::samples_per_measurement)
+      .def_readonly("retries", &BenchResult::retries)
+      .def("json", [](const BenchResult &r) { return r.json().dump(); })
+      .def_static("from_times", &BenchResult::from_times);
+
+  py::class_<Benchmarker>(m, "Benchmarker")
+      .def("benchmark", &Benchmarker::benchmark, py::call_guard<py::gil_scoped_release>());
+  py::class_<SimParams>(m, "SimParams")
+      .def(py::init<>())
+      .def_readwrite("launch_us", &SimParams::launch_us)
+      .def_readwrite("api_us", &SimParams::api_us)
+      .def_readwrite("sync_us", &SimParams::sync_us)
+      .def_readwrite("noise", &SimParams::noise)
+      .def_readwrite("seed", &SimParams::seed)
+      .def_readwrite("contention", &SimParams::contention);
+  py::class_<SimBenchmarker, Benchmarker>(m, "SimBenchmarker")
+      .def(py::init<int, SimParams>(), py::arg("n_streams"), py::arg("params") = SimParams());
+  py::class_<SimExecutor>(m, "SimExecutor")
+      .def(py::init<int, SimParams>(), py::arg("n_streams"), py::arg("params") = SimParams())
+      .def("run_once", &SimExecutor::run_once)
+      .def("trace", [](const SimExecutor &e) {
+        py::list l;
+        for (auto &s : e.trace()) l.append(py::make_tuple(s.name, s.stream, s.start, s.end));
+        return l;
+      });
+  py::class_<CsvBenchmarker, Benchmarker>(m, "CsvBenchmarker")
+      .def(py::init<const std::string &, const Graph &>())
+      .def("__len__", &CsvBenchmarker::size);
+  py::class_<ExecutorRunner>(m, "ExecutorRunner")
+      .def("prepare", &ExecutorRunner::prepare, py::call_guard<py::gil_scoped_release>())
+      .def("run", &ExecutorRunner::run, py::call_guard<py::gil_scoped_release>());
+  py::class_<HostExecutor, ExecutorRunner>(m, "HostExecutor").def(py::init<int>());
+  py::class_<EmpiricalBenchmarker, Benchmarker>(m, "EmpiricalBenchmarker")
+      .def(py::init<ExecutorRunner &, Ctrl &>(), py::keep_alive<1, 2>(), py::keep_alive<1, 3>());
+
+  // ------------------------------------------------------------------ control plane
+  py::class_<Ctrl, std::shared_ptr<Ctrl>>(m, "Ctrl")
+      .def_property_readonly("rank", &Ctrl::rank)
+      .def_property_readonly("size", &Ctrl::size)
+      .def("barrier", &Ctrl::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("bcast", [](Ctrl &c, std::string s, int root) {
+        {
+          py::gil_scoped_release r;
+          c.bcast(s, root);
+        }
+        return py::bytes(s);
+      }, py::arg("data"), py::arg("root") = 0)
+      .def("allreduce_max", [](Ctrl &c, std::vector<double> v) {
+        py::gil_scoped_release r;
+        c.allreduce_max(v.data(), v.size());
+        return v;
+      })
+      .def("allreduce_sum", [](Ctrl &c, std::vector<double> v) {
+        py::gil_scoped_release r;
+        c.allreduce_sum(v.data(), v.size());
+        return v;
+      })
+      .def("allgather", [](Ctrl &c, const std::string &s) {
+        std::vector<std::string> out;
+        {
+          py::gil_scoped_release r;
+          out = c.allgather(s);
+        }
+        py::list l;
+        for (auto &x : out) l.append(py::bytes(x));
+        return l;
+      });
+  py::class_<SelfCtrl, Ctrl, std::shared_ptr<SelfCtrl>>(m, "SelfCtrl").def(py::init<>());
+  py::class_<TcpCtrl, Ctrl, std::shared_ptr<TcpCtrl>>(m, "TcpCtrl")
+      .def(py::init<int, int>())
+      .def("listen", &TcpCtrl::listen, py::arg("port") = 0, py::arg("bind_addr") = "0.0.0.0")
+      .def("connect", &TcpCtrl::connect, py::arg("host"), py::arg("port"), py::arg("timeout_s") = 300.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("rendezvous_file", &TcpCtrl::rendezvous_file, py::arg("path"), py::arg("host") = "127.0.0.1",
+           py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>());
+
+  // ------------------------------------------------------------------ solvers
+  py::class_<MctsOpts>(m, "MctsOpts")
+      .def(py::init<>())
+      .def_readwrite("n_iters", &MctsOpts::n_iters)
+      .def_readwrite("time_budget_s", &MctsOpts::time_budget_s)
+      .def_readwrite("expand_rollout", &MctsOpts::expand_rollout)
+      .def_readwrite("remove_redundant_syncs", &MctsOpts::remove_redundant_syncs)
+      .def_readwrite("reuse_measurements", &MctsOpts::reuse_measurements)
+      .def_readwrite("verify", &MctsOpts::verify)
+      .def_readwrite("dump_tree", &MctsOpts::dump_tree)
+      .def_readwrite("dump_tree_prefix", &MctsOpts::dump_tree_prefix)
+      .def_readwrite("strategy", &MctsOpts::strategy)
+      .def_readwrite("seed", &MctsOpts::seed)
+      .def_readwrite("explore_c", &MctsOpts::explore_c)
+      .def_readwrite("bench", &MctsOpts::bench)
+      .def_readwrite("checkpoint_path", &MctsOpts::checkpoint_path)
+      .def_readwrite("checkpoint_every", &MctsOpts::checkpoint_every)
+      .def_readwrite("resume_path", &MctsOpts::resume_path)
+      .def_readwrite("trap_signals", &MctsOpts::trap_signals)
+      .def("json", [](const MctsOpts &o) { return o.json().dump(); });
+  py::class_<DfsOpts>(m, "DfsOpts")
+      .def(py::init<>())
+      .def_readwrite("max_seqs", &DfsOpts::max_seqs)
+      .def_readwrite("dedup_states", &DfsOpts::dedup_states)
+      .def_readwrite("remove_redundant_syncs", &DfsOpts::remove_redundant_syncs)
+      .def_readwrite("bench", &DfsOpts::bench)
+      .def_readwrite("trap_signals", &DfsOpts::trap_signals)
+      .def("json", [](const DfsOpts &o) { return o.json().dump(); });
+  py::class_<SimResult>(m, "SimResult")
+      .def_readonly("seq", &SimResult::seq)
+      .def_readonly("res", &SimResult::res)
+      .def_readonly("cached", &SimResult::cached);
+  py::class_<SearchResult>(m, "SearchResult")
+      .def_readonly("sims", &SearchResult::sims)
+      .def_readonly("wall_s", &SearchResult::wall_s)
+      .def_readonly("tree_size", &SearchResult::tree_size)
+      .def_readonly("tree_fully_visited", &SearchResult::tree_fully_visited)
+      .def_readonly("stop_reason", &SearchResult::stop_reason)
+      .def("best", &SearchResult::best)
+      .def("counters", [](const SearchResult &r) { return counters_dict(r.counters); })
+      .def("dump_csv", [](const SearchResult &r) {
+        std::ostringstream ss;
+        r.dump_csv(ss);
+        return ss.str();
+      })
+      .def("dump_jsonl", [](const SearchResult &r) {
+        std::ostringstream ss;
+        r.dump_jsonl(ss);
+        return ss.str();
+      });
+  m.def("mcts_explore", [](std::shared_ptr<Graph> g, const Platform &p, Benchmarker &b, Ctrl &c,
+                           const MctsOpts &o, py::object cb) {
+    std::function<void(size_t, const SimResult &)> f;
+    if (!cb.is_none()) {
+      f = [cb](size_t i, const SimResult &r) {
+        py::gil_scoped_acquire a;
+        cb(i, r);
+      };
+    }
+    py::gil_scoped_release r;
+    return mcts_explore(*g, p, b, c, o, f);
+  }, py::arg("graph"), py::arg("platform"), py::arg("bench"), py::arg("ctrl"), py::arg("opts"),
+     py::arg("callback") = py::none());
+  m.def("dfs_explore", [](std::shared_ptr<Graph> g, const Platform &p, Benchmarker &b, Ctrl &c,
+                          const DfsOpts &o, py::object cb) {
+    std::function<void(size_t, const SimResult &)> f;
+    if (!cb.is_none()) {
+      f = [cb](size_t i, const SimResult &r) {
+        py::gil_scoped_acquire a;
+        cb(i, r);
+      };
+    }
+    py::gil_scoped_release r;
+    return dfs_explore(*g, p, b, c, o, f);
+  }, py::arg("graph"), py::arg("platform"), py::arg("bench"), py::arg("ctrl"), py::arg("opts"),
+     py::arg("callback") = py::none());
+  m.def("get_all_sequences", [](std::shared_ptr<Graph> g, const Platform &p, int64_t mx, bool dd, bool rr) {
+    py::gil_scoped_release r;
+    return get_all_sequences(*g, p, mx, dd, rr);
+  }, py::arg("graph"), py::arg("platform"), py::arg("max_seqs") = -1, py::arg("dedup_states") = true,
+     py::arg("remove_redundant_syncs") = true);
+
+  // ------------------------------------------------------------------ HIP runtime
+  py::enum_<ExecMode>(m, "ExecMode").value("Eager", ExecMode::Eager).value("Graph", ExecMode::Graph);
+  py::class_<HipRuntime, ExecutorRunner>(m, "HipRuntime")
+      .def(py::init([](int device, int n, std::vector<int> prio, bool cu, ExecMode mode, double wd) {
+        HipRuntimeOpts o;
+        o.device = device;
+        o.n_streams = n;
+        o.priorities = prio;
+        o.cu_partition = cu;
+        o.mode = mode;
+        o.watchdog_s = wd;
+        return new HipRuntime(o);
+      }), py::arg("device") = -1, py::arg("n_streams") = 2, py::arg("priorities") = std::vector<int>{},
+         py::arg("cu_partition") = false, py::arg("mode") = ExecMode::Eager, py::arg("watchdog_s") = 0.0)
+      .def("set_mode", &HipRuntime::set_mode)
+      .def_property_readonly("mode", &HipRuntime::mode)
+      .def_property_readonly("effective_mode", &HipRuntime::effective_mode)
+      .def_property_readonly("device", &HipRuntime::device)
+      .def("device_name", &HipRuntime::device_name)
+      .def("graph_nodes", &HipRuntime::graph_nodes)
+      .def("num_streams", &HipRuntime::num_streams)
+      .def("native_stream", [](HipRuntime &r, int s) { return reinterpret_cast<uintptr_t>(r.native_stream(s)); })
+      .def("device_sync", &HipRuntime::device_sync, py::call_guard<py::gil_scoped_release>())
+      .def("set_watchdog", &HipRuntime::set_watchdog);
+
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init([](Ctrl &c, int dev) { return std::make_shared<RcclComm>(c, dev); }))
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def("allreduce_sum", [](const RcclComm &c, uintptr_t buf, size_t n, int dt, uintptr_t s) {
+        c.allreduce_sum(P(buf), n, dt, P(s));
+      })
+      .def("sendrecv", [](const RcclComm &c, uintptr_t sb, size_t sc, int sp, uintptr_t rb, size_t rc, int rp, int dt, uintptr_t s) {
+        c.sendrecv(P(sb), sc, sp, P(rb), rc, rp, dt, P(s));
+      });
+
+  // ------------------------------------------------------------------ workloads
+  py::class_<HaloArgs>(m, "HaloArgs")
+      .def(py::init<>())
+      .def_readwrite("nx", &HaloArgs::nx)
+      .def_readwrite("ny", &HaloArgs::ny)
+      .def_readwrite("nz", &HaloArgs::nz)
+      .def_readwrite("nq", &HaloArgs::nq)
+      .def_readwrite("ghost", &HaloArgs::ghost)
+      .def_readwrite("neighbors", &HaloArgs::neighbors)
+      .def_readwrite("order", &HaloArgs::order)
+      .def_readwrite("transport", &HaloArgs::transport)
+      .def_readwrite("fuse", &HaloArgs::fuse)
+      .def_readwrite("comms", &HaloArgs::comms)
+      .def_readwrite("rank", &HaloArgs::rank)
+      .def_readwrite("size", &HaloArgs::size)
+      .def_readwrite("px", &HaloArgs::px)
+      .def_readwrite("py", &HaloArgs::py)
+      .def_readwrite("pz", &HaloArgs::pz)
+      .def_readwrite("device", &HaloArgs::device)
+      .def("json", [](const HaloArgs &a) { return a.json().dump(); });
+  py::class_<HaloExchange, std::shared_ptr<HaloExchange>>(m, "HaloExchange")
+      .def(py::init([](const HaloArgs &a) { return std::make_shared<HaloExchange>(a); }))
+      .def_property_readonly("args", &HaloExchange::args)
+      .def("ndirs", &HaloExchange::ndirs)
+      .def("dir_name", [](const HaloExchange &h, int i) { return h.dir(i).name(); })
+      .def("dir", [](const HaloExchange &h, int i) { auto d = h.dir(i); return py::make_tuple(d.dx, d.dy, d.dz); })
+      .def("opposite", &HaloExchange::opposite)
+      .def("neighbor", &HaloExchange::neighbor)
+      .def("coords", &HaloExchange::coords)
+      .def("rank_grid", &HaloExchange::rank_grid)
+      .def("box_elems", &HaloExchange::box_elems)
+      .def("pack_box", [](const HaloExchange &h, int i) { return box_to_dict(h.pack_box(i)); })
+      .def("unpack_box", [](const HaloExchange &h, int i) { return box_to_dict(h.unpack_box(i)); })
+      .def("grid_elems", &HaloExchange::grid_elems)
+      .def("exchange_bytes", &HaloExchange::exchange_bytes)
+      .def("setup", [](HaloExchange &h, Ctrl *c) { h.setup(c); }, py::arg("ctrl") = nullptr,
+           py::call_guard<py::gil_scoped_release>())
+      .def("ready", &HaloExchange::ready)
+      .def("add_to_graph", &HaloExchange::add_to_graph)
+      .def("grid_ptr", [](const HaloExchange &h) { return reinterpret_cast<uintptr_t>(h.grid()); })
+      .def("init_grid", [](HaloExchange &h, uintptr_t s) { h.init_grid(P(s)); }, py::arg("stream") = 0)
+      .def("check_grid", [](HaloExchange &h, uintptr_t s) { return h.check_grid(P(s)); }, py::arg("stream") = 0)
+      .def("pack", [](const HaloExchange &h, int i, uintptr_t s) { h.pack(i, P(s)); })
+      .def("unpack", [](const HaloExchange &h, int i, uintptr_t s) { h.unpack(i, P(s)); })
+      .def("shift", [](const HaloExchange &h, int i, uintptr_t s) { h.shift(i, P(s)); })
+      .def("pack_all", [](const HaloExchange &h, uintptr_t s) { h.pack_all(P(s)); })
+      .def("unpack_all", [](const HaloExchange &h, uintptr_t s) { h.unpack_all(P(s)); })
+      .def("shift_all", [](const HaloExchange &h, uintptr_t s) { h.shift_all(P(s)); })
+      .def("uses_rccl", &HaloExchange::uses_rccl);
+
+  py::class_<SpmvArgs>(m, "SpmvArgs")
+      .def(py::init<>())
+      .def_readwrite("m", &SpmvArgs::m)
+      .def_readwrite("bw", &SpmvArgs::bw)
+      .def_readwrite("nnz", &SpmvArgs::nnz)
+      .def_readwrite("seed", &SpmvArgs::seed)
+      .def_readwrite("rank", &SpmvArgs::rank)
+      .def_readwrite("size", &SpmvArgs::size)
+      .def_readwrite("device", &SpmvArgs::device)
+      .def_readwrite("compound", &SpmvArgs::compound)
+      .def_readwrite("kernel_choice", &SpmvArgs::kernel_choice)
+      .def_readwrite("prefix", &SpmvArgs::prefix)
+      .def("json", [](const SpmvArgs &a) { return a.json().dump(); });
+  py::class_<DistSpmv, std::shared_ptr<DistSpmv>>(m, "DistSpmv")
+      .def(py::init([](const SpmvArgs &a) { return std::make_shared<DistSpmv>(a); }))
+      .def_property_readonly("args", &DistSpmv::args)
+      .def("local_rows", &DistSpmv::local_rows)
+      .def("local_nnz", &DistSpmv::local_nnz)
+      .def("remote_nnz", &DistSpmv::remote_nnz)
+      .def("remote_cols", &DistSpmv::remote_cols)
+      .def("send_elems", &DistSpmv::send_elems)
+      .def("num_peers", &DistSpmv::num_peers)
+      .def("setup", [](DistSpmv &s, Ctrl *c) { s.setup(c); }, py::arg("ctrl") = nullptr,
+           py::call_guard<py::gil_scoped_release>())
+      .def("ready", &DistSpmv::ready)
+      .def("add_to_graph", &DistSpmv::add_to_graph)
+      .def("op_graph", [](DistSpmv &s) { return std::const_pointer_cast<Graph>(s.op_graph()); })
+      .def("check", [](DistSpmv &s, uintptr_t st) { return s.check(P(st)); }, py::arg("stream") = 0)
+      .def("reset_y", [](DistSpmv &s, uintptr_t st) { s.reset_y(P(st)); }, py::arg("stream") = 0);
+  m.def("random_band_matrix", [](int64_t n, int64_t bw, int64_t nnz, uint64_t seed) {
+    CsrHost a = random_band_matrix(n, bw, nnz, seed);
+    return py::make_tuple(a.rowPtr, a.colInd, a.val);
+  });
+  m.def("row_partition", &row_partition);
+
+  // ------------------------------------------------------------------ raw kernels
+  auto k = m.def_submodule("kernels", "hand-written gfx950 kernels (raw device pointers)");
+  k.def("box_copy", [](uintptr_t grid, py::dict d, bool unpack, uintptr_t s) {
+    kern::box_copy(reinterpret_cast<double *>(grid), box_from_dict(d), unpack, P(s));
+  }, py::arg("grid"), py::arg("box"), py::arg("unpack"), py::arg("stream") = 0);
+  k.def("box_copy_many", [](uintptr_t grid, std::vector<py::dict> ds, bool unpack, uintptr_t s) {
+    std::vector<kern::BoxDesc> bs;
+    for (auto &d : ds) bs.push_back(box_from_dict(d));
+    kern::box_copy_many(reinterpret_cast<double *>(grid), bs.data(), int(bs.size()), unpack, P(s));
+  }, py::arg("grid"), py::arg("boxes"), py::arg("unpack"), py::arg("stream") = 0);
+  k.def("csr_spmv", [](int n, uintptr_t rp, uintptr_t ci, uintptr_t v, uintptr_t x, uintptr_t y, int lanes, bool acc, uintptr_t s) {
+    kern::csr_spmv(n, reinterpret_cast<const int32_t *>(rp), reinterpret_cast<const int32_t *>(ci),
+                   reinterpret_cast<const float *>(v), reinterpret_cast<const float *>(x),
+                   reinterpret_cast<float *>(y), lanes, acc, P(s));
+  }, py::arg("n_rows"), py::arg("row_ptr"), py::arg("col_ind"), py::arg("val"), py::arg("x"), py::arg("y"),
+     py::arg("lanes") = 0, py::arg("accumulate") = false, py::arg("stream") = 0);
+  k.def("gather_f32", [](int n, uintptr_t src, uintptr_t idx, uintptr_t dst, uintptr_t s) {
+    kern::gather_f32(n, reinterpret_cast<const float *>(src), reinterpret_cast<const int32_t *>(idx),
+                     reinterpret_cast<float *>(dst), P(s));
+  }, py::arg("n"), py::arg("src"), py::arg("idx"), py::arg("dst"), py::arg("stream") = 0);
+  k.def("vector_add_f32", [](int n, uintptr_t a, uintptr_t b, uintptr_t y, uintptr_t s) {
+    kern::vector_add_f32(n, reinterpret_cast<const float *>(a), reinterpret_cast<const float *>(b),
+                         reinterpret_cast<float *>(y), P(s));
+  }, py::arg("n"), py::arg("a"), py::arg("b"), py::arg("y"), py::arg("stream") = 0);
+  k.def("axpy_f64", [](int64_t n, double alpha, uintptr_t x, uintptr_t y, uintptr_t s) {
+    kern::axpy_f64(n, alpha, reinterpret_cast<const double *>(x), reinterpret_cast<double *>(y), P(s));
+  }, py::arg("n"), py::arg("alpha"), py::arg("x"), py::arg("y"), py::arg("stream") = 0);
+  k.def("iota_f64", [](int64_t n, double base, double scale, uintptr_t a, uintptr_t s) {
+    kern::iota_f64(n, base, scale, reinterpret_cast<double *>(a), P(s));
+  }, py::arg("n"), py::arg("base"), py::arg("scale"), py::arg("a"), py::arg("stream") = 0);
+  k.def("empty", [](uintptr_t s) { kern::empty(P(s)); }, py::arg("stream") = 0);
+  k.def("busy_wait", [](int64_t t, int b, uintptr_t s) { kern::busy_wait(t, b, P(s)); },
+        py::arg("ticks"), py::arg("blocks") = 1, py::arg("stream") = 0);
+}

@@ -1,0 +1,260 @@
+#include "benchmark.hpp"
+#include "util.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <fstream>
+#include <sstream>
+
+namespace tz {
+
+Json BenchResult::json() const {
+  Json j;
+  j["pct01"] = pct01;
+  j["pct10"] = pct10;
+  j["pct50"] = pct50;
+  j["pct90"] = pct90;
+  j["pct99"] = pct99;
+  j["stddev"] = stddev;
+  j["samples_per_measurement"] = samples_per_measurement;
+  j["retries"] = retries;
+  return j;
+}
+
+BenchResult BenchResult::from_times(std::vector<double> times) {
+  BenchResult r;
+  if (times.empty()) return r;
+  r.stddev = ::tz::stddev(times);
+  std::sort(times.begin(), times.end());
+  r.pct01 = percentile_sorted(times, 1);
+  r.pct10 = percentile_sorted(times, 10);
+  r.pct50 = percentile_sorted(times, 50);
+  r.pct90 = percentile_sorted(times, 90);
+  r.pct99 = percentile_sorted(times, 99);
+  return r;
+}
+
+Json BenchOpts::json() const {
+  Json j;
+  j["nIters"] = n_iters;
+  j["maxRetries"] = max_retries;
+  j["targetSecs"] = target_secs;
+  return j;
+}
+
+// ---------------------------------------------------------------- Empirical
+
+EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, double targetSecs) {
+  Measurement m{std::max<int64_t>(1, nHint), 0};
+  while (true) {
+    ctrl_.barrier();
+    const double t0 = wtime();
+    runner_.run(m.n);
+    double elapsed = wtime() - t0;
+    elapsed = ctrl_.allreduce_max(elapsed); // "true" time is the max over ranks
+    if (elapsed < targetSecs) {
+      const double perSample = std::max(elapsed / double(m.n), 1e-9);
+      const double est = targetSecs / perSample * 1.1;
+      m.n += int64_t(std::ceil((est - double(m.n)) * 0.5));
+      m.n = std::max<int64_t>(m.n, 1);
+    } else {
+      m.time = elapsed / double(m.n);
+      return m;
+    }
+  }
+}
+
+BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts &opts) {
+  runner_.prepare(seq);
+  std::vector<double> times;
+  int retries = 0;
+  int64_t hint = 1;
+  for (int left = opts.max_retries; opts.max_retries == 0 || left > 0; --left) {
+    Measurement m = measure(1, opts.target_secs); // warm-up and size the batch
+    hint = m.n;
+    times.clear();
+    for (int64_t i = 0; i < opts.n_iters; ++i) {
+      m = measure(hint, opts.target_secs);
+      hint = std::max(hint, m.n);
+      times.push_back(m.time);
+    }
+    // per-measurement times are already maxed across ranks inside measure()
+    if (compound_test(times, opts.small_sample) && left > 1) {
+      ++retries;
+      if (ctrl_.rank() == 0) TZ_LOG(Info, "failed randomness test (" << left - 1 << " left)");
+      continue;
+    }
+    break;
+  }
+  BenchResult r = BenchResult::from_times(times);
+  r.samples_per_measurement = hint;
+  r.retries = retries;
+  return r;
+}
+
+void HostExecutor::run(int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    for (const auto &e : seq_.entries) e.op->run(*this);
+}
+
+// ---------------------------------------------------------------- Sim
+
+SimExecutor::SimExecutor(int nStreams, SimParams p)
+    : n_(nStreams), p_(p), rng_(p.seed), streamFree_(nStreams, 0.0) {}
+
+double SimExecutor::dur(double us) {
+  if (p_.noise <= 0) return us;
+  std::normal_distribution<double> nd(1.0, p_.noise);
+  return std::max(0.0, us * nd(rng_));
+}
+
+void SimExecutor::launch(const GpuOp &op, int stream) {
+  TZ_CHECK(stream >= 0 && stream < n_, "sim stream out of range");
+  host_ += p_.launch_us;
+  const double start = std::max(host_, streamFree_[stream]);
+  int busy = 0;
+  for (int s = 0; s < n_; ++s)
+    if (s != stream && streamFree_[s] > start) ++busy;
+  const double d = dur(op.cost_us()) * (1.0 + p_.contention * busy);
+  streamFree_[stream] = start + d;
+  trace_.push_back({op.name(), stream, start, start + d});
+}
+
+void SimExecutor::event_record(int event, int stream) {
+  host_ += p_.api_us;
+  if (event >= int(events_.size())) events_.resize(event + 1, 0.0);
+  events_[event] = std::max(streamFree_[stream], host_);
+}
+
+void SimExecutor::stream_wait_event(int stream, int event) {
+  host_ += p_.api_us;
+  if (event < int(events_.size()))
+    streamFree_[stream] = std::max(streamFree_[stream], events_[event]);
+}
+
+void SimExecutor::event_sync(int event) {
+  if (event < int(events_.size()) && events_[event] > host_) host_ = events_[event] + p_.sync_us;
+  else host_ += p_.api_us;
+}
+
+void SimExecutor::stream_sync(int stream) {
+  if (streamFree_[stream] > host_) host_ = streamFree_[stream] + p_.sync_us;
+  else host_ += p_.api_us;
+}
+
+void SimExecutor::stream_wait(int waiter, int waitee) {
+  host_ += 2 * p_.api_us;
+  streamFree_[waiter] = std::max(streamFree_[waiter], streamFree_[waitee]);
+}
+
+void SimExecutor::device_sync() {
+  double m = host_;
+  for (double t : streamFree_) m = std::max(m, t);
+  host_ = m + p_.sync_us;
+}
+
+double SimExecutor::run_once(const Sequence &seq) {
+  host_ = 0;
+  std::fill(streamFree_.begin(), streamFree_.end(), 0.0);
+  events_.assign(events_.size(), 0.0);
+  trace_.clear();
+  for (const auto &e : seq.entries) e.op->run(*this);
+  // the sequence ends host-synchronized with all its GPU work (Finish has GPU preds synced)
+  double end = host_;
+  for (double t : streamFree_) end = std::max(end, t);
+  return end;
+}
+
+BenchResult SimBenchmarker::benchmark(const Sequence &seq, const BenchOpts &opts) {
+  SimParams p = p_;
+  p.seed = rng_();
+  SimExecutor ex(n_, p);
+  std::vector<double> times;
+  const int64_t n = std::max<int64_t>(1, std::min<int64_t>(opts.n_iters, 200));
+  for (int64_t i = 0; i < n; ++i) times.push_back(ex.run_once(seq) * 1e-6);
+  BenchResult r = BenchResult::from_times(times);
+  r.samples_per_measurement = 1;
+  return r;
+}
+
+// ---------------------------------------------------------------- CSV replay
+
+static std::vector<std::string> split_top(const std::string &line, char delim) {
+  // split on delim, but not inside JSON strings
+  std::vector<std::string> out;
+  std::string cur;
+  bool inStr = false, esc = false;
+  for (char c : line) {
+    if (inStr) {
+      cur.push_back(c);
+      if (esc) esc = false;
+      else if (c == '\\') esc = true;
+      else if (c == '"') inStr = false;
+      continue;
+    }
+    if (c == '"') inStr = true;
+    if (c == delim) {
+      out.push_back(cur);
+      cur.clear();
+    } else {
+      cur.push_back(c);
+    }
+  }
+  out.push_back(cur);
+  return out;
+}
+
+CsvBenchmarker::CsvBenchmarker(const std::string &path, const Graph &g) {
+  std::ifstream f(path);
+  TZ_CHECK(f, "cannot open " << path);
+  OpIndex idx(g);
+  std::string line;
+  while (std::getline(f, line)) {
+    if (line.empty() || line[0] == '{' || line[0] == '#') continue; // opts header / comments
+    auto cols = split_top(line, '|');
+    if (cols.size() < 7) continue;
+    BenchResult r;
+    try {
+      r.pct01 = std::stod(cols[1]);
+      r.pct10 = std::stod(cols[2]);
+      r.pct50 = std::stod(cols[3]);
+      r.pct90 = std::stod(cols[4]);
+      r.pct99 = std::stod(cols[5]);
+      r.stddev = std::stod(cols[6]);
+    } catch (...) {
+      continue; // header row
+    }
+    Sequence s;
+    for (size_t i = 7; i < cols.size(); ++i) s.push_back(idx.from_json(Json::parse(cols[i])));
+    data_.emplace(s.canonical_key(), r);
+  }
+}
+
+BenchResult CsvBenchmarker::benchmark(const Sequence &seq, const BenchOpts &) {
+  auto it = data_.find(seq.canonical_key());
+  if (it == data_.end()) TZ_THROW("no equivalent CSV data for sequence " << seq.desc());
+  return it->second;
+}
+
+BenchResult CachingBenchmarker::benchmark(const Sequence &seq, const BenchOpts &opts) {
+  const std::string k = seq.canonical_key();
+  auto it = cache_.find(k);
+  if (it != cache_.end()) {
+    ++hits_;
+    return it->second;
+  }
+  BenchResult r = inner_.benchmark(seq, opts);
+  cache_.emplace(k, r);
+  return r;
+}
+
+std::string csv_row(size_t i, const BenchResult &r, const Sequence &seq) {
+  std::ostringstream ss;
+  ss.precision(9);
+  ss << i << "|" << r.pct01 << "|" << r.pct10 << "|" << r.pct50 << "|" << r.pct90 << "|"
+     << r.pct99 << "|" << r.stddev;
+  for (const auto &e : seq.entries) ss << "|" << e.op->json().dump();
+  return ss.str();
+}
+
+} // namespace tz

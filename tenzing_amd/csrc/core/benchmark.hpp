@@ -1,0 +1,177 @@
+// Benchmarkers: turn a Sequence into a timing distribution.
+//
+// Parity: reference include/tenzing/benchmarker.hpp:14-30 (Result pct01..pct99/stddev, Opts
+// nIters/maxRetries), src/benchmarker.cpp:83-167 (EmpiricalBenchmarker: adaptive batching to a
+// target wall time, barrier, max over ranks, runs-test retries, percentiles) and :169-223
+// (CsvBenchmarker replay). Additions: SimBenchmarker (discrete-event model of streams, events and
+// the host thread; hardware-free solver tests and what-if searches), a HostExecutor for CPU-only
+// sequences, measurement caching by canonical schedule key.
+#pragma once
+
+#include "ctrl.hpp"
+#include "numeric.hpp"
+#include "serdes.hpp"
+#include "state.hpp"
+
+#include <map>
+#include <random>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace tz {
+
+struct BenchResult {
+  double pct01 = 0, pct10 = 0, pct50 = 0, pct90 = 0, pct99 = 0, stddev = 0;
+  int64_t samples_per_measurement = 0;
+  int retries = 0;
+  Json json() const;
+  static BenchResult from_times(std::vector<double> times);
+};
+
+struct BenchOpts {
+  int64_t n_iters = 1000;      // measurements per benchmark (reference Opts::nIters)
+  int max_retries = 10;        // runs-test retries (reference Opts::maxRetries)
+  double target_secs = 0.01;   // each measurement batches runs to at least this wall time
+  RunsTestSmall small_sample = RunsTestSmall::Accept;
+  Json json() const;
+};
+
+class Benchmarker {
+public:
+  virtual ~Benchmarker() = default;
+  virtual BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) = 0;
+};
+
+/// Runs sequences on an Executor (the HIP runtime, or HostExecutor) with host wall-clock timing,
+/// max across ranks of the control plane.
+class ExecutorRunner {
+public:
+  virtual ~ExecutorRunner() = default;
+  /// provision per-sequence resources (events, captured graphs)
+  virtual void prepare(const Sequence &seq) = 0;
+  /// run the prepared sequence `n` times back to back (host returns when all work is done)
+  virtual void run(int64_t n) = 0;
+};
+
+class EmpiricalBenchmarker : public Benchmarker {
+public:
+  EmpiricalBenchmarker(ExecutorRunner &runner, Ctrl &ctrl) : runner_(runner), ctrl_(ctrl) {}
+  BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) override;
+
+private:
+  struct Measurement {
+    int64_t n;
+    double time;
+  };
+  Measurement measure(int64_t nHint, double targetSecs);
+  ExecutorRunner &runner_;
+  Ctrl &ctrl_;
+};
+
+/// Host-only executor: GPU ops are launched with a null stream, synchronously (tests/CPU runs).
+class HostExecutor : public Executor, public ExecutorRunner {
+public:
+  explicit HostExecutor(int nStreams) : n_(nStreams) {}
+  int num_streams() const override { return n_; }
+  void launch(const GpuOp &op, int) override { op.launch(nullptr, *this); }
+  void event_record(int, int) override {}
+  void stream_wait_event(int, int) override {}
+  void event_sync(int) override {}
+  void stream_sync(int) override {}
+  void stream_wait(int, int) override {}
+  void device_sync() override {}
+  void prepare(const Sequence &seq) override { seq_ = seq; }
+  void run(int64_t n) override;
+
+private:
+  int n_;
+  Sequence seq_;
+};
+
+/// Discrete-event model: each stream executes its ops in order, a GPU op starts no earlier than
+/// the host issues it, events carry completion times, host syncs block the host clock.
+struct SimParams {
+  double launch_us = 4.0;   // host cost to issue a kernel / comm op
+  double api_us = 1.0;      // host cost of an event record / stream wait
+  double sync_us = 5.0;     // host wake-up latency after a blocking sync
+  double noise = 0.0;       // relative gaussian noise on each op duration
+  uint64_t seed = 0;
+  /// concurrent kernels share the device: when k GPU ops overlap, each runs at rate
+  /// 1/(1 + contention*(k-1)); 0 = perfect overlap
+  double contention = 0.0;
+};
+
+class SimExecutor : public Executor {
+public:
+  SimExecutor(int nStreams, SimParams p);
+  int num_streams() const override { return n_; }
+  void launch(const GpuOp &op, int stream) override;
+  void host_busy(double us) override { host_ += us; }
+  void event_record(int event, int stream) override;
+  void stream_wait_event(int stream, int event) override;
+  void event_sync(int event) override;
+  void stream_sync(int stream) override;
+  void stream_wait(int waiter, int waitee) override;
+  void device_sync() override;
+  /// simulated wall time (us) of one run of the sequence, starting from an idle machine
+  double run_once(const Sequence &seq);
+  /// trace of (op name, stream, start, end) of the last run
+  struct Span {
+    std::string name;
+    int stream;
+    double start, end;
+  };
+  const std::vector<Span> &trace() const { return trace_; }
+
+private:
+  double dur(double us);
+  int n_;
+  SimParams p_;
+  std::mt19937_64 rng_;
+  double host_ = 0;
+  std::vector<double> streamFree_;
+  std::vector<double> events_;
+  std::vector<Span> trace_;
+};
+
+class SimBenchmarker : public Benchmarker {
+public:
+  SimBenchmarker(int nStreams, SimParams p) : n_(nStreams), p_(p), rng_(p.seed + 17) {}
+  BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) override;
+
+private:
+  int n_;
+  SimParams p_;
+  std::mt19937_64 rng_;
+};
+
+/// Replays recorded timings from a results CSV (`i|p01|p10|p50|p90|p99|stddev|op-json|...`),
+/// matching sequences by equivalence (reference CsvBenchmarker, src/benchmarker.cpp:169-223).
+class CsvBenchmarker : public Benchmarker {
+public:
+  CsvBenchmarker(const std::string &path, const Graph &g);
+  BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) override;
+  size_t size() const { return data_.size(); }
+
+private:
+  std::unordered_map<std::string, BenchResult> data_;
+};
+
+/// Wraps another benchmarker and returns cached results for equivalent sequences.
+class CachingBenchmarker : public Benchmarker {
+public:
+  explicit CachingBenchmarker(Benchmarker &inner) : inner_(inner) {}
+  BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) override;
+  size_t hits() const { return hits_; }
+
+private:
+  Benchmarker &inner_;
+  std::unordered_map<std::string, BenchResult> cache_;
+  size_t hits_ = 0;
+};
+
+/// one row of the reference results CSV
+std::string csv_row(size_t i, const BenchResult &r, const Sequence &seq);
+
+} // namespace tz

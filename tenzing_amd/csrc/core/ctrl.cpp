@@ -1,0 +1,230 @@
+#include "ctrl.hpp"
+#include "util.hpp"
+
+#include <arpa/inet.h>
+#include <cerrno>
+#include <cstring>
+#include <fstream>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <thread>
+#include <unistd.h>
+
+namespace tz {
+
+int64_t Ctrl::bcast_int(int64_t v, int root) {
+  std::string s(reinterpret_cast<const char *>(&v), sizeof(v));
+  bcast(s, root);
+  std::memcpy(&v, s.data(), sizeof(v));
+  return v;
+}
+
+namespace {
+void send_all(int fd, const void *buf, size_t n) {
+  const char *p = static_cast<const char *>(buf);
+  while (n) {
+    ssize_t w = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      TZ_THROW("ctrl send failed: " << std::strerror(errno));
+    }
+    p += w;
+    n -= size_t(w);
+  }
+}
+void recv_all(int fd, void *buf, size_t n) {
+  char *p = static_cast<char *>(buf);
+  while (n) {
+    ssize_t r = ::recv(fd, p, n, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      TZ_THROW("ctrl recv failed: " << std::strerror(errno));
+    }
+    if (r == 0) TZ_THROW("ctrl peer closed connection");
+    p += r;
+    n -= size_t(r);
+  }
+}
+void send_frame(int fd, const std::string &s) {
+  uint64_t n = s.size();
+  send_all(fd, &n, sizeof(n));
+  if (n) send_all(fd, s.data(), n);
+}
+std::string recv_frame(int fd) {
+  uint64_t n = 0;
+  recv_all(fd, &n, sizeof(n));
+  std::string s(n, '\0');
+  if (n) recv_all(fd, &s[0], n);
+  return s;
+}
+void nodelay(int fd) {
+  int one = 1;
+  ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+}
+} // namespace
+
+TcpCtrl::TcpCtrl(int rank, int size) : rank_(rank), size_(size), peers_(size, -1) {
+  TZ_CHECK(size >= 1 && rank >= 0 && rank < size, "bad rank/size " << rank << "/" << size);
+}
+
+TcpCtrl::~TcpCtrl() {
+  for (int fd : peers_)
+    if (fd >= 0) ::close(fd);
+  if (listenFd_ >= 0) ::close(listenFd_);
+}
+
+int TcpCtrl::listen(int port, const std::string &bindAddr) {
+  TZ_CHECK(rank_ == 0, "only rank 0 listens");
+  listenFd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+  TZ_CHECK(listenFd_ >= 0, "socket: " << std::strerror(errno));
+  int one = 1;
+  ::setsockopt(listenFd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons(uint16_t(port));
+  TZ_CHECK(::inet_pton(AF_INET, bindAddr.c_str(), &addr.sin_addr) == 1, "bad bind addr");
+  TZ_CHECK(::bind(listenFd_, reinterpret_cast<sockaddr *>(&addr), sizeof(addr)) == 0,
+           "bind: " << std::strerror(errno));
+  TZ_CHECK(::listen(listenFd_, 256) == 0, "listen: " << std::strerror(errno));
+  socklen_t len = sizeof(addr);
+  ::getsockname(listenFd_, reinterpret_cast<sockaddr *>(&addr), &len);
+  return ntohs(addr.sin_port);
+}
+
+void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
+  if (size_ == 1) return;
+  if (rank_ == 0) {
+    TZ_CHECK(listenFd_ >= 0, "rank 0 must listen() before connect()");
+    for (int i = 1; i < size_; ++i) {
+      int fd = ::accept(listenFd_, nullptr, nullptr);
+      TZ_CHECK(fd >= 0, "accept: " << std::strerror(errno));
+      nodelay(fd);
+      int32_t r = -1;
+      recv_all(fd, &r, sizeof(r));
+      TZ_CHECK(r > 0 && r < size_ && peers_[r] < 0, "bad or duplicate peer rank " << r);
+      peers_[r] = fd;
+    }
+    // release everyone
+    for (int i = 1; i < size_; ++i) {
+      char c = 1;
+      send_all(peers_[i], &c, 1);
+    }
+    return;
+  }
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  const std::string ps = std::to_string(port);
+  TZ_CHECK(::getaddrinfo(host.c_str(), ps.c_str(), &hints, &res) == 0, "getaddrinfo " << host);
+  const double t0 = wtime();
+  int fd = -1;
+  while (true) {
+    fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+    ::close(fd);
+    fd = -1;
+    if (wtime() - t0 > timeoutS) {
+      ::freeaddrinfo(res);
+      TZ_THROW("ctrl connect to " << host << ":" << port << " timed out");
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+  ::freeaddrinfo(res);
+  nodelay(fd);
+  int32_t r = rank_;
+  send_all(fd, &r, sizeof(r));
+  char c = 0;
+  recv_all(fd, &c, 1);
+  peers_[0] = fd;
+}
+
+void TcpCtrl::rendezvous_file(const std::string &path, const std::string &host, double timeoutS) {
+  if (rank_ == 0) {
+    int port = listen(0);
+    const std::string tmp = path + ".tmp";
+    {
+      std::ofstream f(tmp);
+      f << port << "\n";
+    }
+    ::rename(tmp.c_str(), path.c_str());
+    connect(host, port, timeoutS);
+  } else {
+    const double t0 = wtime();
+    int port = 0;
+    while (true) {
+      std::ifstream f(path);
+      if (f && (f >> port) && port > 0) break;
+      TZ_CHECK(wtime() - t0 < timeoutS, "rendezvous file " << path << " never appeared");
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+    connect(host, port, timeoutS);
+  }
+}
+
+void TcpCtrl::barrier() {
+  if (size_ == 1) return;
+  char c = 0;
+  if (rank_ == 0) {
+    for (int i = 1; i < size_; ++i) recv_all(peers_[i], &c, 1);
+    for (int i = 1; i < size_; ++i) send_all(peers_[i], &c, 1);
+  } else {
+    send_all(peers_[0], &c, 1);
+    recv_all(peers_[0], &c, 1);
+  }
+}
+
+void TcpCtrl::bcast(std::string &data, int root) {
+  if (size_ == 1) return;
+  if (root != 0) {
+    if (rank_ == root) send_frame(peers_[0], data);
+    else if (rank_ == 0) data = recv_frame(peers_[root]);
+  }
+  if (rank_ == 0) {
+    for (int i = 1; i < size_; ++i)
+      if (i != root) send_frame(peers_[i], data);
+  } else if (rank_ != root) {
+    data = recv_frame(peers_[0]);
+  }
+}
+
+void TcpCtrl::allreduce(double *v, size_t n, bool isMax) {
+  if (size_ == 1) return;
+  std::string buf(reinterpret_cast<const char *>(v), n * sizeof(double));
+  if (rank_ == 0) {
+    std::vector<double> tmp(n);
+    for (int i = 1; i < size_; ++i) {
+      std::string f = recv_frame(peers_[i]);
+      TZ_CHECK(f.size() == n * sizeof(double), "allreduce size mismatch");
+      std::memcpy(tmp.data(), f.data(), f.size());
+      for (size_t k = 0; k < n; ++k) v[k] = isMax ? std::max(v[k], tmp[k]) : v[k] + tmp[k];
+    }
+    std::string out(reinterpret_cast<const char *>(v), n * sizeof(double));
+    for (int i = 1; i < size_; ++i) send_frame(peers_[i], out);
+  } else {
+    send_frame(peers_[0], buf);
+    std::string f = recv_frame(peers_[0]);
+    std::memcpy(v, f.data(), n * sizeof(double));
+  }
+}
+
+void TcpCtrl::allreduce_max(double *v, size_t n) { allreduce(v, n, true); }
+void TcpCtrl::allreduce_sum(double *v, size_t n) { allreduce(v, n, false); }
+
+std::vector<std::string> TcpCtrl::allgather(const std::string &mine) {
+  std::vector<std::string> all(size_);
+  all[rank_] = mine;
+  if (size_ == 1) return all;
+  if (rank_ == 0) {
+    for (int i = 1; i < size_; ++i) all[i] = recv_frame(peers_[i]);
+    for (int i = 1; i < size_; ++i)
+      for (int k = 0; k < size_; ++k) send_frame(peers_[i], all[k]);
+  } else {
+    send_frame(peers_[0], mine);
+    for (int k = 0; k < size_; ++k) all[k] = recv_frame(peers_[0]);
+  }
+  return all;
+}
+
+} // namespace tz

@@ -1,0 +1,78 @@
+// Host control plane: the tiny, latency-bound collectives the search needs (stop flags,
+// schedule broadcast, barrier, max-reduction of timings).
+//
+// Parity: the reference uses MPI for these (MPI_Bcast of the schedule JSON, src/sequence.cpp:
+// 88-125; MPI_Barrier/MPI_Allreduce(MAX) in src/benchmarker.cpp:45-145; Stop-flag MPI_Bcast in
+// tenzing-mcts mcts.hpp:149-150 and tenzing-dfs dfs.hpp:67-68). There is no MPI on the MI355X
+// image and the GPU data plane is RCCL, so the control plane is a native TCP star (rank 0 hub,
+// TCP_NODELAY, length-prefixed frames) bootstrapped from the launcher's rendezvous. It is not
+// on the device path: candidate schedules move their payloads over RCCL/xGMI.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace tz {
+
+class Ctrl {
+public:
+  virtual ~Ctrl() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual void barrier() = 0;
+  virtual void bcast(std::string &data, int root) = 0;
+  virtual void allreduce_max(double *v, size_t n) = 0;
+  virtual void allreduce_sum(double *v, size_t n) = 0;
+  /// every rank gets every rank's string
+  virtual std::vector<std::string> allgather(const std::string &mine) = 0;
+
+  double allreduce_max(double v) {
+    allreduce_max(&v, 1);
+    return v;
+  }
+  int64_t bcast_int(int64_t v, int root);
+};
+
+class SelfCtrl : public Ctrl {
+public:
+  int rank() const override { return 0; }
+  int size() const override { return 1; }
+  void barrier() override {}
+  void bcast(std::string &, int) override {}
+  void allreduce_max(double *, size_t) override {}
+  void allreduce_sum(double *, size_t) override {}
+  std::vector<std::string> allgather(const std::string &mine) override { return {mine}; }
+};
+
+class TcpCtrl : public Ctrl {
+public:
+  TcpCtrl(int rank, int size);
+  ~TcpCtrl() override;
+  TcpCtrl(const TcpCtrl &) = delete;
+  TcpCtrl &operator=(const TcpCtrl &) = delete;
+
+  /// rank 0 only: bind and listen (port 0 = ephemeral); returns the bound port
+  int listen(int port = 0, const std::string &bindAddr = "0.0.0.0");
+  /// rank 0: accept size-1 peers; others: connect (retrying until timeout)
+  void connect(const std::string &host, int port, double timeoutS = 300.0);
+  /// rank 0 writes its port to `path`; others poll the file (CLI bootstrap without Python)
+  void rendezvous_file(const std::string &path, const std::string &host, double timeoutS = 300.0);
+
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  void barrier() override;
+  void bcast(std::string &data, int root) override;
+  void allreduce_max(double *v, size_t n) override;
+  void allreduce_sum(double *v, size_t n) override;
+  std::vector<std::string> allgather(const std::string &mine) override;
+  using Ctrl::allreduce_max;
+
+private:
+  void allreduce(double *v, size_t n, bool isMax);
+  int rank_, size_;
+  int listenFd_ = -1;
+  std::vector<int> peers_; // rank 0: fd per rank (index 0 unused); others: peers_[0] = root
+};
+
+} // namespace tz

@@ -1,0 +1,757 @@
+#include "solve.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <csignal>
+#include <fstream>
+#include <iostream>
+#include <limits>
+#include <map>
+#include <sstream>
+#include <unordered_map>
+#include <unordered_set>
+
+#ifndef TZ_VERSION_MAJOR
+#define TZ_VERSION_MAJOR 0
+#define TZ_VERSION_MINOR 1
+#define TZ_VERSION_PATCH 0
+#endif
+#ifndef TZ_GIT_HASH
+#define TZ_GIT_HASH "unknown"
+#endif
+
+namespace tz {
+
+static constexpr double kInf = std::numeric_limits<double>::infinity();
+
+// ======================================================================== results
+
+int SearchResult::best() const {
+  int b = -1;
+  for (size_t i = 0; i < sims.size(); ++i)
+    if (b < 0 || sims[i].res.pct10 < sims[b].res.pct10) b = int(i);
+  return b;
+}
+
+void SearchResult::dump_csv(std::ostream &os) const {
+  os << opts.dump() << "\n";
+  for (size_t i = 0; i < sims.size(); ++i) os << csv_row(i, sims[i].res, sims[i].seq) << "\n";
+}
+
+void SearchResult::dump_jsonl(std::ostream &os) const {
+  for (size_t i = 0; i < sims.size(); ++i) {
+    Json j;
+    j["i"] = int64_t(i);
+    j["result"] = sims[i].res.json();
+    j["cached"] = sims[i].cached;
+    j["seq"] = sims[i].seq.json();
+    os << j.dump() << "\n";
+  }
+}
+
+// ======================================================================== MCTS nodes
+
+size_t MctsNode::size() const {
+  size_t s = 1;
+  for (const auto &c : children) s += c->size();
+  return s;
+}
+size_t MctsNode::fully_visited_size() const {
+  size_t s = fully_visited ? 1 : 0;
+  for (const auto &c : children) s += c->fully_visited_size();
+  return s;
+}
+size_t MctsNode::unvisited_size() const {
+  size_t s = n == 0 ? 1 : 0;
+  for (const auto &c : children) s += c->unvisited_size();
+  return s;
+}
+bool MctsNode::is_leaf() const {
+  if (children.empty()) return true;
+  for (const auto &c : children)
+    if (c->n == 0) return true;
+  return false;
+}
+
+// ======================================================================== strategies
+
+std::string Strategy::label(const MctsNode &node) const {
+  std::ostringstream ss;
+  ss.precision(3);
+  ss << std::scientific;
+  if (std::isfinite(node.tmin)) ss << node.tmin << " - " << node.tmax;
+  else if (!node.times.empty()) ss << node.times.front() << " - " << node.times.back();
+  return ss.str();
+}
+
+namespace {
+
+double clamp01(double v) {
+  if (std::isnan(v)) return 0;
+  return v < 0 ? 0 : (v > 1 ? 1 : v);
+}
+
+void push_sorted(std::vector<double> &v, double x) { v.insert(std::upper_bound(v.begin(), v.end(), x), x); }
+
+std::vector<uint64_t> histogram(const std::vector<double> &v, double tMin, double tMax, int nBins) {
+  std::vector<uint64_t> h(nBins, 0);
+  for (double e : v) {
+    long i = tMax > tMin ? long((e - tMin) / (tMax - tMin) * nBins) : 0;
+    if (i < 0) i = 0;
+    if (i >= nBins) i = nBins - 1;
+    ++h[i];
+  }
+  return h;
+}
+
+// reference mcts_strategy_fast_min.hpp:40-65
+struct FastMin : Strategy {
+  std::string name() const override { return "FastMin"; }
+  double select(const MctsNode &child) override {
+    const MctsNode &root = child.root();
+    if (&child == &root) return 1;
+    if (root.n < 2 || root.tmax == root.tmin) return 1;
+    if (child.n < 1) return select(*child.parent);
+    return clamp01(1 - (child.tmin - root.tmin) / (root.tmax - root.tmin));
+  }
+  void backprop(MctsNode &node, const BenchResult &br) override {
+    node.tmin = std::min(node.tmin, br.pct10);
+    node.tmax = std::max(node.tmax, br.pct10);
+  }
+};
+
+// reference mcts_strategy_coverage.hpp:39-101
+struct Coverage : Strategy {
+  std::string name() const override { return "Coverage"; }
+  double select(const MctsNode &child) override {
+    const MctsNode &parent = *child.parent;
+    const auto &pt = parent.times, &ct = child.times;
+    if (pt.size() < 2 || ct.empty()) return 1;
+    const double pMin = pt.front(), pMax = pt.back();
+    if (pMin == pMax) return 1;
+    if (ct.size() < 2) return clamp01(std::max(ct[0] - pMin, pMax - ct[0]) / (pMax - pMin));
+    return clamp01((ct.back() - ct.front()) / (pMax - pMin));
+  }
+  void backprop(MctsNode &node, const BenchResult &br) override {
+    push_sorted(node.times, br.pct10);
+    node.tmin = node.times.front();
+    node.tmax = node.times.back();
+  }
+};
+
+// reference mcts_strategy_random.hpp:31-54
+struct RandomS : Strategy {
+  std::mt19937_64 rng;
+  std::unordered_map<const MctsNode *, size_t> selected;
+  explicit RandomS(uint64_t seed) : rng(seed) {}
+  std::string name() const override { return "Random"; }
+  double select(const MctsNode &child) override {
+    const MctsNode &parent = *child.parent;
+    auto it = selected.find(&parent);
+    if (it == selected.end()) {
+      std::uniform_int_distribution<size_t> u(0, parent.children.size() - 1);
+      it = selected.emplace(&parent, u(rng)).first;
+    }
+    return parent.children[it->second].get() == &child ? kInf : 0;
+  }
+  void backprop(MctsNode &node, const BenchResult &br) override {
+    node.times.push_back(br.pct10);
+    if (!node.parent) selected.clear();
+  }
+};
+
+// reference mcts_strategy_avg_time.hpp:33-58
+struct AvgTime : Strategy {
+  std::string name() const override { return "AvgTime"; }
+  double select(const MctsNode &child) override {
+    const MctsNode &root = child.root();
+    if (child.n < 1 || root.n < 2 || root.tmax == root.tmin) return 0;
+    double acc = 0;
+    for (double t : child.times) acc += clamp01(1 - (t - root.tmin) / (root.tmax - root.tmin));
+    return acc / double(child.times.size());
+  }
+  void backprop(MctsNode &node, const BenchResult &br) override {
+    node.tmin = std::min(node.tmin, br.pct10);
+    node.tmax = std::max(node.tmax, br.pct10);
+    node.times.push_back(br.pct10);
+  }
+};
+
+// reference mcts_strategy_unvisited.hpp:26-36
+struct Unvisited : Strategy {
+  std::string name() const override { return "Unvisited"; }
+  double select(const MctsNode &child) override { return child.times.empty() ? kInf : 0; }
+  void backprop(MctsNode &node, const BenchResult &br) override { node.times.push_back(br.pct10); }
+};
+
+constexpr int kBins = 10;
+
+// reference mcts_strategy_anti_corr.hpp:25-88
+struct AntiCorrelation : Strategy {
+  std::string name() const override { return "AntiCorrelation"; }
+  double select(const MctsNode &child) override {
+    const MctsNode &parent = *child.parent;
+    if (parent.times.size() < 2 || child.times.size() < 2) return 0;
+    const double tMin = std::min(parent.times.front(), child.times.front());
+    const double tMax = std::max(parent.times.back(), child.times.back());
+    double v = corr(histogram(parent.times, tMin, tMax, kBins), histogram(child.times, tMin, tMax, kBins));
+    return clamp01((2 - (v + 1)) / 2);
+  }
+  void backprop(MctsNode &node, const BenchResult &br) override { push_sorted(node.times, br.pct10); }
+};
+
+// reference mcts_strategy_norm_anti_corr.hpp:45-110 (correlation against the root histogram,
+// normalized by the best sibling). `anti` selects anti-correlation vs correlation
+// (NormRootCorr, mcts_strategy_norm_root_corr.hpp:46-110).
+struct NormCorr : Strategy {
+  bool anti;
+  explicit NormCorr(bool a) : anti(a) {}
+  std::string name() const override { return anti ? "NormalizedAntiCorrelation" : "NormRootCorr"; }
+  double score(const std::vector<uint64_t> &rh, const std::vector<double> &times, double tMin, double tMax) const {
+    double c = corr(rh, histogram(times, tMin, tMax, kBins)) + 1; // [0,2]
+    return anti ? 2 - c : c;
+  }
+  double select(const MctsNode &child) override {
+    const MctsNode &parent = *child.parent;
+    const MctsNode &root = child.root();
+    if (parent.times.size() < 2 || child.times.size() < 2 || root.times.empty()) return 0;
+    const double tMin = root.times.front(), tMax = root.times.back();
+    auto rh = histogram(root.times, tMin, tMax, kBins);
+    double best = -1;
+    for (const auto &sib : parent.children) best = std::max(best, score(rh, sib->times, tMin, tMax));
+    if (best <= 0) return 0;
+    return clamp01(score(rh, child.times, tMin, tMax) / best);
+  }
+  void backprop(MctsNode &node, const BenchResult &br) override { push_sorted(node.times, br.pct10); }
+};
+
+// reference mcts_strategy_balance_hist.hpp:49-190 (active #if 1 branch)
+struct BalanceHistogram : Strategy {
+  std::string name() const override { return "BalanceHistogram"; }
+  double select(const MctsNode &child) override {
+    const MctsNode &parent = *child.parent;
+    const MctsNode &root = child.root();
+    if (parent.times.empty() || child.times.empty() || root.times.empty()) return 0;
+    const double tMin = root.times.front(), tMax = root.times.back();
+    auto rh = histogram(root.times, tMin, tMax, kBins);
+    auto ch = histogram(child.times, tMin, tMax, kBins);
+    long smallest = -1, largest = -1;
+    uint64_t cnt = std::numeric_limits<uint64_t>::max();
+    for (int i = 0; i < kBins; ++i)
+      if (rh[i] > 0 && rh[i] < cnt && ch[i] > 0) {
+        smallest = i;
+        cnt = rh[i];
+      }
+    int64_t lc = -1;
+    for (int i = 0; i < kBins; ++i)
+      if (rh[i] > 0 && int64_t(rh[i]) > lc) {
+        largest = i;
+        lc = int64_t(rh[i]);
+      }
+    if (smallest < 0 || largest < 0) return 0;
+    return clamp01(1.0 - double(rh[smallest]) / double(rh[largest]));
+  }
+  void backprop(MctsNode &node, const BenchResult &br) override { push_sorted(node.times, br.pct10); }
+};
+
+} // namespace
+
+std::vector<std::string> strategy_names() {
+  return {"FastMin", "Coverage", "Random", "AvgTime", "Unvisited", "AntiCorrelation",
+          "NormalizedAntiCorrelation", "NormRootCorr", "BalanceHistogram"};
+}
+
+std::unique_ptr<Strategy> make_strategy(const std::string &name, uint64_t seed) {
+  std::string n = name;
+  std::transform(n.begin(), n.end(), n.begin(), ::tolower);
+  n.erase(std::remove(n.begin(), n.end(), '_'), n.end());
+  if (n == "fastmin" || n == "mintime") return std::make_unique<FastMin>();
+  if (n == "coverage") return std::make_unique<Coverage>();
+  if (n == "random") return std::make_unique<RandomS>(seed);
+  if (n == "avgtime") return std::make_unique<AvgTime>();
+  if (n == "unvisited") return std::make_unique<Unvisited>();
+  if (n == "anticorrelation" || n == "anticorr") return std::make_unique<AntiCorrelation>();
+  if (n == "normalizedanticorrelation" || n == "normanticorr") return std::make_unique<NormCorr>(true);
+  if (n == "normrootcorr") return std::make_unique<NormCorr>(false);
+  if (n == "balancehistogram" || n == "balancehist") return std::make_unique<BalanceHistogram>();
+  TZ_THROW("unknown MCTS strategy '" << name << "'");
+}
+
+// ======================================================================== MCTS
+
+Json MctsOpts::json() const {
+  Json j, o;
+  o["nIters"] = n_iters;
+  o["timeBudgetS"] = time_budget_s;
+  o["expandRollout"] = expand_rollout;
+  o["removeRedundantSyncs"] = remove_redundant_syncs;
+  o["reuseMeasurements"] = reuse_measurements;
+  o["strategy"] = strategy;
+  o["seed"] = int64_t(seed);
+  o["exploreC"] = explore_c;
+  o["benchOpts"] = bench.json();
+  j["mcts__Opts"] = o;
+  return j;
+}
+
+namespace {
+
+struct Tree {
+  MctsNode root;
+  std::unique_ptr<Strategy> strat;
+  std::mt19937_64 rng;
+  double c;
+
+  void ensure_children(MctsNode &node, const State &st) {
+    if (node.expanded) return;
+    node.expanded = true;
+    node.terminal = st.complete();
+    for (auto &d : st.get_decisions()) {
+      auto ch = std::make_unique<MctsNode>();
+      ch->parent = &node;
+      ch->decision = d;
+      node.children.push_back(std::move(ch));
+    }
+  }
+
+  MctsNode *pick_uct(MctsNode &node) {
+    std::vector<double> ucts;
+    ucts.reserve(node.children.size());
+    double m = -kInf;
+    for (auto &ch : node.children) {
+      double u;
+      if (ch->fully_visited) {
+        u = -kInf;
+      } else {
+        const double exploit = strat->select(*ch);
+        const double explore = c * std::sqrt(std::log(double(node.n)) / double(ch->n));
+        u = exploit + explore;
+        if (std::isnan(u)) u = exploit;
+      }
+      ucts.push_back(u);
+      m = std::max(m, u);
+    }
+    std::vector<size_t> best;
+    for (size_t i = 0; i < ucts.size(); ++i)
+      if (ucts[i] == m) best.push_back(i);
+    std::uniform_int_distribution<size_t> u(0, best.size() - 1);
+    return node.children[best[u(rng)]].get();
+  }
+
+  void backprop(MctsNode *node, const BenchResult &br) {
+    for (; node; node = node->parent) {
+      ++node->n;
+      if (node->children.empty()) {
+        if (node->expanded) node->fully_visited = true;
+      } else {
+        bool all = true;
+        for (auto &ch : node->children) all = all && ch->fully_visited;
+        if (all) node->fully_visited = true;
+      }
+      strat->backprop(*node, br);
+    }
+  }
+
+  Json save(const MctsNode &node) const {
+    Json j;
+    j["n"] = int64_t(node.n);
+    if (std::isfinite(node.tmin)) j["tmin"] = node.tmin;
+    if (std::isfinite(node.tmax)) j["tmax"] = node.tmax;
+    if (!node.times.empty()) {
+      Json t = Json::array();
+      for (double x : node.times) t.push_back(x);
+      j["times"] = t;
+    }
+    j["fv"] = node.fully_visited;
+    if (node.expanded) {
+      Json cs = Json::array();
+      for (auto &ch : node.children) cs.push_back(ch->n ? save(*ch) : Json());
+      j["c"] = cs;
+    }
+    return j;
+  }
+
+  void load(MctsNode &node, const Json &j, const State &st) {
+    if (j.is_null()) return;
+    node.n = size_t(j.at("n").as_int());
+    if (j.contains("tmin")) node.tmin = j.at("tmin").as_double();
+    if (j.contains("tmax")) node.tmax = j.at("tmax").as_double();
+    if (j.contains("times"))
+      for (auto &x : j.at("times").as_array()) node.times.push_back(x.as_double());
+    node.fully_visited = j.at("fv").as_bool();
+    if (j.contains("c")) {
+      ensure_children(node, st);
+      const auto &cs = j.at("c").as_array();
+      TZ_CHECK(cs.size() == node.children.size(), "checkpoint does not match this graph");
+      for (size_t i = 0; i < cs.size(); ++i) {
+        if (cs[i].is_null()) continue;
+        load(*node.children[i], cs[i], st.apply(node.children[i]->decision));
+      }
+    }
+  }
+};
+
+void graphviz_rec(const MctsNode &node, const Strategy &strat, std::ostream &os, size_t &count,
+                  size_t maxNodes, const std::string &id) {
+  std::string color = node.fully_visited ? "green" : "black";
+  os << "  " << id << " [label=\"" << node.decision.desc() << "\\nn=" << node.n << "\\n"
+     << strat.label(node) << "\", color=" << color << "];\n";
+  ++count;
+  size_t i = 0;
+  for (const auto &ch : node.children) {
+    ++i;
+    if (count >= maxNodes) break;
+    // hide unvisited, fully-visited and single-rollout subtrees (reference mcts.hpp:60-100)
+    if (ch->n == 0) continue;
+    const std::string cid = id + "_" + std::to_string(i);
+    if (ch->fully_visited || ch->n == 1) {
+      os << "  " << cid << " [label=\"" << ch->decision.desc() << "\\nn=" << ch->n
+         << "\", color=" << (ch->fully_visited ? "green" : "gray") << "];\n";
+      ++count;
+    } else {
+      graphviz_rec(*ch, strat, os, count, maxNodes, cid);
+    }
+    os << "  " << id << " -> " << cid << ";\n";
+  }
+}
+
+void write_file(const std::string &path, const std::string &s) {
+  std::ofstream f(path);
+  f << s;
+}
+
+} // namespace
+
+std::string mcts_tree_graphviz(const MctsNode &root, const Strategy &strat, size_t maxNodes) {
+  std::ostringstream os;
+  os << "digraph MCTS {\n";
+  size_t count = 0;
+  graphviz_rec(root, strat, os, count, maxNodes, "n");
+  os << "}\n";
+  return os.str();
+}
+
+SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &bench, Ctrl &ctrl,
+                          const MctsOpts &opts,
+                          const std::function<void(size_t, const SimResult &)> &onResult) {
+  const bool root = ctrl.rank() == 0;
+  const double t0 = wtime();
+  SearchResult result;
+  result.opts = opts.json();
+
+  auto gp = std::make_shared<Graph>(g);
+  gp->normalize();
+  State rootState(gp, plat);
+  OpIndex index(*gp);
+
+  Tree tree;
+  tree.strat = make_strategy(opts.strategy, opts.seed + 1);
+  tree.rng.seed(opts.seed);
+  tree.c = opts.explore_c;
+  std::unordered_map<std::string, size_t> cache; // canonical key -> sims index
+
+  if (root && !opts.resume_path.empty()) {
+    std::ifstream f(opts.resume_path);
+    TZ_CHECK(f, "cannot open checkpoint " << opts.resume_path);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    Json ck = Json::parse(ss.str());
+    tree.load(tree.root, ck.at("tree"), rootState);
+    for (const auto &s : ck.at("sims").as_array()) {
+      SimResult sr;
+      sr.seq = index.sequence_from_json(s.at("seq"));
+      const Json &r = s.at("result");
+      sr.res.pct01 = r.at("pct01").as_double();
+      sr.res.pct10 = r.at("pct10").as_double();
+      sr.res.pct50 = r.at("pct50").as_double();
+      sr.res.pct90 = r.at("pct90").as_double();
+      sr.res.pct99 = r.at("pct99").as_double();
+      sr.res.stddev = r.at("stddev").as_double();
+      cache.emplace(sr.seq.canonical_key(), result.sims.size());
+      result.sims.push_back(sr);
+    }
+    TZ_LOG(Info, "resumed MCTS: tree size " << tree.root.size() << ", " << result.sims.size()
+                                            << " results");
+  }
+
+  std::function<void(int)> dump = [&result](int) { result.dump_csv(std::cout); };
+  if (root && opts.trap_signals) register_handler(dump);
+
+  auto checkpoint = [&]() {
+    if (!root || opts.checkpoint_path.empty()) return;
+    Json ck;
+    ck["tree"] = tree.save(tree.root);
+    Json sims = Json::array();
+    for (const auto &s : result.sims) {
+      Json j;
+      j["result"] = s.res.json();
+      j["seq"] = s.seq.json();
+      sims.push_back(j);
+    }
+    ck["sims"] = sims;
+    ck["opts"] = opts.json();
+    write_file(opts.checkpoint_path + ".tmp", ck.dump());
+    std::rename((opts.checkpoint_path + ".tmp").c_str(), opts.checkpoint_path.c_str());
+  };
+
+  Counters &C = result.counters;
+  for (int64_t iter = 0;; ++iter) {
+    int64_t stop = 0;
+    if (root) {
+      if (tree.root.fully_visited) {
+        stop = 1;
+        result.stop_reason = "full_tree";
+      } else if (opts.n_iters > 0 && iter >= opts.n_iters) {
+        stop = 2;
+        result.stop_reason = "iterations";
+      } else if (opts.time_budget_s > 0 && wtime() - t0 > opts.time_budget_s) {
+        stop = 3;
+        result.stop_reason = "time_budget";
+      }
+    }
+    stop = ctrl.bcast_int(stop, 0);
+    if (stop) break;
+
+    std::string msg;
+    MctsNode *bpStart = nullptr;
+    size_t cachedIdx = size_t(-1);
+    Sequence seq;
+    if (root) {
+      State st = rootState;
+      MctsNode *node = &tree.root;
+      {
+        ScopedTimer t(C, "SELECT");
+        while (!node->is_leaf() && !node->terminal) {
+          node = tree.pick_uct(*node);
+          st.apply_inplace(node->decision);
+        }
+      }
+      {
+        ScopedTimer t(C, "EXPAND");
+        tree.ensure_children(*node, st);
+        if (!node->children.empty()) {
+          MctsNode *next = nullptr;
+          for (auto &ch : node->children)
+            if (ch->n == 0) {
+              next = ch.get();
+              break;
+            }
+          if (!next) next = tree.pick_uct(*node);
+          node = next;
+          st.apply_inplace(node->decision);
+        }
+      }
+      {
+        ScopedTimer t(C, "ROLLOUT");
+        bpStart = node;
+        MctsNode *cur = node;
+        std::uniform_int_distribution<size_t> u;
+        while (!st.complete()) {
+          if (opts.expand_rollout) {
+            tree.ensure_children(*cur, st);
+            TZ_CHECK(!cur->children.empty(), "dead-end state during rollout");
+            u = std::uniform_int_distribution<size_t>(0, cur->children.size() - 1);
+            cur = cur->children[u(tree.rng)].get();
+            st.apply_inplace(cur->decision);
+            bpStart = cur;
+          } else {
+            auto ds = st.get_decisions();
+            TZ_CHECK(!ds.empty(), "dead-end state during rollout");
+            u = std::uniform_int_distribution<size_t>(0, ds.size() - 1);
+            st.apply_inplace(ds[u(tree.rng)]);
+          }
+        }
+        if (opts.expand_rollout) tree.ensure_children(*cur, st);
+      }
+      seq = st.sequence();
+      if (opts.remove_redundant_syncs) {
+        ScopedTimer t(C, "REDUNDANT_SYNC");
+        remove_redundant_syncs(seq, st.graph(), plat.n_streams);
+      }
+      if (opts.verify) {
+        ScopedTimer t(C, "VERIFY");
+        auto v = verify(seq, st.graph(), plat.n_streams);
+        if (!v.empty()) TZ_THROW("candidate schedule has a race: " << v[0].desc());
+      }
+      if (opts.reuse_measurements) {
+        auto it = cache.find(seq.canonical_key());
+        if (it != cache.end()) cachedIdx = it->second;
+      }
+      Json m;
+      m["cached"] = cachedIdx != size_t(-1);
+      m["seq"] = seq.json(true);
+      msg = m.dump();
+    }
+    {
+      ScopedTimer t(C, "BCAST");
+      ctrl.bcast(msg, 0);
+    }
+    Json m = Json::parse(msg);
+    const bool cached = m.at("cached").as_bool();
+    if (!root) seq = index.sequence_from_json(m.at("seq"));
+
+    BenchResult br;
+    if (!cached) {
+      ScopedTimer t(C, "BENCHMARK");
+      br = bench.benchmark(seq, opts.bench);
+    }
+    if (root) {
+      SimResult sr;
+      sr.seq = seq;
+      if (cached) {
+        sr.res = result.sims[cachedIdx].res;
+        sr.cached = true;
+      } else {
+        sr.res = br;
+        cache.emplace(seq.canonical_key(), result.sims.size());
+      }
+      result.sims.push_back(sr);
+      {
+        ScopedTimer t(C, "BACKPROP");
+        tree.backprop(bpStart, sr.res);
+      }
+      if (onResult) onResult(size_t(iter), sr);
+      TZ_LOG(Info, "mcts iter " << iter << " pct10=" << sr.res.pct10 << (cached ? " (cached)" : "")
+                                << " tree=" << tree.root.size());
+      if (opts.dump_tree && (iter < 10 || (iter < 50 && iter % 10 == 0) ||
+                             (iter < 100 && iter % 25 == 0))) {
+        write_file(opts.dump_tree_prefix + std::to_string(iter) + ".dot",
+                   mcts_tree_graphviz(tree.root, *tree.strat));
+      }
+      if (opts.checkpoint_every > 0 && (iter + 1) % opts.checkpoint_every == 0) checkpoint();
+    }
+  }
+  ctrl.barrier();
+  if (root) {
+    unregister_handler();
+    checkpoint();
+    result.tree_size = tree.root.size();
+    result.tree_fully_visited = tree.root.fully_visited_size();
+  }
+  result.wall_s = wtime() - t0;
+  return result;
+}
+
+// ======================================================================== DFS
+
+Json DfsOpts::json() const {
+  Json j, o;
+  o["maxSeqs"] = max_seqs;
+  j["dfs__Opts"] = o;
+  return j;
+}
+
+std::vector<Sequence> get_all_sequences(const Graph &g, const Platform &plat, int64_t maxSeqs,
+                                        bool dedupStates, bool removeRedundant) {
+  auto gp = std::make_shared<Graph>(g);
+  gp->normalize();
+  std::vector<State> work{State(gp, plat)};
+  std::unordered_set<std::string> seenStates, seenSeqs;
+  std::vector<Sequence> out;
+  while (!work.empty()) {
+    if (maxSeqs >= 0 && int64_t(out.size()) >= maxSeqs) break;
+    State cur = std::move(work.back());
+    work.pop_back();
+    if (cur.complete()) {
+      Sequence s = cur.sequence();
+      if (removeRedundant) remove_redundant_syncs(s, cur.graph(), plat.n_streams);
+      if (seenSeqs.insert(s.canonical_key()).second) out.push_back(std::move(s));
+      continue;
+    }
+    auto ds = cur.get_decisions();
+    // push in reverse so the first decision is explored first
+    for (auto it = ds.rbegin(); it != ds.rend(); ++it) {
+      State nx = cur.apply(*it);
+      if (dedupStates && !seenStates.insert(nx.canonical_key()).second) continue;
+      work.push_back(std::move(nx));
+    }
+  }
+  return out;
+}
+
+SearchResult dfs_explore(const Graph &g, const Platform &plat, Benchmarker &bench, Ctrl &ctrl,
+                         const DfsOpts &opts,
+                         const std::function<void(size_t, const SimResult &)> &onResult) {
+  const bool root = ctrl.rank() == 0;
+  const double t0 = wtime();
+  SearchResult result;
+  result.opts = opts.json();
+  auto gp = std::make_shared<Graph>(g);
+  gp->normalize();
+  OpIndex index(*gp);
+  std::vector<Sequence> seqs;
+  if (root) {
+    ScopedTimer t(result.counters, "ENUMERATE");
+    seqs = get_all_sequences(*gp, plat, opts.max_seqs, opts.dedup_states, opts.remove_redundant_syncs);
+  }
+  std::function<void(int)> dump = [&result](int) { result.dump_csv(std::cout); };
+  if (root && opts.trap_signals) register_handler(dump);
+  for (size_t i = 0;; ++i) {
+    int64_t stop = root ? int64_t(i >= seqs.size()) : 0;
+    stop = ctrl.bcast_int(stop, 0);
+    if (stop) break;
+    std::string msg;
+    if (root) msg = seqs[i].json(true).dump();
+    ctrl.bcast(msg, 0);
+    Sequence seq = root ? seqs[i] : index.sequence_from_json(Json::parse(msg));
+    SimResult sr;
+    sr.seq = seq;
+    {
+      ScopedTimer t(result.counters, "BENCHMARK");
+      sr.res = bench.benchmark(seq, opts.bench);
+    }
+    if (root) {
+      result.sims.push_back(sr);
+      if (onResult) onResult(i, sr);
+    }
+  }
+  ctrl.barrier();
+  if (root) unregister_handler();
+  result.stop_reason = "enumerated";
+  result.wall_s = wtime() - t0;
+  return result;
+}
+
+// ======================================================================== trap / reproduce
+
+namespace {
+std::function<void(int)> g_handler;
+void trap_fn(int sig) {
+  if (g_handler) g_handler(sig);
+  std::_Exit(1);
+}
+} // namespace
+
+void register_handler(std::function<void(int)> fn) {
+  g_handler = std::move(fn);
+  std::signal(SIGINT, trap_fn);
+  std::signal(SIGTERM, trap_fn);
+  std::signal(SIGABRT, trap_fn);
+}
+
+void unregister_handler() {
+  g_handler = nullptr;
+  std::signal(SIGINT, SIG_DFL);
+  std::signal(SIGTERM, SIG_DFL);
+  std::signal(SIGABRT, SIG_DFL);
+}
+
+std::string version_string() {
+  std::ostringstream ss;
+  ss << TZ_VERSION_MAJOR << "." << TZ_VERSION_MINOR << "." << TZ_VERSION_PATCH << "+" << TZ_GIT_HASH;
+  return ss.str();
+}
+
+Json reproduce_json(const std::vector<std::string> &args) {
+  Json j;
+  j["major"] = TZ_VERSION_MAJOR;
+  j["minor"] = TZ_VERSION_MINOR;
+  j["patch"] = TZ_VERSION_PATCH;
+  j["hash"] = TZ_GIT_HASH;
+  Json a = Json::array();
+  for (const auto &s : args) a.push_back(s);
+  j["args"] = a;
+  return j;
+}
+
+} // namespace tz

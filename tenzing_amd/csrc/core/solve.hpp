@@ -1,0 +1,145 @@
+// Solvers: exhaustive DFS and Monte-Carlo tree search over the State decision tree.
+//
+// Parity:
+//   tenzing-dfs: get_all_sequences / explore / Result::dump_csv (tenzing-dfs/src/dfs.cpp:16-105,
+//     tenzing-dfs/include/tenzing/dfs/dfs.hpp:78-178)
+//   tenzing-mcts: explore (mcts.hpp:154-326), Node select/expand/rollout/backprop
+//     (mcts_node.hpp:119-564), dump_graphviz (mcts.hpp:52-127), per-phase counters
+//     (mcts/counters.hpp:15-25), strategies FastMin, Coverage, Random (built in the reference),
+//     AvgTime, Unvisited, AntiCorrelation, NormalizedAntiCorrelation, NormRootCorr,
+//     BalanceHistogram (stale in the reference, all implemented here behind one interface).
+// Differences: tree nodes store only their decision and statistics; the State is rebuilt
+// incrementally along the selection path (the reference stores a full Graph per node,
+// mcts_node.hpp:45); RNG is a seeded mt19937_64 instead of rand(); equivalent final schedules
+// are benchmarked once and re-used (cache by canonical key) unless disabled; search can be
+// bounded by a wall-clock budget; the tree can be checkpointed to JSON and resumed.
+#pragma once
+
+#include "benchmark.hpp"
+#include "util.hpp"
+
+#include <functional>
+#include <limits>
+#include <memory>
+#include <ostream>
+#include <random>
+
+namespace tz {
+
+struct SimResult {
+  Sequence seq;
+  BenchResult res;
+  bool cached = false;
+};
+
+struct SearchResult {
+  std::vector<SimResult> sims;
+  Counters counters;
+  Json opts;
+  double wall_s = 0;
+  size_t tree_size = 0;
+  size_t tree_fully_visited = 0;
+  std::string stop_reason;
+
+  /// index of the best (lowest pct10) result, -1 if none
+  int best() const;
+  /// CSV rows in the reference format, preceded by a one-line JSON of the options
+  void dump_csv(std::ostream &os) const;
+  /// one JSON object per line: {"i", "result", "seq"}
+  void dump_jsonl(std::ostream &os) const;
+};
+
+// ------------------------------------------------------------------------ MCTS
+
+struct MctsNode {
+  MctsNode *parent = nullptr;
+  std::vector<std::unique_ptr<MctsNode>> children;
+  Decision decision;
+  bool expanded = false;
+  bool fully_visited = false;
+  bool terminal = false;
+  size_t n = 0;
+  // strategy statistics
+  double tmin = std::numeric_limits<double>::infinity();
+  double tmax = -std::numeric_limits<double>::infinity();
+  std::vector<double> times; // kept sorted by strategies that need quantiles
+
+  const MctsNode &root() const { return parent ? parent->root() : *this; }
+  size_t size() const;
+  size_t fully_visited_size() const;
+  size_t unvisited_size() const;
+  bool is_leaf() const;
+};
+
+class Strategy {
+public:
+  virtual ~Strategy() = default;
+  virtual std::string name() const = 0;
+  /// exploitation score of `child` in [0,1] (or +inf to force)
+  virtual double select(const MctsNode &child) = 0;
+  virtual void backprop(MctsNode &node, const BenchResult &br) = 0;
+  virtual std::string label(const MctsNode &node) const;
+};
+
+std::unique_ptr<Strategy> make_strategy(const std::string &name, uint64_t seed);
+std::vector<std::string> strategy_names();
+
+struct MctsOpts {
+  int64_t n_iters = 300;        // 0 = until the tree is fully visited / budget exhausted
+  double time_budget_s = 0;     // 0 = unlimited
+  bool expand_rollout = true;   // keep rollout paths in the tree (reference Opts::expandRollout)
+  bool remove_redundant_syncs = true;
+  bool reuse_measurements = true; // benchmark each equivalent final schedule once
+  bool verify = true;           // race-check every candidate before it runs
+  bool dump_tree = false;
+  std::string dump_tree_prefix = "mcts_";
+  std::string strategy = "FastMin";
+  uint64_t seed = 0;
+  double explore_c = 1.41421356; // UCT exploration constant (reference sqrt(2))
+  BenchOpts bench;
+  std::string checkpoint_path;  // write tree + results JSON here every checkpoint_every iters
+  int64_t checkpoint_every = 0;
+  bool trap_signals = false;     // dump partial CSV on SIGINT/SIGTERM/SIGABRT (CLI)
+  std::string resume_path;      // resume a checkpointed tree
+  Json json() const;
+};
+
+/// Runs on every rank of `ctrl`; rank 0 owns the tree, all ranks benchmark each candidate
+/// together. Only rank 0's result holds the simulations.
+SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &bench, Ctrl &ctrl,
+                          const MctsOpts &opts,
+                          const std::function<void(size_t, const SimResult &)> &onResult = nullptr);
+
+/// graphviz of an MCTS tree (reference mcts.hpp:52-127)
+std::string mcts_tree_graphviz(const MctsNode &root, const Strategy &strat, size_t maxNodes = 2000);
+
+// ------------------------------------------------------------------------ DFS
+
+struct DfsOpts {
+  int64_t max_seqs = -1; // stop enumerating at this many sequences (reference maxSeqs)
+  bool dedup_states = true;
+  bool remove_redundant_syncs = true;
+  bool trap_signals = false;
+  BenchOpts bench;
+  Json json() const;
+};
+
+/// all complete, pairwise non-equivalent sequences (reference dfs.cpp:16-82)
+std::vector<Sequence> get_all_sequences(const Graph &g, const Platform &plat, int64_t maxSeqs = -1,
+                                        bool dedupStates = true, bool removeRedundant = true);
+
+SearchResult dfs_explore(const Graph &g, const Platform &plat, Benchmarker &bench, Ctrl &ctrl,
+                         const DfsOpts &opts,
+                         const std::function<void(size_t, const SimResult &)> &onResult = nullptr);
+
+// ------------------------------------------------------------------------ misc
+
+/// install SIGINT/SIGTERM/SIGABRT handler that calls fn then exits (reference trap.cpp:11-35)
+void register_handler(std::function<void(int)> fn);
+void unregister_handler();
+
+/// {"major","minor","patch","hash","args"} (reference reproduce.cpp:22-37)
+Json reproduce_json(const std::vector<std::string> &args);
+std::string version_string();
+
+} // namespace tz

@@ -1,0 +1,566 @@
+#include "state.hpp"
+#include "util.hpp"
+
+#include <algorithm>
+#include <map>
+#include <sstream>
+#include <unordered_map>
+
+namespace tz {
+
+// ---------------------------------------------------------------- Sequence
+
+Json Sequence::json(bool inGraph) const {
+  Json a = Json::array();
+  for (const auto &e : entries) {
+    Json j = e.op->json();
+    if (inGraph) j["in_graph"] = e.op->op_class() != OpClass::Sync;
+    a.push_back(j);
+  }
+  return a;
+}
+
+std::string Sequence::desc(const std::string &delim) const {
+  std::string s;
+  for (size_t i = 0; i < entries.size(); ++i) {
+    if (i) s += delim;
+    s += entries[i].op->desc();
+  }
+  return s;
+}
+
+static void op_streams_events(const BoundOp &op, int &s1, int &s2, int &ev) {
+  s1 = s2 = ev = -1;
+  if (op.op_class() == OpClass::BoundGpu) {
+    s1 = static_cast<const BoundGpuOp &>(op).stream();
+  } else if (op.op_class() == OpClass::Sync) {
+    const auto &so = static_cast<const SyncOp &>(op);
+    s1 = so.stream();
+    s2 = so.stream2();
+    ev = so.event();
+  }
+}
+
+int Sequence::num_events() const {
+  int m = 0;
+  for (const auto &e : entries) {
+    int s1, s2, ev;
+    op_streams_events(*e.op, s1, s2, ev);
+    m = std::max(m, ev + 1);
+  }
+  return m;
+}
+
+int Sequence::num_streams() const {
+  int m = 0;
+  for (const auto &e : entries) {
+    int s1, s2, ev;
+    op_streams_events(*e.op, s1, s2, ev);
+    m = std::max(m, std::max(s1, s2) + 1);
+  }
+  return m;
+}
+
+int Sequence::count_sync_ops() const {
+  int n = 0;
+  for (const auto &e : entries) n += e.op->op_class() == OpClass::Sync;
+  return n;
+}
+
+namespace {
+struct Relabel {
+  std::unordered_map<int, int> m;
+  bool identity = false;
+  int operator()(int x) {
+    if (x < 0 || identity) return x;
+    auto it = m.find(x);
+    if (it != m.end()) return it->second;
+    int v = int(m.size());
+    m[x] = v;
+    return v;
+  }
+};
+
+void key_entry(const BoundOp &op, Relabel &rs, Relabel &re, std::string &out) {
+  int s1, s2, ev;
+  op_streams_events(op, s1, s2, ev);
+  if (op.op_class() == OpClass::Sync) {
+    out += op.kind();
+  } else {
+    out += op.name();
+  }
+  if (s1 >= 0) out += "|s" + std::to_string(rs(s1));
+  if (s2 >= 0) out += "|t" + std::to_string(rs(s2));
+  if (ev >= 0) out += "|e" + std::to_string(re(ev));
+  out += ';';
+}
+} // namespace
+
+std::string Sequence::canonical_key() const {
+  Relabel rs, re;
+  std::string out;
+  for (const auto &e : entries) key_entry(*e.op, rs, re, out);
+  return out;
+}
+
+bool equivalent(const Sequence &a, const Sequence &b) {
+  return a.size() == b.size() && a.canonical_key() == b.canonical_key();
+}
+
+// ---------------------------------------------------------------- SyncModel
+
+SyncModel::SyncModel(int nStreams)
+    : S_(nStreams), cnt_(nStreams, 0), vc_(size_t(nStreams + 1) * nStreams, 0), tmp_(nStreams) {}
+
+void SyncModel::join_row(int dst, const int *src) {
+  int *d = &vc_[size_t(dst) * S_];
+  for (int c = 0; c < S_; ++c) d[c] = std::max(d[c], src[c]);
+}
+
+void SyncModel::host_to_stream(int s) { join_row(s, &vc_[size_t(S_) * S_]); }
+
+void SyncModel::ensure_event(int e) {
+  if (e >= int(evStream_.size())) {
+    evStream_.resize(e + 1, -1);
+    evClock_.resize(size_t(e + 1) * S_, 0);
+  }
+}
+
+int SyncModel::apply(const BoundOp &op) {
+  switch (op.op_class()) {
+  case OpClass::BoundGpu: {
+    const int s = static_cast<const BoundGpuOp &>(op).stream();
+    TZ_CHECK(s >= 0 && s < S_, "stream " << s << " out of range (" << S_ << " streams)");
+    host_to_stream(s);
+    return ++cnt_[s];
+  }
+  case OpClass::Sync: {
+    if (auto *cer = dynamic_cast<const EventRecord *>(&op)) {
+      const int s = cer->stream(), e = cer->event();
+      TZ_CHECK(s >= 0 && s < S_, "stream out of range");
+      host_to_stream(s);
+      ensure_event(e);
+      std::copy(&vc_[size_t(s) * S_], &vc_[size_t(s) * S_] + S_, &evClock_[size_t(e) * S_]);
+      evClock_[size_t(e) * S_ + s] = cnt_[s];
+      evStream_[e] = s;
+    } else if (auto *cswe = dynamic_cast<const StreamWaitEvent *>(&op)) {
+      const int s = cswe->stream(), e = cswe->event();
+      TZ_CHECK(s >= 0 && s < S_, "stream out of range");
+      host_to_stream(s);
+      if (event_recorded(e)) join_row(s, &evClock_[size_t(e) * S_]);
+    } else if (auto *ces = dynamic_cast<const EventSync *>(&op)) {
+      const int e = ces->event();
+      if (event_recorded(e)) join_row(S_, &evClock_[size_t(e) * S_]);
+    } else if (auto *ss = dynamic_cast<const StreamSync *>(&op)) {
+      const int s = ss->stream();
+      TZ_CHECK(s >= 0 && s < S_, "stream out of range");
+      std::copy(&vc_[size_t(s) * S_], &vc_[size_t(s) * S_] + S_, tmp_.begin());
+      tmp_[s] = cnt_[s];
+      join_row(S_, tmp_.data());
+    } else if (auto *sw = dynamic_cast<const StreamWait *>(&op)) {
+      const int w = sw->stream(), t = sw->stream2();
+      TZ_CHECK(w >= 0 && w < S_ && t >= 0 && t < S_, "stream out of range");
+      host_to_stream(w);
+      std::copy(&vc_[size_t(t) * S_], &vc_[size_t(t) * S_] + S_, tmp_.begin());
+      tmp_[t] = cnt_[t];
+      join_row(w, tmp_.data());
+    }
+    return 0;
+  }
+  default: return 0;
+  }
+}
+
+bool SyncModel::gpu_covered_for_stream(int t, int k, int s) const {
+  return t == s || vc(s, t) >= k || vc(S_, t) >= k;
+}
+
+bool SyncModel::gpu_covered_for_host(int t, int k) const { return vc(S_, t) >= k; }
+
+int SyncModel::covering_event(int t, int k) const {
+  for (int e = 0; e < num_events(); ++e)
+    if (evStream_[e] == t && evClock_[size_t(e) * S_ + t] >= k) return e;
+  return -1;
+}
+
+// ---------------------------------------------------------------- Decision
+
+std::string Decision::desc() const {
+  std::ostringstream ss;
+  switch (kind) {
+  case Kind::Execute: ss << "Execute{" << (op ? op->desc() : "?") << "}"; break;
+  case Kind::Expand: ss << "Expand{" << node << "}"; break;
+  case Kind::Choose: ss << "Choose{" << node << "," << choice << "}"; break;
+  case Kind::Assign: ss << "Assign{" << node << ", s:" << stream << "}"; break;
+  }
+  return ss.str();
+}
+
+bool Decision::same(const Decision &o) const {
+  if (kind != o.kind || node != o.node || stream != o.stream || choice != o.choice) return false;
+  if (kind == Kind::Execute) return op && o.op && op->eq(*o.op);
+  return true;
+}
+
+// ---------------------------------------------------------------- State
+
+State::State(GraphPtr g, const Platform &plat) : plat_(plat), sync_(plat.n_streams) {
+  TZ_CHECK(plat.n_streams >= 1, "platform needs at least one stream");
+  auto gg = std::make_shared<Graph>(*g);
+  gg->normalize();
+  g_ = gg;
+  grow();
+  auto start = std::dynamic_pointer_cast<const BoundOp>(g_->op(Graph::kStart));
+  posOf_[Graph::kStart] = 0;
+  seq_.push_back(start, Graph::kStart);
+}
+
+void State::grow() {
+  const size_t n = size_t(g_->capacity());
+  if (streamOf_.size() < n) {
+    streamOf_.resize(n, -1);
+    posOf_.resize(n, -1);
+    stamp_.resize(n, 0);
+  }
+}
+
+std::vector<int> State::frontier() const {
+  std::vector<int> f;
+  for (int v = 0; v < g_->capacity(); ++v) {
+    if (!g_->alive(v) || posOf_[v] >= 0) continue;
+    bool ready = true;
+    for (int p : g_->preds(v))
+      if (posOf_[p] < 0) {
+        ready = false;
+        break;
+      }
+    if (ready) f.push_back(v);
+  }
+  return f;
+}
+
+BoundOpPtr State::bound_op(int node) const {
+  const OpPtr &op = g_->op(node);
+  if (op->op_class() == OpClass::Gpu) {
+    TZ_CHECK(streamOf_[node] >= 0, "gpu op " << op->name() << " is not bound");
+    return std::make_shared<BoundGpuOp>(std::static_pointer_cast<const GpuOp>(op), streamOf_[node]);
+  }
+  auto b = std::dynamic_pointer_cast<const BoundOp>(op);
+  TZ_CHECK(b, "op " << op->name() << " is not executable");
+  return b;
+}
+
+static int gpu_stream_of(const BoundOp &op) {
+  return op.op_class() == OpClass::BoundGpu ? static_cast<const BoundGpuOp &>(op).stream() : -1;
+}
+
+bool State::is_synced(int node, const BoundOp &op) const {
+  const int s = gpu_stream_of(op);
+  for (int p : g_->preds(node)) {
+    const int k = stamp_[p];
+    if (k == 0) continue; // cpu-like pred (or Start): host order suffices
+    const int t = streamOf_[p];
+    if (s >= 0 ? !sync_.gpu_covered_for_stream(t, k, s) : !sync_.gpu_covered_for_host(t, k))
+      return false;
+  }
+  return true;
+}
+
+std::vector<BoundOpPtr> State::syncs_before(int node, const BoundOp &op) const {
+  std::vector<BoundOpPtr> out;
+  const int s = gpu_stream_of(op);
+  const int newEvent = sync_.num_events();
+  auto push = [&](BoundOpPtr x) {
+    for (const auto &y : out)
+      if (y->eq(*x)) return;
+    out.push_back(std::move(x));
+  };
+  for (int p : g_->preds(node)) {
+    const int k = stamp_[p];
+    if (k == 0) continue;
+    const int t = streamOf_[p];
+    const std::string &pn = g_->op(p)->name();
+    if (s >= 0) {
+      if (sync_.gpu_covered_for_stream(t, k, s)) continue;
+      const int e = sync_.covering_event(t, k);
+      if (e >= 0) push(std::make_shared<StreamWaitEvent>(s, e, "CSWE-after-" + pn));
+      else push(std::make_shared<EventRecord>(newEvent, t, "CER-b4-" + op.name()));
+    } else {
+      if (sync_.gpu_covered_for_host(t, k)) continue;
+      const int e = sync_.covering_event(t, k);
+      if (e >= 0) push(std::make_shared<EventSync>(e, "CES-b4-" + op.name()));
+      else push(std::make_shared<EventRecord>(newEvent, t, "CER-after-" + pn));
+      if (plat_.offer_stream_sync) push(std::make_shared<StreamSync>(t, "SS-b4-" + op.name()));
+    }
+  }
+  return out;
+}
+
+std::vector<int> State::used_streams() const {
+  std::vector<char> used(plat_.n_streams, 0);
+  for (int v = 0; v < g_->capacity(); ++v)
+    if (g_->alive(v) && streamOf_[v] >= 0) used[streamOf_[v]] = 1;
+  for (const auto &e : seq_.entries) {
+    int s1, s2, ev;
+    op_streams_events(*e.op, s1, s2, ev);
+    if (s1 >= 0 && s1 < plat_.n_streams) used[s1] = 1;
+    if (s2 >= 0 && s2 < plat_.n_streams) used[s2] = 1;
+  }
+  std::vector<int> out;
+  for (int s = 0; s < plat_.n_streams; ++s)
+    if (used[s]) out.push_back(s);
+  return out;
+}
+
+std::vector<Decision> State::get_decisions() const {
+  std::vector<Decision> ds;
+  if (complete()) return ds;
+  const std::vector<int> front = frontier();
+
+  std::vector<int> offer;
+  {
+    const std::vector<int> used = used_streams();
+    if (plat_.symmetric_streams) {
+      offer = used;
+      for (int s = 0; s < plat_.n_streams; ++s)
+        if (std::find(used.begin(), used.end(), s) == used.end()) {
+          offer.push_back(s);
+          break;
+        }
+      std::sort(offer.begin(), offer.end());
+    } else {
+      for (int s = 0; s < plat_.n_streams; ++s) offer.push_back(s);
+    }
+  }
+
+  for (int v : front) {
+    const OpPtr &op = g_->op(v);
+    switch (op->op_class()) {
+    case OpClass::Compound: {
+      Decision d;
+      d.kind = Decision::Kind::Expand;
+      d.node = v;
+      ds.push_back(d);
+      break;
+    }
+    case OpClass::Choice: {
+      auto c = std::static_pointer_cast<const ChoiceOp>(op);
+      const int n = int(c->choices().size());
+      for (int i = 0; i < n; ++i) {
+        Decision d;
+        d.kind = Decision::Kind::Choose;
+        d.node = v;
+        d.choice = i;
+        ds.push_back(d);
+      }
+      break;
+    }
+    case OpClass::Gpu:
+      if (streamOf_[v] < 0) {
+        for (int s : offer) {
+          Decision d;
+          d.kind = Decision::Kind::Assign;
+          d.node = v;
+          d.stream = s;
+          ds.push_back(d);
+        }
+        break;
+      }
+      // bound: fall through to execution
+      [[fallthrough]];
+    default: {
+      BoundOpPtr bop = bound_op(v);
+      std::vector<BoundOpPtr> syncs = syncs_before(v, *bop);
+      if (syncs.empty()) {
+        Decision d;
+        d.kind = Decision::Kind::Execute;
+        d.op = bop;
+        d.node = v;
+        ds.push_back(d);
+      } else {
+        for (auto &sy : syncs) {
+          Decision d;
+          d.kind = Decision::Kind::Execute;
+          d.op = sy;
+          d.node = -1;
+          bool dup = false;
+          for (const auto &x : ds)
+            if (x.same(d)) {
+              dup = true;
+              break;
+            }
+          if (!dup) ds.push_back(d);
+        }
+      }
+    }
+    }
+  }
+  return ds;
+}
+
+void State::apply_inplace(const Decision &d) {
+  switch (d.kind) {
+  case Decision::Kind::Execute: {
+    TZ_CHECK(d.op, "execute without op");
+    const int k = sync_.apply(*d.op);
+    if (d.node >= 0) {
+      TZ_CHECK(posOf_[d.node] < 0, "op " << d.op->name() << " executed twice");
+      posOf_[d.node] = int(seq_.size());
+      if (k > 0) {
+        stamp_[d.node] = k;
+        streamOf_[d.node] = gpu_stream_of(*d.op);
+      }
+    }
+    seq_.push_back(d.op, d.node);
+    break;
+  }
+  case Decision::Kind::Expand: {
+    auto c = std::dynamic_pointer_cast<const CompoundOp>(g_->op(d.node));
+    TZ_CHECK(c, "expand of non-compound op");
+    transforms_.insert("X:" + c->name());
+    g_ = g_->clone_but_expand(d.node, *c->graph());
+    grow();
+    break;
+  }
+  case Decision::Kind::Choose: {
+    auto c = std::dynamic_pointer_cast<const ChoiceOp>(g_->op(d.node));
+    TZ_CHECK(c, "choose on non-choice op");
+    auto chs = c->choices();
+    TZ_CHECK(d.choice >= 0 && d.choice < int(chs.size()), "bad choice index");
+    transforms_.insert("C:" + c->name() + "=" + chs[d.choice]->name());
+    g_ = g_->clone_but_replace(d.node, chs[d.choice]);
+    grow();
+    break;
+  }
+  case Decision::Kind::Assign: {
+    TZ_CHECK(d.stream >= 0 && d.stream < plat_.n_streams, "bad stream");
+    streamOf_[d.node] = d.stream;
+    break;
+  }
+  }
+}
+
+State State::apply(const Decision &d) const {
+  State s = *this;
+  s.apply_inplace(d);
+  return s;
+}
+
+std::string State::canonical_key() const {
+  Relabel rs, re;
+  rs.identity = !plat_.symmetric_streams;
+  std::string out;
+  for (const auto &e : seq_.entries) key_entry(*e.op, rs, re, out);
+  out += '#';
+  for (int v = 0; v < g_->capacity(); ++v) {
+    if (!g_->alive(v) || posOf_[v] >= 0 || streamOf_[v] < 0) continue;
+    out += g_->op(v)->name() + ":s" + std::to_string(rs(streamOf_[v])) + ";";
+  }
+  out += '#';
+  for (const auto &t : transforms_) out += t + ";";
+  return out;
+}
+
+bool equivalent(const State &a, const State &b) { return a.canonical_key() == b.canonical_key(); }
+
+// ---------------------------------------------------------------- verify / redundant syncs
+
+std::string Violation::desc() const {
+  std::ostringstream ss;
+  ss << "@" << position << " " << op << " not ordered after " << pred;
+  return ss.str();
+}
+
+namespace {
+// returns violations; stops at the first one when firstOnly
+std::vector<Violation> check(const Sequence &seq, const Graph &g, int S, bool firstOnly,
+                             const std::vector<char> *skip = nullptr) {
+  std::vector<Violation> out;
+  SyncModel m(S);
+  std::vector<int> stampT(g.capacity(), -1), stampK(g.capacity(), 0);
+  std::vector<char> done(g.capacity(), 0);
+  for (size_t i = 0; i < seq.entries.size(); ++i) {
+    if (skip && (*skip)[i]) continue;
+    const BoundOp &op = *seq.entries[i].op;
+    if (op.op_class() != OpClass::Sync) {
+      const int node = g.find(op.name());
+      if (node < 0) {
+        out.push_back({int(i), op.name(), "<not in graph>"});
+        if (firstOnly) return out;
+      } else {
+        const int s = gpu_stream_of(op);
+        for (int p : g.preds(node)) {
+          bool ok;
+          if (!done[p]) ok = false;
+          else if (stampK[p] == 0) ok = true;
+          else if (s >= 0) ok = m.gpu_covered_for_stream(stampT[p], stampK[p], s);
+          else ok = m.gpu_covered_for_host(stampT[p], stampK[p]);
+          if (!ok) {
+            out.push_back({int(i), op.name(), g.op(p)->name()});
+            if (firstOnly) return out;
+          }
+        }
+        const int k = m.apply(op);
+        done[node] = 1;
+        if (k > 0) {
+          stampT[node] = s;
+          stampK[node] = k;
+        }
+        continue;
+      }
+    }
+    m.apply(op);
+  }
+  for (int v = 0; v < g.capacity(); ++v) {
+    if (g.alive(v) && !done[v]) {
+      out.push_back({int(seq.size()), g.op(v)->name(), "<never executed>"});
+      if (firstOnly) return out;
+    }
+  }
+  return out;
+}
+} // namespace
+
+std::vector<Violation> verify(const Sequence &seq, const Graph &g, int nStreams) {
+  return check(seq, g, nStreams, false);
+}
+
+int remove_redundant_syncs(Sequence &seq, const Graph &g, int nStreams) {
+  int removed = 0;
+  std::vector<char> skip(seq.size(), 0);
+  TZ_CHECK(check(seq, g, nStreams, true, &skip).empty(),
+           "remove_redundant_syncs on an invalid sequence");
+  bool changed = true;
+  while (changed) {
+    changed = false;
+    for (int i = int(seq.size()) - 1; i >= 0; --i) {
+      if (skip[i] || seq.entries[i].op->op_class() != OpClass::Sync) continue;
+      skip[i] = 1;
+      if (check(seq, g, nStreams, true, &skip).empty()) {
+        ++removed;
+        changed = true;
+      } else {
+        skip[i] = 0;
+      }
+    }
+  }
+  if (removed) {
+    Sequence out;
+    for (size_t i = 0; i < seq.size(); ++i)
+      if (!skip[i]) out.entries.push_back(seq.entries[i]);
+    seq = std::move(out);
+  }
+  return removed;
+}
+
+Sequence random_rollout(State s, std::mt19937_64 &rng) {
+  while (!s.complete()) {
+    auto ds = s.get_decisions();
+    TZ_CHECK(!ds.empty(), "dead end state (no decisions, not complete)");
+    std::uniform_int_distribution<size_t> u(0, ds.size() - 1);
+    s.apply_inplace(ds[u(rng)]);
+  }
+  return s.sequence();
+}
+
+} // namespace tz

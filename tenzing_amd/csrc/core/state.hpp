@@ -1,0 +1,187 @@
+// Sequential-decision-process core: Platform model, Sequence, happens-before (vector clock)
+// synchronizer, Decisions and State.
+//
+// Parity:
+//   Sequence<BoundOp> (include/tenzing/sequence.hpp:21-112, src/sequence.cpp:21-167)
+//   EventSynchronizer::is_synced / make_syncs (include/tenzing/event_synchronizer.hpp:183-329)
+//   Decision: ExecuteOp / ExpandOp / ChooseOp / AssignOpStream (include/tenzing/decision.hpp)
+//   SDP::State::get_decisions / apply / frontier (src/state.cpp:25-124)
+//   Schedule::remove_redundant_syncs (src/schedule.cpp:19-321)
+//   get_equivalence(Seq,Seq) / (State,State) (src/sequence.cpp:21-86, src/state.cpp:126-143)
+//
+// Synchronizer model. The reference decides "is a synced with b" by pattern-matching the prefix
+// (a ... CER(a.stream, e) ... CSWE(b.stream, e) / CES(e)). Here every stream and the host carry
+// a vector clock over streams: a GPU op is stamped (stream, k), an event captures its stream's
+// clock, CSWE/CES/StreamSync/StreamWait join clocks, and anything enqueued on a stream first
+// joins the host clock (host issue order). An edge a->b is covered iff b's clock has seen a's
+// stamp. This accepts every prefix the reference accepts and, in addition, transitive
+// coverage (a -> CES -> b on another stream; a -> CSWE chain), so fewer syncs are inserted and
+// the same model gives an exact race verifier and a general redundant-sync eliminator (drop any
+// sync op whose removal keeps every edge covered), which subsumes the reference's five
+// pattern rules.
+#pragma once
+
+#include "graph.hpp"
+
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+namespace tz {
+
+/// search-time model of the execution resources (reference Platform streams_,
+/// platform.hpp:147-219). The runtime counterpart is an Executor.
+struct Platform {
+  int n_streams = 2;
+  /// all streams interchangeable: assignments that differ only by a stream relabelling are
+  /// equivalent, so only already-used streams plus one fresh stream are offered
+  bool symmetric_streams = true;
+  /// also offer StreamSync(s) as a gpu->host synchronization (one op instead of CER+CES)
+  bool offer_stream_sync = false;
+
+  static Platform make_n_streams(int n) {
+    Platform p;
+    p.n_streams = n;
+    return p;
+  }
+};
+
+struct SeqEntry {
+  BoundOpPtr op;
+  int node = -1; // graph vertex id, -1 for synchronizer-inserted ops
+};
+
+class Sequence {
+public:
+  std::vector<SeqEntry> entries;
+
+  size_t size() const { return entries.size(); }
+  bool empty() const { return entries.empty(); }
+  const BoundOpPtr &operator[](size_t i) const { return entries[i].op; }
+  void push_back(BoundOpPtr op, int node = -1) { entries.push_back({std::move(op), node}); }
+
+  /// JSON array of op JSON (reference to_json(Sequence), operation_serdes.hpp:20-28)
+  Json json(bool inGraph = false) const;
+  std::string desc(const std::string &delim = ", ") const;
+  int num_events() const;  // 1 + max event id used
+  int num_streams() const; // 1 + max stream id used
+  int count_sync_ops() const;
+  /// canonical form under stream/event relabeling (first-use order). Two sequences are
+  /// equivalent (reference get_equivalence(Seq,Seq)) iff their canonical keys are equal.
+  std::string canonical_key() const;
+};
+
+bool equivalent(const Sequence &a, const Sequence &b);
+
+/// Vector-clock happens-before model of a (partial) sequence on S streams.
+class SyncModel {
+public:
+  explicit SyncModel(int nStreams = 0);
+  int n_streams() const { return S_; }
+
+  /// apply one bound op. `graphNode` is used only to stamp GPU ops; returns GPU stamp k (1-based
+  /// position on its stream) or 0 for non-GPU ops
+  int apply(const BoundOp &op);
+
+  /// is GPU work stamped (t,k) complete before the next op enqueued on stream s?
+  bool gpu_covered_for_stream(int t, int k, int s) const;
+  /// ... before the host's next action?
+  bool gpu_covered_for_host(int t, int k) const;
+  /// earliest recorded event on stream t whose clock covers stamp (t,k), or -1
+  int covering_event(int t, int k) const;
+  int num_events() const { return int(evStream_.size()); }
+  bool event_recorded(int e) const { return e < num_events() && evStream_[e] >= 0; }
+
+private:
+  void ensure_event(int e);
+  int &vc(int row, int col) { return vc_[size_t(row) * S_ + col]; }
+  int vc(int row, int col) const { return vc_[size_t(row) * S_ + col]; }
+  void join_row(int dst, const int *src);
+  void host_to_stream(int s);
+
+  int S_;
+  std::vector<int> cnt_;     // ops enqueued per stream
+  std::vector<int> vc_;      // (S+1) x S, row S = host
+  std::vector<int> evClock_; // E x S
+  std::vector<int> evStream_;
+  std::vector<int> tmp_;
+};
+
+struct Decision {
+  enum class Kind { Execute, Expand, Choose, Assign };
+  Kind kind = Kind::Execute;
+  BoundOpPtr op;   // Execute: the op (graph op or sync)
+  int node = -1;   // graph vertex (Execute of a graph op, Expand, Choose, Assign)
+  int stream = -1; // Assign
+  int choice = -1; // Choose
+  std::string desc() const;
+  bool same(const Decision &o) const;
+};
+
+class State {
+public:
+  State() = default;
+  State(GraphPtr g, const Platform &plat);
+
+  const Graph &graph() const { return *g_; }
+  const GraphPtr &graph_ptr() const { return g_; }
+  const Platform &platform() const { return plat_; }
+  const Sequence &sequence() const { return seq_; }
+  int stream_of(int node) const { return node < int(streamOf_.size()) ? streamOf_[node] : -1; }
+  bool executed(int node) const { return node < int(posOf_.size()) && posOf_[node] >= 0; }
+  bool complete() const { return executed(Graph::kFinish); }
+
+  /// vertices whose predecessors have all executed and that have not executed themselves
+  std::vector<int> frontier() const;
+  /// legal next moves (reference state.cpp:25-69), deterministic order
+  std::vector<Decision> get_decisions() const;
+  /// synchronization ops needed before a bound op can execute (empty = synced)
+  std::vector<BoundOpPtr> syncs_before(int node, const BoundOp &op) const;
+  bool is_synced(int node, const BoundOp &op) const;
+
+  State apply(const Decision &d) const;
+  void apply_inplace(const Decision &d);
+
+  /// canonical key (sequence + pending bindings + graph transforms) for equivalence / dedup
+  std::string canonical_key() const;
+
+private:
+  BoundOpPtr bound_op(int node) const;
+  void grow();
+  std::vector<int> used_streams() const;
+
+  GraphPtr g_;
+  Platform plat_;
+  Sequence seq_;
+  std::vector<int> streamOf_;
+  std::vector<int> posOf_;
+  std::vector<int> stamp_;         // GPU stamp (position on its stream) per vertex
+  SyncModel sync_;
+  std::set<std::string> transforms_; // applied Expand/Choose decisions (for canonical keys)
+};
+
+bool equivalent(const State &a, const State &b);
+
+// ---- whole-sequence analyses
+
+struct Violation {
+  int position;   // index in sequence of the op whose predecessor is not covered
+  std::string op; // op name
+  std::string pred;
+  std::string desc() const;
+};
+
+/// Replay `seq` in the happens-before model and report every graph edge that is not covered
+/// (race / missing synchronization). `g` must contain every graph op of the sequence (e.g. the
+/// final State's graph); ops are matched by name.
+std::vector<Violation> verify(const Sequence &seq, const Graph &g, int nStreams);
+
+/// Remove synchronization ops whose removal keeps every edge covered (fix-point, scanning from
+/// the end). Returns the number removed. Reference: Schedule::remove_redundant_syncs.
+int remove_redundant_syncs(Sequence &seq, const Graph &g, int nStreams);
+
+/// random complete rollout from a state (for tests / sampling)
+Sequence random_rollout(State s, std::mt19937_64 &rng);
+
+} // namespace tz

@@ -1,0 +1,110 @@
+// HIP runtime: the MI355X execution platform for candidate schedules.
+//
+// Parity: reference Platform (include/tenzing/platform.hpp:147-219: cudaStream pool via
+// make_n_streams, ResourceMap Event->cudaEvent_t, CudaEventPool :221-242), the CUDA sync ops'
+// run() (src/cuda/ops_cuda.cpp:48-168) and the benchmark hot loop (src/benchmarker.cpp:93-97).
+// MI355X design:
+//  * N non-blocking HIP streams, optionally with priorities or disjoint CU masks
+//    (hipExtStreamCreateWithCUMask: a stream can be pinned to a subset of the 256 CUs / 8 XCDs,
+//    turning "which CUs" into a schedulable resource);
+//  * a pool of timing-disabled hipEvents indexed by the schedule's abstract event ids;
+//  * two execution modes for one schedule: Eager (host issues every op each iteration, like the
+//    reference) and Graph (the whole multi-stream schedule, RCCL calls included, is recorded
+//    once by stream capture into a hipGraph and replayed with one hipGraphLaunch per
+//    iteration). In Graph mode host synchronizations (CES / StreamSync) become graph joins: every
+//    later enqueue on any stream waits for the events the host had synchronized on;
+//  * a watchdog: a schedule whose iteration exceeds `watchdog_s` (e.g. an RCCL deadlock) aborts
+//    the process with a diagnostic instead of hanging the search.
+#pragma once
+
+#include "core/benchmark.hpp"
+
+#include <atomic>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace tz {
+
+enum class ExecMode { Eager, Graph };
+
+struct HipRuntimeOpts {
+  int device = -1;            // -1: keep current device
+  int n_streams = 2;
+  std::vector<int> priorities; // optional per-stream priorities
+  bool cu_partition = false;   // give each stream a disjoint, XCD-balanced CU mask
+  ExecMode mode = ExecMode::Eager;
+  double watchdog_s = 0;       // 0 = off
+};
+
+class HipRuntime : public Executor, public ExecutorRunner {
+public:
+  explicit HipRuntime(const HipRuntimeOpts &opts);
+  ~HipRuntime() override;
+  HipRuntime(const HipRuntime &) = delete;
+  HipRuntime &operator=(const HipRuntime &) = delete;
+
+  // Executor
+  int num_streams() const override { return int(streams_.size()); }
+  void launch(const GpuOp &op, int stream) override;
+  void event_record(int event, int stream) override;
+  void stream_wait_event(int stream, int event) override;
+  void event_sync(int event) override;
+  void stream_sync(int stream) override;
+  void stream_wait(int waiter, int waitee) override;
+  void device_sync() override;
+  void *native_stream(int stream) override;
+
+  // ExecutorRunner
+  void prepare(const Sequence &seq) override;
+  void run(int64_t n) override;
+
+  void set_mode(ExecMode m);
+  ExecMode mode() const { return mode_; }
+  /// mode actually used for the prepared sequence (Graph falls back to Eager when a host op
+  /// cannot be captured)
+  ExecMode effective_mode() const { return graphExec_ ? ExecMode::Graph : ExecMode::Eager; }
+  int device() const { return device_; }
+  std::string device_name() const;
+  /// number of nodes of the captured graph (0 in eager mode)
+  size_t graph_nodes() const { return graphNodes_; }
+  void set_watchdog(double s) { watchdogS_ = s; }
+
+private:
+  void *event(int e);
+  void *internal_event();
+  void capture_guard(int stream);
+  void destroy_graph();
+  bool capturable(const Sequence &seq) const;
+  void run_eager_once();
+
+  int device_ = 0;
+  ExecMode mode_;
+  std::vector<void *> streams_;
+  std::vector<void *> events_;   // schedule events
+  std::vector<void *> internal_; // capture / StreamWait helpers
+  size_t internalUsed_ = 0;
+  Sequence seq_;
+  void *graphExec_ = nullptr;
+  size_t graphNodes_ = 0;
+
+  // graph-capture host-sync emulation
+  bool capturing_ = false;
+  std::vector<int> hostSynced_;              // events the host "waited" on during capture
+  std::vector<std::vector<char>> applied_;   // [stream][k] hostSynced_[k] applied to stream
+
+  double watchdogS_ = 0;
+  std::atomic<double> deadline_{0};
+  std::atomic<bool> stop_{false};
+  std::thread watchdog_;
+};
+
+/// hipGetDeviceCount (0 if no GPU / no driver)
+int hip_device_count();
+/// throw tz::Error if `err` (a hipError_t) is not success
+void hip_check(int err, const char *what, const char *file, int line);
+
+} // namespace tz
+
+#define TZ_HIP(x) ::tz::hip_check(int(x), #x, __FILE__, __LINE__)

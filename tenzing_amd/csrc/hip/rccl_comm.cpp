@@ -1,0 +1,86 @@
+#include "rccl_comm.hpp"
+
+#include "core/util.hpp"
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+namespace tz {
+
+#define TZ_NCCL(x)                                                                                 \
+  do {                                                                                             \
+    ncclResult_t r_ = (x);                                                                         \
+    if (r_ != ncclSuccess) TZ_THROW(#x << " failed: " << ncclGetErrorString(r_));                  \
+  } while (0)
+
+static ncclDataType_t dt(int dtype) {
+  switch (dtype) {
+  case 0: return ncclFloat32;
+  case 1: return ncclFloat64;
+  case 2: return ncclInt32;
+  default: TZ_THROW("bad dtype " << dtype);
+  }
+}
+
+RcclComm::RcclComm(Ctrl &ctrl, int device) : rank_(ctrl.rank()), size_(ctrl.size()) {
+  if (device >= 0) {
+    if (hipSetDevice(device) != hipSuccess) TZ_THROW("hipSetDevice failed");
+  }
+  ncclUniqueId id;
+  std::string s(sizeof(id), '\0');
+  if (rank_ == 0) {
+    TZ_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(&s[0], &id, sizeof(id));
+  }
+  ctrl.bcast(s, 0);
+  std::memcpy(&id, s.data(), sizeof(id));
+  ncclComm_t c = nullptr;
+  TZ_NCCL(ncclCommInitRank(&c, size_, id, rank_));
+  comm_ = c;
+}
+
+RcclComm::~RcclComm() {
+  if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+}
+
+void RcclComm::sendrecv(const void *sendBuf, size_t sendCount, int sendPeer, void *recvBuf,
+                        size_t recvCount, int recvPeer, int dtype, void *stream) const {
+  ncclComm_t c = static_cast<ncclComm_t>(comm_);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  TZ_NCCL(ncclGroupStart());
+  if (sendCount) TZ_NCCL(ncclSend(sendBuf, sendCount, dt(dtype), sendPeer, c, s));
+  if (recvCount) TZ_NCCL(ncclRecv(recvBuf, recvCount, dt(dtype), recvPeer, c, s));
+  TZ_NCCL(ncclGroupEnd());
+}
+
+void RcclComm::exchange(const std::vector<Xfer> &xs, int dtype, void *stream) const {
+  ncclComm_t c = static_cast<ncclComm_t>(comm_);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  TZ_NCCL(ncclGroupStart());
+  for (const auto &x : xs) {
+    if (x.sendCount) TZ_NCCL(ncclSend(x.send, x.sendCount, dt(dtype), x.sendPeer, c, s));
+    if (x.recvCount) TZ_NCCL(ncclRecv(x.recv, x.recvCount, dt(dtype), x.recvPeer, c, s));
+  }
+  TZ_NCCL(ncclGroupEnd());
+}
+
+void RcclComm::allreduce_sum(void *buf, size_t count, int dtype, void *stream) const {
+  TZ_NCCL(ncclAllReduce(buf, buf, count, dt(dtype), ncclSum, static_cast<ncclComm_t>(comm_),
+                        static_cast<hipStream_t>(stream)));
+}
+
+std::string RcclComm::version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return std::to_string(v);
+}
+
+std::vector<std::shared_ptr<RcclComm>> make_rccl_comms(Ctrl &ctrl, int device, int n) {
+  std::vector<std::shared_ptr<RcclComm>> out;
+  for (int i = 0; i < n; ++i) out.push_back(std::make_shared<RcclComm>(ctrl, device));
+  return out;
+}
+
+} // namespace tz

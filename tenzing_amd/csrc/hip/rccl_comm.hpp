@@ -1,0 +1,61 @@
+// RCCL data plane over xGMI.
+//
+// Reference data plane: CUDA-aware MPI point-to-point (include/tenzing/mpi/ops_mpi.hpp:17-192,
+// src/mpi/ops_mpi.cpp:11-49) issued from the host. Here communication is stream-ordered RCCL:
+// a transfer is a GPU op bound to a HIP stream (so GPU->comm edges need only an event wait,
+// not a host round trip) and RCCL kernels can be captured into hipGraphs. Because RCCL
+// point-to-point has no tags and a pending send occupies its stream until the peer posts the
+// matching receive, every exchange is issued as one ncclGroupStart/End group (deadlock-free on
+// periodic rings), and the reference's per-direction MPI tags become one communicator per
+// direction: transfers of different directions use different xGMI links and can overlap.
+// Communicator unique ids are distributed over the host control plane (Ctrl).
+#pragma once
+
+#include "core/ctrl.hpp"
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace tz {
+
+class RcclComm {
+public:
+  /// collective over `ctrl`: rank 0 creates the unique id, broadcasts it, all ranks init
+  RcclComm(Ctrl &ctrl, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm &) = delete;
+  RcclComm &operator=(const RcclComm &) = delete;
+
+  void *comm() const { return comm_; } // ncclComm_t
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+
+  /// grouped point-to-point: send `sendCount` elements to `sendPeer` and receive `recvCount`
+  /// into `recvBuf` from `recvPeer` (either count may be 0); dtype: 0=f32, 1=f64, 2=i32
+  void sendrecv(const void *sendBuf, size_t sendCount, int sendPeer, void *recvBuf,
+                size_t recvCount, int recvPeer, int dtype, void *stream) const;
+  /// grouped multi-peer exchange (all-to-all-v style)
+  struct Xfer {
+    const void *send = nullptr;
+    size_t sendCount = 0;
+    int sendPeer = -1;
+    void *recv = nullptr;
+    size_t recvCount = 0;
+    int recvPeer = -1;
+  };
+  void exchange(const std::vector<Xfer> &xs, int dtype, void *stream) const;
+  /// in-place all-reduce sum (f32/f64) — used by tests and device-side checks
+  void allreduce_sum(void *buf, size_t count, int dtype, void *stream) const;
+
+  static std::string version();
+
+private:
+  void *comm_ = nullptr;
+  int rank_ = 0, size_ = 1;
+};
+
+/// a set of communicators over the same ranks (one per exchange direction)
+std::vector<std::shared_ptr<RcclComm>> make_rccl_comms(Ctrl &ctrl, int device, int n);
+
+} // namespace tz

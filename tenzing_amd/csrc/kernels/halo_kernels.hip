@@ -1,0 +1,277 @@
+// Halo pack / unpack kernels for gfx950 (CDNA4).
+//
+// Reference kernels: src/halo_exchange/ops_halo_exchange.cu:519-664 (pack/unpack for QXYZ and
+// XYZQ, one CUDA thread block of (32,4,4) per tile; their loops start at 0 without thread
+// offsets, so every thread copies the same elements — SURVEY.md §7.4). Design here:
+//  * one generic "box <-> dense buffer" copy: the box is rows of `len` contiguous elements
+//    (x-runs for XYZQ, (q,x)-runs for QXYZ), so one kernel serves every face/edge/corner and
+//    both storage orders;
+//  * a flat 1-D work space (item = VEC consecutive doubles of one row, buffer offset =
+//    item*VEC exactly) decoded with multiply-high "magic" division (no integer divides), so
+//    consecutive lanes touch consecutive addresses of both the grid row and the buffer;
+//  * 16-byte (double2) accesses whenever the row and all strides are even — the halo layout
+//    (HaloExchange) pads x so interior rows start 64-B aligned, making every y/z face
+//    dwordx4-vectorizable; 3-wide x faces fall back to 8-byte accesses (their 24-byte runs at a
+//    4 KB pitch are sector-bound either way);
+//  * 4 items in flight per lane (all loads issued before the stores) to cover HBM latency on a
+//    wave64 machine without relying on occupancy alone;
+//  * a multi-box variant packs every face/edge/corner of an exchange in ONE launch: blocks are
+//    assigned to boxes through a prefix table in the kernel arguments (scalar loads, wave-
+//    uniform), so small edge/corner boxes cost a handful of blocks instead of a launch each.
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+namespace tz {
+namespace kern {
+
+namespace {
+
+#define TZ_HIP_LAUNCH_CHECK()                                                                      \
+  do {                                                                                             \
+    hipError_t e_ = hipGetLastError();                                                             \
+    if (e_ != hipSuccess)                                                                          \
+      throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e_));     \
+  } while (0)
+
+struct FastDiv {
+  uint32_t d = 1, m = 0, s = 0;
+  FastDiv() = default;
+  explicit FastDiv(uint32_t div) : d(div) {
+    s = 0;
+    while ((uint64_t(1) << s) < div) ++s;
+    m = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << s) - div)) / div + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    const uint32_t t = __umulhi(n, m);
+    return uint32_t((uint64_t(t) + n) >> s);
+  }
+};
+
+struct DevDesc {
+  double *buf;
+  int64_t grid_off, s1, s2, s3;
+  uint32_t lvec, n1, n2, items;
+  FastDiv dl, d1, d2;
+  int32_t vec;
+};
+
+struct DevBatch {
+  DevDesc d[kMaxBoxes];
+  uint32_t block_start[kMaxBoxes + 1];
+  int32_t n;
+};
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;
+
+DevDesc make_dev(const BoxDesc &b) {
+  DevDesc d{};
+  d.buf = b.buf;
+  d.grid_off = b.grid_off;
+  d.s1 = b.s1;
+  d.s2 = b.s2;
+  d.s3 = b.s3;
+  const bool even = (b.len % 2 == 0) && (b.grid_off % 2 == 0) && (b.s1 % 2 == 0) &&
+                    (b.s2 % 2 == 0) && (b.s3 % 2 == 0) &&
+                    (reinterpret_cast<uintptr_t>(b.buf) % 16 == 0);
+  d.vec = even ? 2 : 1;
+  d.lvec = uint32_t(b.len / d.vec);
+  d.n1 = uint32_t(b.n1);
+  d.n2 = uint32_t(b.n2);
+  const uint64_t items = uint64_t(d.lvec) * b.n1 * b.n2 * b.n3;
+  if (items >= (uint64_t(1) << 31)) throw std::runtime_error("box too large for 32-bit indexing");
+  d.items = uint32_t(items);
+  d.dl = FastDiv(std::max<uint32_t>(d.lvec, 1));
+  d.d1 = FastDiv(std::max<uint32_t>(d.n1, 1));
+  d.d2 = FastDiv(std::max<uint32_t>(d.n2, 1));
+  return d;
+}
+
+uint32_t blocks_for(const DevDesc &d) {
+  const uint64_t per = uint64_t(kThreads) * kUnroll;
+  uint64_t b = (uint64_t(d.items) + per - 1) / per;
+  return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(b, 4096)));
+}
+
+template <int VEC> struct Vec;
+template <> struct Vec<1> { using T = double; };
+template <> struct Vec<2> { using T = double2; };
+
+template <int VEC>
+__device__ __forceinline__ int64_t grid_index(const DevDesc &d, uint32_t it) {
+  const uint32_t row = d.dl.div(it);
+  const uint32_t xv = it - row * d.lvec;
+  const uint32_t r1 = d.d1.div(row);
+  const uint32_t i1 = row - r1 * d.n1;
+  const uint32_t i3 = d.d2.div(r1);
+  const uint32_t i2 = r1 - i3 * d.n2;
+  return d.grid_off + int64_t(i1) * d.s1 + int64_t(i2) * d.s2 + int64_t(i3) * d.s3 +
+         int64_t(xv) * VEC;
+}
+
+template <int VEC, bool UNPACK>
+__device__ __forceinline__ void box_body(double *__restrict__ grid, const DevDesc &d, uint32_t tid,
+                                         uint32_t nthreads) {
+  using T = typename Vec<VEC>::T;
+  T *__restrict__ buf = reinterpret_cast<T *>(d.buf);
+  uint32_t it = tid;
+  for (; it + (kUnroll - 1) * nthreads < d.items; it += kUnroll * nthreads) {
+    T v[kUnroll];
+    int64_t g[kUnroll];
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k) g[k] = grid_index<VEC>(d, it + k * nthreads);
+    if (UNPACK) {
+#pragma unroll
+      for (int k = 0; k < kUnroll; ++k) v[k] = buf[it + k * nthreads];
+#pragma unroll
+      for (int k = 0; k < kUnroll; ++k) *reinterpret_cast<T *>(grid + g[k]) = v[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kUnroll; ++k) v[k] = *reinterpret_cast<const T *>(grid + g[k]);
+#pragma unroll
+      for (int k = 0; k < kUnroll; ++k) buf[it + k * nthreads] = v[k];
+    }
+  }
+  for (; it < d.items; it += nthreads) {
+    const int64_t g = grid_index<VEC>(d, it);
+    if (UNPACK) *reinterpret_cast<T *>(grid + g) = buf[it];
+    else buf[it] = *reinterpret_cast<const T *>(grid + g);
+  }
+}
+
+template <bool UNPACK>
+__global__ __launch_bounds__(kThreads) void box_copy_one_k(double *__restrict__ grid, DevDesc d) {
+  const uint32_t tid = blockIdx.x * kThreads + threadIdx.x;
+  const uint32_t nth = gridDim.x * kThreads;
+  if (d.vec == 2) box_body<2, UNPACK>(grid, d, tid, nth);
+  else box_body<1, UNPACK>(grid, d, tid, nth);
+}
+
+template <bool UNPACK>
+__global__ __launch_bounds__(kThreads) void box_copy_many_k(double *__restrict__ grid, DevBatch b) {
+  int box = 0;
+  while (box + 1 < b.n && blockIdx.x >= b.block_start[box + 1]) ++box;
+  const DevDesc &d = b.d[box];
+  const uint32_t nb = b.block_start[box + 1] - b.block_start[box];
+  const uint32_t tid = (blockIdx.x - b.block_start[box]) * kThreads + threadIdx.x;
+  const uint32_t nth = nb * kThreads;
+  if (d.vec == 2) box_body<2, UNPACK>(grid, d, tid, nth);
+  else box_body<1, UNPACK>(grid, d, tid, nth);
+}
+
+// ---- grid initialization / verification (test support; not on the timed path)
+
+__device__ __forceinline__ int64_t wrapi(int64_t a, int64_t n) {
+  a %= n;
+  return a < 0 ? a + n : a;
+}
+
+__device__ __forceinline__ double halo_value(int q, int64_t gx, int64_t gy, int64_t gz) {
+  constexpr int64_t G = 65536;
+  return double(((int64_t(q) * G + gz) * G + gy) * G + gx);
+}
+
+// classify logical element (x,y,z,q); returns expected value after a complete exchange and
+// writes the storage index
+__device__ __forceinline__ double halo_expect(const HaloGeom &g, int64_t lin, int64_t &idx,
+                                              bool afterExchange) {
+  const int64_t X = g.nx + 2 * g.g, Y = g.ny + 2 * g.g, Z = g.nz + 2 * g.g;
+  const int64_t x = lin % X;
+  int64_t r = lin / X;
+  const int64_t y = r % Y;
+  r /= Y;
+  const int64_t z = r % Z;
+  const int q = int(r / Z);
+  if (g.order == 0) idx = q * g.sq + z * g.sz + y * g.sy + x + g.xoff;
+  else idx = q + int64_t(g.nq) * (x + X * (y + Y * z));
+  const int gx = (x < g.g || x >= g.nx + g.g), gy = (y < g.g || y >= g.ny + g.g),
+            gz = (z < g.g || z >= g.nz + g.g);
+  const int k = gx + gy + gz;
+  if (k > 0) {
+    const bool filled = afterExchange && (g.neighbors == 26 || k == 1);
+    if (!filled) return -1.0;
+  }
+  const int64_t GX = int64_t(g.nx) * g.px, GY = int64_t(g.ny) * g.py, GZ = int64_t(g.nz) * g.pz;
+  return halo_value(q, wrapi(int64_t(g.cx) * g.nx + x - g.g, GX),
+                    wrapi(int64_t(g.cy) * g.ny + y - g.g, GY),
+                    wrapi(int64_t(g.cz) * g.nz + z - g.g, GZ));
+}
+
+__global__ __launch_bounds__(kThreads) void halo_init_k(double *__restrict__ grid, HaloGeom g) {
+  const int64_t total = int64_t(g.nx + 2 * g.g) * (g.ny + 2 * g.g) * (g.nz + 2 * g.g) * g.nq;
+  for (int64_t lin = int64_t(blockIdx.x) * kThreads + threadIdx.x; lin < total;
+       lin += int64_t(gridDim.x) * kThreads) {
+    int64_t idx;
+    const double v = halo_expect(g, lin, idx, false);
+    grid[idx] = v;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void halo_check_k(const double *__restrict__ grid, HaloGeom g,
+                                                         unsigned long long *count) {
+  const int64_t total = int64_t(g.nx + 2 * g.g) * (g.ny + 2 * g.g) * (g.nz + 2 * g.g) * g.nq;
+  unsigned long long bad = 0;
+  for (int64_t lin = int64_t(blockIdx.x) * kThreads + threadIdx.x; lin < total;
+       lin += int64_t(gridDim.x) * kThreads) {
+    int64_t idx;
+    const double v = halo_expect(g, lin, idx, true);
+    bad += grid[idx] != v;
+  }
+  // wave64 reduction, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_xor(bad, off);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(count, bad);
+}
+
+} // namespace
+
+void halo_init(double *grid, const HaloGeom &g, void *stream) {
+  hipLaunchKernelGGL(halo_init_k, dim3(4096), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     grid, g);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void halo_check(const double *grid, const HaloGeom &g, unsigned long long *count, void *stream) {
+  hipLaunchKernelGGL(halo_check_k, dim3(4096), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     grid, g, count);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void box_copy(double *grid, const BoxDesc &b, bool unpack, void *stream) {
+  DevDesc d = make_dev(b);
+  if (d.items == 0) return;
+  const dim3 grid_dim(blocks_for(d));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (unpack) hipLaunchKernelGGL(box_copy_one_k<true>, grid_dim, dim3(kThreads), 0, s, grid, d);
+  else hipLaunchKernelGGL(box_copy_one_k<false>, grid_dim, dim3(kThreads), 0, s, grid, d);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void box_copy_many(double *grid, const BoxDesc *boxes, int n, bool unpack, void *stream) {
+  if (n <= 0) return;
+  if (n > kMaxBoxes) throw std::runtime_error("box_copy_many: too many boxes");
+  DevBatch b{};
+  b.n = 0;
+  uint32_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    DevDesc d = make_dev(boxes[i]);
+    if (d.items == 0) continue;
+    b.d[b.n] = d;
+    b.block_start[b.n] = total;
+    total += blocks_for(d);
+    ++b.n;
+  }
+  if (b.n == 0) return;
+  b.block_start[b.n] = total;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (unpack) hipLaunchKernelGGL(box_copy_many_k<true>, dim3(total), dim3(kThreads), 0, s, grid, b);
+  else hipLaunchKernelGGL(box_copy_many_k<false>, dim3(total), dim3(kThreads), 0, s, grid, b);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+} // namespace kern
+} // namespace tz

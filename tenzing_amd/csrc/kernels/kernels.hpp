@@ -1,0 +1,62 @@
+// Host-side launch API of the hand-written gfx950 kernels (implemented in *.hip).
+// All launches are asynchronous on the given hipStream_t (passed as void* so host-only
+// translation units need no HIP headers) and never allocate or synchronize, so they can be
+// captured into hipGraphs.
+#pragma once
+
+#include <cstdint>
+
+namespace tz {
+namespace kern {
+
+/// A 4-D box inside a pitched array, copied to/from a dense buffer.
+/// The box is `n3 x n2 x n1` rows of `len` contiguous elements; row (i1,i2,i3) starts at
+/// element `grid_off + i1*s1 + i2*s2 + i3*s3` of the array; the buffer is dense
+/// ((i3*n2 + i2)*n1 + i1)*len + x. For the XYZQ halo layout rows are x-runs and
+/// (i1,i2,i3) = (y,z,q); for QXYZ rows are (q,x)-runs and (i1,i2,i3) = (y,z,1).
+struct BoxDesc {
+  double *buf = nullptr;
+  int64_t grid_off = 0;
+  int64_t s1 = 0, s2 = 0, s3 = 0;
+  int32_t len = 0, n1 = 0, n2 = 0, n3 = 0;
+};
+
+constexpr int kMaxBoxes = 32;
+
+/// pack (grid -> buf) or unpack (buf -> grid) one box
+void box_copy(double *grid, const BoxDesc &d, bool unpack, void *stream);
+/// pack/unpack up to kMaxBoxes boxes in ONE launch (fused multi-face halo pack/unpack)
+void box_copy_many(double *grid, const BoxDesc *d, int n, bool unpack, void *stream);
+
+/// y[r] = sum_j A[r,j] x[j] for CSR A (f32 values, i32 indices). `lanesPerRow` in {1,2,4,8,16,32,64}
+/// (0 = pick from nnz/row). When `accumulate`, y[r] += ... instead.
+void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,
+              const float *x, float *y, int lanesPerRow, bool accumulate, void *stream);
+/// dst[i] = src[idx[i]]
+void gather_f32(int n, const float *src, const int32_t *idx, float *dst, void *stream);
+/// y = a + b (f32, vectorized)
+void vector_add_f32(int n, const float *a, const float *b, float *y, void *stream);
+/// y += alpha * x (f64)
+void axpy_f64(int64_t n, double alpha, const double *x, double *y, void *stream);
+/// fill a[i] = base + scale * i (f64) — deterministic test patterns
+void iota_f64(int64_t n, double base, double scale, double *a, void *stream);
+/// empty kernel (launch-overhead probes, reference test/test_gpu_graph.cu:10)
+void empty(void *stream);
+/// spin for `ticks` of the constant-rate wall clock (synthetic device work for scheduling tests)
+void busy_wait(int64_t ticks, int blocks, void *stream);
+
+/// Halo grid geometry for init / verification kernels.
+struct HaloGeom {
+  int32_t order = 0; // 0 = XYZQ (x fastest, q slowest, x-padded rows), 1 = QXYZ
+  int64_t xoff = 0, sy = 0, sz = 0, sq = 0; // XYZQ strides (elements)
+  int32_t nx = 0, ny = 0, nz = 0, nq = 0, g = 0;
+  int32_t cx = 0, cy = 0, cz = 0, px = 1, py = 1, pz = 1;
+  int32_t neighbors = 6; // which ghost regions an exchange fills (6 faces, 26 all)
+};
+/// interior = encoded global coordinate, ghosts = -1
+void halo_init(double *grid, const HaloGeom &g, void *stream);
+/// count elements that differ from what a completed exchange must leave; result in *count
+void halo_check(const double *grid, const HaloGeom &g, unsigned long long *count, void *stream);
+
+} // namespace kern
+} // namespace tz

@@ -1,0 +1,171 @@
+// CSR SpMV and vector kernels for gfx950.
+//
+// Reference: include/tenzing/spmv/ops_spmv.cuh:25-186 (a one-thread-per-row `spmv` kernel that
+// is never launched; the op calls cuSPARSE CSR_ALG2; `VectorAdd::run` is a no-op;
+// `scatter<<<128,100>>>` grid-stride gather). Here:
+//  * csr_spmv: W lanes of a wave64 cooperate on one row (W chosen from the average row length,
+//    W | 64 so a row group never straddles a wave), strided coalesced loads of col/val, x read
+//    through L2/MALL (the band structure keeps x L2-resident), butterfly reduction with
+//    __shfl_xor inside the W-lane group, optional accumulate (y += A x) so the remote part can
+//    be fused into y without a separate add. CSR SpMV is bandwidth/latency bound (2 flops per
+//    8-12 bytes); MFMA does not apply to a general CSR band matrix.
+//  * gather (x-halo scatter), f32 vector add with 16-byte accesses, f64 axpy / iota, an empty
+//    kernel for launch-overhead probes and a clocked busy kernel for scheduling tests.
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+#include <stdexcept>
+#include <string>
+
+namespace tz {
+namespace kern {
+
+namespace {
+
+#define TZ_HIP_LAUNCH_CHECK()                                                                      \
+  do {                                                                                             \
+    hipError_t e_ = hipGetLastError();                                                             \
+    if (e_ != hipSuccess)                                                                          \
+      throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e_));     \
+  } while (0)
+
+constexpr int kThreads = 256;
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void csr_spmv_k(int nRows, const int32_t *__restrict__ rowPtr,
+                                                       const int32_t *__restrict__ colInd,
+                                                       const float *__restrict__ val,
+                                                       const float *__restrict__ x,
+                                                       float *__restrict__ y, int accumulate) {
+  const int gtid = blockIdx.x * kThreads + threadIdx.x;
+  const int row = gtid / W;
+  const int lane = gtid & (W - 1);
+  if (row >= nRows) return; // whole W-lane groups exit together (W divides 64)
+  const int b = rowPtr[row], e = rowPtr[row + 1];
+  float sum = 0.f;
+  for (int j = b + lane; j < e; j += W) sum = fmaf(val[j], x[colInd[j]], sum);
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) sum += __shfl_xor(sum, off, W);
+  if (lane == 0) y[row] = accumulate ? y[row] + sum : sum;
+}
+
+__global__ __launch_bounds__(kThreads) void gather_k(int n, const float *__restrict__ src,
+                                                     const int32_t *__restrict__ idx,
+                                                     float *__restrict__ dst) {
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads)
+    dst[i] = src[idx[i]];
+}
+
+__global__ __launch_bounds__(kThreads) void vector_add_k(int n, const float *__restrict__ a,
+                                                         const float *__restrict__ b,
+                                                         float *__restrict__ y) {
+  const int n4 = n / 4;
+  const float4 *a4 = reinterpret_cast<const float4 *>(a);
+  const float4 *b4 = reinterpret_cast<const float4 *>(b);
+  float4 *y4 = reinterpret_cast<float4 *>(y);
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
+    float4 u = a4[i], v = b4[i];
+    y4[i] = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+  }
+  for (int i = n4 * 4 + blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads)
+    y[i] = a[i] + b[i];
+}
+
+__global__ __launch_bounds__(kThreads) void axpy_k(int64_t n, double alpha,
+                                                   const double *__restrict__ x,
+                                                   double *__restrict__ y) {
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * kThreads)
+    y[i] = fma(alpha, x[i], y[i]);
+}
+
+__global__ __launch_bounds__(kThreads) void iota_k(int64_t n, double base, double scale,
+                                                   double *__restrict__ a) {
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * kThreads)
+    a[i] = base + scale * double(i);
+}
+
+__global__ void empty_k() {}
+
+__global__ void busy_k(int64_t ticks) {
+  // wall_clock64 runs at a fixed rate (hipDeviceAttributeWallClockRate), unlike the shader clock
+  const int64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+int grid_for(int64_t n, int perThread = 1) {
+  int64_t b = (n + int64_t(kThreads) * perThread - 1) / (int64_t(kThreads) * perThread);
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  return int(b);
+}
+
+} // namespace
+
+void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,
+              const float *x, float *y, int lanesPerRow, bool accumulate, void *stream) {
+  if (nRows <= 0) return;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int W = lanesPerRow;
+  if (W <= 0) W = 8;
+  const int64_t threads = int64_t(nRows) * W;
+  const dim3 g(unsigned((threads + kThreads - 1) / kThreads)), b(kThreads);
+  const int acc = accumulate ? 1 : 0;
+  switch (W) {
+  case 1: hipLaunchKernelGGL(csr_spmv_k<1>, g, b, 0, s, nRows, rowPtr, colInd, val, x, y, acc); break;
+  case 2: hipLaunchKernelGGL(csr_spmv_k<2>, g, b, 0, s, nRows, rowPtr, colInd, val, x, y, acc); break;
+  case 4: hipLaunchKernelGGL(csr_spmv_k<4>, g, b, 0, s, nRows, rowPtr, colInd, val, x, y, acc); break;
+  case 8: hipLaunchKernelGGL(csr_spmv_k<8>, g, b, 0, s, nRows, rowPtr, colInd, val, x, y, acc); break;
+  case 16: hipLaunchKernelGGL(csr_spmv_k<16>, g, b, 0, s, nRows, rowPtr, colInd, val, x, y, acc); break;
+  case 32: hipLaunchKernelGGL(csr_spmv_k<32>, g, b, 0, s, nRows, rowPtr, colInd, val, x, y, acc); break;
+  case 64: hipLaunchKernelGGL(csr_spmv_k<64>, g, b, 0, s, nRows, rowPtr, colInd, val, x, y, acc); break;
+  default: throw std::runtime_error("csr_spmv: lanesPerRow must be a power of two <= 64");
+  }
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void gather_f32(int n, const float *src, const int32_t *idx, float *dst, void *stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_k, dim3(grid_for(n)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), n, src, idx, dst);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void vector_add_f32(int n, const float *a, const float *b, float *y, void *stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(vector_add_k, dim3(grid_for(n, 4)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), n, a, b, y);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void axpy_f64(int64_t n, double alpha, const double *x, double *y, void *stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(axpy_k, dim3(grid_for(n, 4)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), n, alpha, x, y);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void iota_f64(int64_t n, double base, double scale, double *a, void *stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(iota_k, dim3(grid_for(n, 4)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), n, base, scale, a);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void empty(void *stream) {
+  hipLaunchKernelGGL(empty_k, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream));
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void busy_wait(int64_t cycles, int blocks, void *stream) {
+  hipLaunchKernelGGL(busy_k, dim3(blocks > 0 ? blocks : 1), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), cycles);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+} // namespace kern
+} // namespace tz

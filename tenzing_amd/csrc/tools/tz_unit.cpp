@@ -1,0 +1,456 @@
+// Native unit tests of the core (no GPU, no Python). Mirrors the reference's in-source doctest
+// cases (src/operation.cpp:87-101 "[cpu] op eq", src/graph.cpp:422-501 graph construction /
+// clone / replace / expand, src/sequence.cpp:169-176) and test/test_noop_graph.cpp,
+// test/test_gpu_graph.cu (decision generation under 2 streams and stream-swap equivalence),
+// plus synchronizer race-freedom, redundant-sync removal, serdes round trips and solvers.
+// Run: tenzing_amd/bin/tz-unit [filter]
+#include "core/benchmark.hpp"
+#include "core/solve.hpp"
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <iostream>
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+using namespace tz;
+
+static int g_fail = 0, g_checks = 0;
+#define CHECK(c)                                                                                   \
+  do {                                                                                             \
+    ++g_checks;                                                                                    \
+    if (!(c)) {                                                                                    \
+      ++g_fail;                                                                                    \
+      std::fprintf(stderr, "  CHECK FAILED %s:%d: %s\n", __FILE__, __LINE__, #c);                  \
+    }                                                                                              \
+  } while (0)
+
+struct TestCase {
+  const char *name;
+  std::function<void()> fn;
+};
+static std::vector<TestCase> &cases() {
+  static std::vector<TestCase> c;
+  return c;
+}
+struct Reg {
+  Reg(const char *n, std::function<void()> f) { cases().push_back({n, std::move(f)}); }
+};
+#define TEST(name)                                                                                 \
+  static void name();                                                                              \
+  static Reg reg_##name(#name, name);                                                              \
+  static void name()
+
+static std::shared_ptr<Graph> diamond(double a = 10, double b = 20, double c = 30, double d = 5) {
+  auto g = std::make_shared<Graph>();
+  auto k1 = std::make_shared<SimGpuOp>("k1", a);
+  auto k2 = std::make_shared<SimGpuOp>("k2", b);
+  auto k3 = std::make_shared<SimGpuOp>("k3", c);
+  auto k4 = std::make_shared<SimGpuOp>("k4", d);
+  g->start_then(k1);
+  g->then(k1, k2);
+  g->then(k1, k3);
+  g->then(k2, k4);
+  g->then(k3, k4);
+  g->then_finish(k4);
+  return g;
+}
+
+TEST(json_roundtrip) {
+  Json j = Json::parse(R"({"b":[1,2.5,"x\n",true,null],"a":{"k":-3}})");
+  CHECK(j.at("a").at("k").as_int() == -3);
+  CHECK(j.at("b").at(1).as_double() == 2.5);
+  CHECK(j.dump() == R"({"a":{"k":-3},"b":[1,2.5,"x\n",true,null]})");
+  CHECK(Json::parse(j.dump()) == j);
+}
+
+TEST(op_eq) {
+  NoOp a("a"), a2("a"), b("b");
+  CHECK(a.eq(a2));
+  CHECK(!a.eq(b));
+  EventRecord r1(0, 1, "x"), r2(0, 1, "y"), r3(1, 1);
+  CHECK(r1.eq(r2));
+  CHECK(!r1.eq(r3));
+  CHECK(r1.json().dump() == R"({"event":0,"kind":"CudaEventRecord","name":"x","stream":1})");
+}
+
+TEST(graph_build_clone_replace_expand) {
+  auto g = diamond();
+  g->normalize();
+  CHECK(g->size() == 6);
+  CHECK(g->num_edges() == 6);
+  CHECK(g->succs(Graph::kStart).size() == 1);
+  auto topo = g->topo_order();
+  CHECK(topo.front() == Graph::kStart && topo.back() == Graph::kFinish);
+  const int k2 = g->find("k2");
+  auto g2 = g->clone_but_replace(k2, std::make_shared<SimGpuOp>("k2b", 1));
+  CHECK(g2->find("k2") < 0 && g2->find("k2b") == k2);
+  CHECK(g->find("k2") == k2);
+  // expand a compound op into the outer graph
+  auto outer = std::make_shared<Graph>();
+  auto sub = std::make_shared<Graph>();
+  auto x = std::make_shared<NoOp>("x"), y = std::make_shared<NoOp>("y");
+  sub->start_then(x);
+  sub->then(x, y);
+  sub->then_finish(y);
+  auto c = std::make_shared<StaticCompoundOp>("c", sub);
+  auto pre = std::make_shared<NoOp>("pre"), post = std::make_shared<NoOp>("post");
+  outer->start_then(pre);
+  outer->then(pre, c);
+  outer->then(c, post);
+  outer->then_finish(post);
+  auto e = outer->clone_but_expand(outer->find("c"), *sub);
+  CHECK(e->find("c") < 0);
+  CHECK(e->size() == 6);
+  const int ix = e->find("x"), iy = e->find("y");
+  CHECK(e->preds(ix).size() == 1 && e->op(e->preds(ix)[0])->name() == "pre");
+  CHECK(e->succs(iy).size() == 1 && e->op(e->succs(iy)[0])->name() == "post");
+}
+
+TEST(noop_graph_decisions) {
+  // reference test/test_noop_graph.cpp:10-42
+  auto g = std::make_shared<Graph>();
+  auto op1 = std::make_shared<NoOp>("op1");
+  g->start_then(op1);
+  g->then_finish(op1);
+  State s(g, Platform::make_n_streams(2));
+  CHECK(s.sequence().size() == 1);
+  auto ds = s.get_decisions();
+  int count = 0;
+  for (auto &d : ds) count += d.kind == Decision::Kind::Execute && d.op->name() == "op1";
+  CHECK(count == 1);
+  for (auto &d : ds) CHECK(s.apply(d).sequence().size() == 2);
+}
+
+TEST(gpu_graph_decisions_and_equivalence) {
+  // reference test/test_gpu_graph.cu:41-118
+  auto g = std::make_shared<Graph>();
+  auto k1 = std::make_shared<SimGpuOp>("kernel1", 1), k2 = std::make_shared<SimGpuOp>("kernel2", 1),
+       k3 = std::make_shared<SimGpuOp>("kernel3", 1);
+  g->start_then(k1);
+  g->then(k1, k2);
+  g->then(k1, k3);
+  g->then_finish(k2);
+  g->then_finish(k3);
+  Platform nonsym = Platform::make_n_streams(2);
+  nonsym.symmetric_streams = false;
+  State s0(g, nonsym);
+  auto ds = s0.get_decisions();
+  int a0 = 0, a1 = 0;
+  for (auto &d : ds) {
+    a0 += d.kind == Decision::Kind::Assign && d.stream == 0;
+    a1 += d.kind == Decision::Kind::Assign && d.stream == 1;
+  }
+  CHECK(a0 == 1 && a1 == 1);
+  State sa = s0.apply(ds[0]), sb = s0.apply(ds[1]);
+  CHECK(sa.sequence().size() == 1);
+  // binding kernel1 to stream 0 or 1 is equivalent under a stream bijection
+  State sa2(g, Platform::make_n_streams(2)), sb2(g, Platform::make_n_streams(2));
+  Decision d0, d1;
+  d0.kind = d1.kind = Decision::Kind::Assign;
+  d0.node = d1.node = sa2.graph().find("kernel1");
+  d0.stream = 0;
+  d1.stream = 1;
+  CHECK(equivalent(sa2.apply(d0), sb2.apply(d1)));
+  // symmetric platform offers only one fresh stream initially
+  State s1(g, Platform::make_n_streams(2));
+  CHECK(s1.get_decisions().size() == 1);
+  // after binding, kernel1 is executable
+  auto ds2 = sa.get_decisions();
+  CHECK(ds2.size() == 1 && ds2[0].kind == Decision::Kind::Execute && ds2[0].op->name() == "kernel1");
+}
+
+TEST(synchronizer_inserts_syncs) {
+  auto g = diamond();
+  Platform p = Platform::make_n_streams(2);
+  State s(g, p);
+  auto exec = [&](const std::string &kind, int stream) {
+    for (auto &d : s.get_decisions()) {
+      if (kind == "assign" && d.kind == Decision::Kind::Assign && d.stream == stream) {
+        s.apply_inplace(d);
+        return true;
+      }
+      if (kind == "exec" && d.kind == Decision::Kind::Execute) {
+        s.apply_inplace(d);
+        return true;
+      }
+    }
+    return false;
+  };
+  CHECK(exec("assign", 0)); // k1 -> s0
+  CHECK(exec("exec", 0));   // k1
+  // k2, k3 frontier: assign k2 -> s1 (second stream)
+  bool ok = false;
+  for (auto &d : s.get_decisions())
+    if (d.kind == Decision::Kind::Assign && s.graph().op(d.node)->name() == "k2" && d.stream == 1) {
+      s.apply_inplace(d);
+      ok = true;
+      break;
+    }
+  CHECK(ok);
+  // k2 on s1 depends on k1 on s0 -> decisions must contain a CER on stream 0, not k2 itself
+  bool sawCer = false, sawK2 = false;
+  for (auto &d : s.get_decisions()) {
+    if (d.kind != Decision::Kind::Execute) continue;
+    if (d.op->kind() == "CudaEventRecord" && static_cast<const SyncOp &>(*d.op).stream() == 0) sawCer = true;
+    if (d.op->name() == "k2") sawK2 = true;
+  }
+  CHECK(sawCer && !sawK2);
+}
+
+TEST(every_rollout_is_race_free) {
+  std::mt19937_64 rng(7);
+  for (int streams = 1; streams <= 3; ++streams) {
+    auto g = diamond();
+    for (int t = 0; t < 200; ++t) {
+      State s(g, Platform::make_n_streams(streams));
+      Sequence seq = random_rollout(s, rng);
+      // final graph == normalized g here (no compound/choice)
+      Graph ng = *g;
+      ng.normalize();
+      CHECK(verify(seq, ng, streams).empty());
+      Sequence r = seq;
+      remove_redundant_syncs(r, ng, streams);
+      CHECK(verify(r, ng, streams).empty());
+      CHECK(r.count_sync_ops() <= seq.count_sync_ops());
+    }
+  }
+}
+
+TEST(verify_detects_race) {
+  auto g = diamond();
+  Graph ng = *g;
+  ng.normalize();
+  auto k = [&](const char *n) { return std::static_pointer_cast<const GpuOp>(ng.op(ng.find(n))); };
+  Sequence s;
+  s.push_back(std::make_shared<Start>());
+  s.push_back(std::make_shared<BoundGpuOp>(k("k1"), 0));
+  s.push_back(std::make_shared<BoundGpuOp>(k("k2"), 1)); // races with k1 (no event)
+  s.push_back(std::make_shared<BoundGpuOp>(k("k3"), 0));
+  s.push_back(std::make_shared<BoundGpuOp>(k("k4"), 0));
+  s.push_back(std::make_shared<Finish>());
+  auto v = verify(s, ng, 2);
+  CHECK(v.size() >= 2); // k2 after k1, k4 after k2, Finish after k4
+  // fixed version
+  Sequence f;
+  f.push_back(std::make_shared<Start>());
+  f.push_back(std::make_shared<BoundGpuOp>(k("k1"), 0));
+  f.push_back(std::make_shared<EventRecord>(0, 0));
+  f.push_back(std::make_shared<StreamWaitEvent>(1, 0));
+  f.push_back(std::make_shared<BoundGpuOp>(k("k2"), 1));
+  f.push_back(std::make_shared<BoundGpuOp>(k("k3"), 0));
+  f.push_back(std::make_shared<StreamWait>(0, 1));
+  f.push_back(std::make_shared<BoundGpuOp>(k("k4"), 0));
+  f.push_back(std::make_shared<StreamSync>(0));
+  f.push_back(std::make_shared<Finish>());
+  CHECK(verify(f, ng, 2).empty());
+}
+
+TEST(serdes_roundtrip) {
+  auto g = diamond();
+  std::mt19937_64 rng(3);
+  Sequence seq = random_rollout(State(g, Platform::make_n_streams(2)), rng);
+  OpIndex idx(*g);
+  Sequence back = idx.sequence_from_json(Json::parse(seq.json(true).dump()));
+  CHECK(back.size() == seq.size());
+  CHECK(back.canonical_key() == seq.canonical_key());
+  for (size_t i = 0; i < seq.size(); ++i) CHECK(back[i]->eq(*seq[i]));
+}
+
+TEST(equivalence_under_relabel) {
+  auto g = diamond();
+  Graph ng = *g;
+  ng.normalize();
+  auto k = [&](const char *n) { return std::static_pointer_cast<const GpuOp>(ng.op(ng.find(n))); };
+  auto build = [&](int s0, int s1, int e) {
+    Sequence s;
+    s.push_back(std::make_shared<Start>());
+    s.push_back(std::make_shared<BoundGpuOp>(k("k1"), s0));
+    s.push_back(std::make_shared<EventRecord>(e, s0));
+    s.push_back(std::make_shared<StreamWaitEvent>(s1, e));
+    s.push_back(std::make_shared<BoundGpuOp>(k("k2"), s1));
+    return s;
+  };
+  CHECK(equivalent(build(0, 1, 0), build(1, 0, 3)));
+  CHECK(!equivalent(build(0, 1, 0), build(0, 0, 0)));
+}
+
+TEST(dfs_enumerates_and_dedups) {
+  auto g = diamond();
+  for (int streams = 1; streams <= 2; ++streams) {
+    auto seqs = get_all_sequences(*g, Platform::make_n_streams(streams), -1);
+    CHECK(!seqs.empty());
+    Graph ng = *g;
+    ng.normalize();
+    std::set<std::string> keys;
+    for (auto &s : seqs) {
+      CHECK(verify(s, ng, streams).empty());
+      keys.insert(s.canonical_key());
+    }
+    CHECK(keys.size() == seqs.size());
+    if (streams == 1) CHECK(seqs.size() == 2); // k2/k3 order
+  }
+}
+
+TEST(sim_prefers_overlap) {
+  auto g = diamond(10, 100, 100, 10);
+  SimParams p;
+  p.launch_us = 1;
+  SimBenchmarker sb(2, p);
+  BenchOpts bo;
+  bo.n_iters = 3;
+  auto seqs = get_all_sequences(*g, Platform::make_n_streams(2), -1);
+  double best = 1e9, worst = 0;
+  for (auto &s : seqs) {
+    double t = sb.benchmark(s, bo).pct10;
+    best = std::min(best, t);
+    worst = std::max(worst, t);
+  }
+  CHECK(best < 180e-6);  // k2 || k3 on two streams
+  CHECK(worst > 200e-6); // serialized
+}
+
+TEST(mcts_finds_good_schedule) {
+  auto g = diamond(10, 100, 100, 10);
+  SimParams p;
+  p.launch_us = 1;
+  SelfCtrl ctrl;
+  for (const auto &strat : strategy_names()) {
+    SimBenchmarker sb(2, p);
+    MctsOpts o;
+    o.n_iters = 60;
+    o.strategy = strat;
+    o.seed = 5;
+    o.bench.n_iters = 3;
+    SearchResult r = mcts_explore(*g, Platform::make_n_streams(2), sb, ctrl, o);
+    CHECK(!r.sims.empty());
+    CHECK(r.best() >= 0);
+    if (strat == "FastMin") CHECK(r.sims[r.best()].res.pct10 < 180e-6);
+  }
+}
+
+TEST(mcts_full_tree_stops) {
+  auto g = std::make_shared<Graph>();
+  auto a = std::make_shared<NoOp>("a"), b = std::make_shared<NoOp>("b");
+  g->start_then(a);
+  g->start_then(b);
+  g->then_finish(a);
+  g->then_finish(b);
+  SimBenchmarker sb(1, SimParams());
+  SelfCtrl ctrl;
+  MctsOpts o;
+  o.n_iters = 100;
+  o.bench.n_iters = 2;
+  SearchResult r = mcts_explore(*g, Platform::make_n_streams(1), sb, ctrl, o);
+  CHECK(r.stop_reason == "full_tree");
+  CHECK(r.sims.size() <= 4);
+}
+
+TEST(csv_benchmarker_replay) {
+  auto g = diamond();
+  SimBenchmarker sb(2, SimParams());
+  SelfCtrl ctrl;
+  DfsOpts o;
+  o.bench.n_iters = 2;
+  SearchResult r = dfs_explore(*g, Platform::make_n_streams(2), sb, ctrl, o);
+  const std::string path = "/tmp/tz_unit_replay.csv";
+  {
+    std::ofstream f(path);
+    r.dump_csv(f);
+  }
+  CsvBenchmarker cb(path, *g);
+  CHECK(cb.size() == r.sims.size());
+  for (auto &s : r.sims) CHECK(std::abs(cb.benchmark(s.seq, o.bench).pct10 - s.res.pct10) < 1e-12);
+  std::remove(path.c_str());
+}
+
+TEST(choice_and_compound_in_search) {
+  auto sub = std::make_shared<Graph>();
+  auto x = std::make_shared<SimGpuOp>("x", 5);
+  auto fast = std::make_shared<SimGpuOp>("y_fast", 5), slow = std::make_shared<SimGpuOp>("y_slow", 50);
+  auto ch = std::make_shared<StaticChoiceOp>("y", std::vector<OpPtr>{slow, fast});
+  sub->start_then(x);
+  sub->then(x, ch);
+  sub->then_finish(ch);
+  auto c = std::make_shared<StaticCompoundOp>("comp", sub);
+  auto g = std::make_shared<Graph>();
+  g->start_then(c);
+  g->then_finish(c);
+  auto seqs = get_all_sequences(*g, Platform::make_n_streams(2), -1);
+  bool sawFast = false, sawSlow = false;
+  for (auto &s : seqs)
+    for (auto &e : s.entries) {
+      sawFast |= e.op->name() == "y_fast";
+      sawSlow |= e.op->name() == "y_slow";
+    }
+  CHECK(sawFast && sawSlow);
+  SimBenchmarker sb(2, SimParams());
+  SelfCtrl ctrl;
+  MctsOpts o;
+  o.n_iters = 40;
+  o.bench.n_iters = 2;
+  SearchResult r = mcts_explore(*g, Platform::make_n_streams(2), sb, ctrl, o);
+  bool bestFast = false;
+  for (auto &e : r.sims[r.best()].seq.entries) bestFast |= e.op->name() == "y_fast";
+  CHECK(bestFast);
+  // schedules deserialize against the original (unexpanded) graph
+  OpIndex idx(*g);
+  Sequence back = idx.sequence_from_json(Json::parse(r.sims[0].seq.json().dump()));
+  CHECK(back.canonical_key() == r.sims[0].seq.canonical_key());
+}
+
+TEST(mcts_checkpoint_resume) {
+  auto g = diamond(10, 100, 100, 10);
+  SelfCtrl ctrl;
+  SimBenchmarker sb(2, SimParams());
+  MctsOpts o;
+  o.n_iters = 20;
+  o.bench.n_iters = 2;
+  o.checkpoint_path = "/tmp/tz_unit_ck.json";
+  SearchResult r1 = mcts_explore(*g, Platform::make_n_streams(2), sb, ctrl, o);
+  MctsOpts o2 = o;
+  o2.resume_path = o.checkpoint_path;
+  o2.checkpoint_path = "";
+  o2.n_iters = 30;
+  SearchResult r2 = mcts_explore(*g, Platform::make_n_streams(2), sb, ctrl, o2);
+  CHECK(r2.sims.size() >= r1.sims.size());
+  std::remove(o.checkpoint_path.c_str());
+}
+
+TEST(runs_test_behaviour) {
+  std::vector<double> alt, trend;
+  for (int i = 0; i < 40; ++i) {
+    alt.push_back(i % 2 ? 1.0 : 2.0);
+    trend.push_back(double(i));
+  }
+  CHECK(runs_test(trend));   // monotone trend: non-random
+  CHECK(runs_test(alt));     // perfectly alternating: non-random
+  std::vector<double> small{1, 2, 3};
+  CHECK(!runs_test(small, RunsTestSmall::Accept));
+  CHECK(runs_test(small, RunsTestSmall::Reject)); // reference behaviour
+  auto pf = prime_factors(24);
+  CHECK(pf.size() == 4 && pf[0] == 3 && pf[3] == 2);
+}
+
+int main(int argc, char **argv) {
+  const char *filter = argc > 1 ? argv[1] : nullptr;
+  int ran = 0;
+  for (auto &c : cases()) {
+    if (filter && !std::strstr(c.name, filter)) continue;
+    const int before = g_fail;
+    try {
+      c.fn();
+    } catch (const std::exception &e) {
+      ++g_fail;
+      std::fprintf(stderr, "  EXCEPTION in %s: %s\n", c.name, e.what());
+    }
+    std::fprintf(stderr, "[%s] %s\n", g_fail == before ? " ok " : "FAIL", c.name);
+    ++ran;
+  }
+  std::fprintf(stderr, "%d test cases, %d checks, %d failures\n", ran, g_checks, g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,395 @@
+#include "workloads.hpp"
+
+#include "core/numeric.hpp"
+#include "core/util.hpp"
+#include "hip/hip_runtime.hpp"
+#include "hip/rccl_comm.hpp"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+
+namespace tz {
+
+Json HaloArgs::json() const {
+  Json j;
+  j["nx"] = nx;
+  j["ny"] = ny;
+  j["nz"] = nz;
+  j["nq"] = nq;
+  j["ghost"] = ghost;
+  j["neighbors"] = neighbors;
+  j["order"] = order;
+  j["transport"] = transport;
+  j["fuse"] = fuse;
+  j["comms"] = comms;
+  j["rank"] = rank;
+  j["size"] = size;
+  j["px"] = px;
+  j["py"] = py;
+  j["pz"] = pz;
+  return j;
+}
+
+std::string HaloExchange::Dir::name() const {
+  return "dx" + std::to_string(dx) + "_dy" + std::to_string(dy) + "_dz" + std::to_string(dz);
+}
+
+namespace {
+
+// byte-cost model for the simulator: ~5 TB/s effective HBM stream + launch latency
+double copy_cost_us(double bytes) { return 3.0 + bytes / 5.0e6; }
+
+class HaloPack : public GpuOp {
+public:
+  HaloPack(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_pack_" + h_->dir(i_).name(); }
+  std::string kind() const override { return "HaloPack"; }
+  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
+  double cost_us() const override { return copy_cost_us(bytes()); }
+  void launch(void *s, Executor &) const override { h_->pack(i_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+class HaloUnpack : public GpuOp {
+public:
+  HaloUnpack(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_unpack_" + h_->dir(i_).name(); }
+  std::string kind() const override { return "HaloUnpack"; }
+  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
+  double cost_us() const override { return copy_cost_us(bytes()); }
+  void launch(void *s, Executor &) const override { h_->unpack(i_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+class HaloShift : public GpuOp {
+public:
+  HaloShift(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_shift_" + h_->dir(i_).name(); }
+  std::string kind() const override { return h_->uses_rccl() ? "HaloShift" : "HaloCopy"; }
+  double bytes() const override { return 8.0 * double(h_->box_elems(i_)); }
+  // xGMI link ~100 GB/s effective per direction + RCCL launch; self copy ~2.5 TB/s
+  double cost_us() const override {
+    return h_->uses_rccl() ? 8.0 + bytes() / 1.0e5 : 3.0 + bytes() / 2.5e6;
+  }
+  void launch(void *s, Executor &) const override { h_->shift(i_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+class HaloStageAll : public GpuOp {
+public:
+  enum Stage { Pack, Shift, Unpack };
+  HaloStageAll(std::shared_ptr<const HaloExchange> h, Stage st) : h_(std::move(h)), st_(st) {}
+  std::string name() const override {
+    return st_ == Pack ? "he_pack_all" : (st_ == Shift ? "he_shift_all" : "he_unpack_all");
+  }
+  std::string kind() const override {
+    return st_ == Pack ? "HaloPackAll" : (st_ == Shift ? "HaloShiftAll" : "HaloUnpackAll");
+  }
+  double bytes() const override {
+    return (st_ == Shift ? 1.0 : 2.0) * h_->exchange_bytes();
+  }
+  double cost_us() const override {
+    if (st_ == Shift) return h_->uses_rccl() ? 10.0 + bytes() / 3.0e5 : 3.0 + bytes() / 2.5e6;
+    return copy_cost_us(bytes());
+  }
+  void launch(void *s, Executor &) const override {
+    if (st_ == Pack) h_->pack_all(s);
+    else if (st_ == Shift) h_->shift_all(s);
+    else h_->unpack_all(s);
+  }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  Stage st_;
+};
+
+} // namespace
+
+HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
+  TZ_CHECK(a_.nx > 0 && a_.ny > 0 && a_.nz > 0 && a_.nq > 0 && a_.ghost > 0, "bad halo extents");
+  TZ_CHECK(a_.ghost <= a_.nx && a_.ghost <= a_.ny && a_.ghost <= a_.nz, "ghost wider than domain");
+  TZ_CHECK(a_.neighbors == 6 || a_.neighbors == 26, "neighbors must be 6 or 26");
+  TZ_CHECK(a_.order == "xyzq" || a_.order == "qxyz", "order must be xyzq or qxyz");
+  TZ_CHECK(a_.rank >= 0 && a_.rank < a_.size, "bad rank");
+
+  // rank grid: prime factors (descending) multiply the currently smallest dimension, ties to
+  // the later dimension (reference halo_run_strategy.hpp:80-98: 2 -> 1x1x2, 4 -> 1x2x2)
+  if (a_.px <= 0 || a_.py <= 0 || a_.pz <= 0) {
+    int d[3] = {1, 1, 1};
+    for (int64_t p : prime_factors(a_.size)) {
+      int best = 2;
+      for (int k = 2; k >= 0; --k)
+        if (d[k] < d[best]) best = k;
+      d[best] *= int(p);
+    }
+    a_.px = d[0];
+    a_.py = d[1];
+    a_.pz = d[2];
+  }
+  TZ_CHECK(a_.px * a_.py * a_.pz == a_.size, "rank grid does not match size");
+  cx_ = a_.rank % a_.px;
+  cy_ = (a_.rank / a_.px) % a_.py;
+  cz_ = a_.rank / (a_.px * a_.py);
+
+  for (int dz = -1; dz <= 1; ++dz)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int k = (dx != 0) + (dy != 0) + (dz != 0);
+        if (k == 0) continue;
+        if (a_.neighbors == 6 && k != 1) continue;
+        dirs_.push_back({dx, dy, dz});
+      }
+  for (size_t i = 0; i < dirs_.size(); ++i) {
+    for (size_t j = 0; j < dirs_.size(); ++j)
+      if (dirs_[j].dx == -dirs_[i].dx && dirs_[j].dy == -dirs_[i].dy && dirs_[j].dz == -dirs_[i].dz)
+        opp_.push_back(int(j));
+    nbr_.push_back(coord_to_rank(cx_ + dirs_[i].dx, cy_ + dirs_[i].dy, cz_ + dirs_[i].dz));
+  }
+
+  const int64_t X = a_.nx + 2 * a_.ghost, Y = a_.ny + 2 * a_.ghost, Z = a_.nz + 2 * a_.ghost;
+  if (a_.order == "xyzq") {
+    xoff_ = (8 - a_.ghost % 8) % 8;                 // interior rows start 64-B aligned
+    pitch_ = round_up(xoff_ + X, 16);                // rows are whole 128-B lines
+    sy_ = pitch_;
+    sz_ = pitch_ * Y;
+    sq_ = sz_ * Z;
+    gridElems_ = size_t(sq_ * a_.nq);
+  } else {
+    gridElems_ = size_t(X * Y * Z * a_.nq);
+  }
+  std::string t = a_.transport;
+  if (t == "auto") t = a_.size == 1 ? "copy" : "rccl";
+  if (t == "copy") {
+    for (int n : nbr_) TZ_CHECK(n == a_.rank, "copy transport needs self-neighbours (1 rank)");
+  } else {
+    TZ_CHECK(t == "rccl", "unknown transport " << a_.transport);
+  }
+  useRccl_ = t == "rccl";
+}
+
+HaloExchange::~HaloExchange() = default;
+
+int HaloExchange::coord_to_rank(int x, int y, int z) const {
+  auto w = [](int v, int n) { return ((v % n) + n) % n; };
+  return w(x, a_.px) + a_.px * (w(y, a_.py) + a_.py * w(z, a_.pz));
+}
+
+static void axis_range(int d, int n, int g, bool ghost, int &lo, int &ext) {
+  if (d == 0) {
+    lo = g;
+    ext = n;
+  } else if (d < 0) {
+    lo = ghost ? 0 : g;
+    ext = g;
+  } else {
+    lo = ghost ? n + g : n;
+    ext = g;
+  }
+}
+
+static kern::BoxDesc make_box(const HaloArgs &a, const HaloExchange::Dir &d, bool ghost,
+                              int64_t xoff, int64_t sy, int64_t sz, int64_t sq) {
+  int x0, ex, y0, ey, z0, ez;
+  axis_range(d.dx, a.nx, a.ghost, ghost, x0, ex);
+  axis_range(d.dy, a.ny, a.ghost, ghost, y0, ey);
+  axis_range(d.dz, a.nz, a.ghost, ghost, z0, ez);
+  kern::BoxDesc b;
+  if (a.order == "xyzq") {
+    b.grid_off = z0 * sz + y0 * sy + x0 + xoff;
+    b.len = ex;
+    b.n1 = ey;
+    b.n2 = ez;
+    b.n3 = a.nq;
+    b.s1 = sy;
+    b.s2 = sz;
+    b.s3 = sq;
+  } else {
+    const int64_t X = a.nx + 2 * a.ghost, Y = a.ny + 2 * a.ghost;
+    b.grid_off = int64_t(a.nq) * (x0 + X * (y0 + Y * int64_t(z0)));
+    b.len = a.nq * ex;
+    b.n1 = ey;
+    b.n2 = ez;
+    b.n3 = 1;
+    b.s1 = a.nq * X;
+    b.s2 = a.nq * X * Y;
+    b.s3 = 0;
+  }
+  return b;
+}
+
+kern::BoxDesc HaloExchange::pack_box(int i) const {
+  kern::BoxDesc b = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
+  if (!send_.empty()) b.buf = send_[i].as<double>();
+  return b;
+}
+
+kern::BoxDesc HaloExchange::unpack_box(int i) const {
+  kern::BoxDesc b = make_box(a_, dirs_[i], true, xoff_, sy_, sz_, sq_);
+  if (!recv_.empty()) b.buf = recv_[i].as<double>();
+  return b;
+}
+
+size_t HaloExchange::box_elems(int i) const {
+  kern::BoxDesc b = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
+  return size_t(b.len) * b.n1 * b.n2 * b.n3;
+}
+
+double HaloExchange::exchange_bytes() const {
+  double s = 0;
+  for (int i = 0; i < ndirs(); ++i) s += 8.0 * double(box_elems(i));
+  return s;
+}
+
+kern::HaloGeom HaloExchange::geom() const {
+  kern::HaloGeom g;
+  g.order = a_.order == "xyzq" ? 0 : 1;
+  g.xoff = xoff_;
+  g.sy = sy_;
+  g.sz = sz_;
+  g.sq = sq_;
+  g.nx = a_.nx;
+  g.ny = a_.ny;
+  g.nz = a_.nz;
+  g.nq = a_.nq;
+  g.g = a_.ghost;
+  g.cx = cx_;
+  g.cy = cy_;
+  g.cz = cz_;
+  g.px = a_.px;
+  g.py = a_.py;
+  g.pz = a_.pz;
+  g.neighbors = a_.neighbors;
+  return g;
+}
+
+void HaloExchange::setup(Ctrl *ctrl) {
+  if (ready()) return;
+  if (a_.device >= 0) TZ_HIP(hipSetDevice(a_.device));
+  grid_ = DeviceBuffer(gridElems_ * sizeof(double));
+  for (int i = 0; i < ndirs(); ++i) {
+    send_.emplace_back(box_elems(i) * sizeof(double));
+    recv_.emplace_back(box_elems(opp_[i]) * sizeof(double));
+  }
+  count_ = DeviceBuffer(sizeof(unsigned long long));
+  if (useRccl_) {
+    TZ_CHECK(ctrl && ctrl->size() == a_.size, "RCCL transport needs a control plane of size "
+                                                  << a_.size);
+    const int n = a_.comms > 0 ? std::min(a_.comms, ndirs()) : ndirs();
+    int dev = 0;
+    TZ_HIP(hipGetDevice(&dev));
+    comms_ = make_rccl_comms(*ctrl, dev, n);
+  }
+  init_grid();
+  TZ_HIP(hipDeviceSynchronize());
+}
+
+void HaloExchange::init_grid(void *stream) {
+  TZ_CHECK(ready(), "halo not set up");
+  kern::halo_init(grid(), geom(), stream);
+}
+
+uint64_t HaloExchange::check_grid(void *stream) {
+  TZ_CHECK(ready(), "halo not set up");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  TZ_HIP(hipMemsetAsync(count_.get(), 0, sizeof(unsigned long long), s));
+  kern::halo_check(grid(), geom(), count_.as<unsigned long long>(), stream);
+  unsigned long long n = 0;
+  TZ_HIP(hipMemcpyAsync(&n, count_.get(), sizeof(n), hipMemcpyDeviceToHost, s));
+  TZ_HIP(hipStreamSynchronize(s));
+  return n;
+}
+
+void HaloExchange::pack(int i, void *stream) const {
+  kern::box_copy(grid(), pack_box(i), false, stream);
+}
+
+void HaloExchange::unpack(int i, void *stream) const {
+  kern::box_copy(grid(), unpack_box(i), true, stream);
+}
+
+void HaloExchange::shift(int i, void *stream) const {
+  // send my slab facing d to nbr(d); receive nbr(-d)'s slab facing d into my ghost on side -d
+  const int o = opp_[i];
+  const size_t n = box_elems(i);
+  if (useRccl_) {
+    const RcclComm &c = *comms_[size_t(i) % comms_.size()];
+    c.sendrecv(send_[i].get(), n, nbr_[i], recv_[o].get(), n, nbr_[o], 1, stream);
+  } else {
+    TZ_HIP(hipMemcpyAsync(recv_[o].get(), send_[i].get(), n * sizeof(double),
+                          hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+  }
+}
+
+void HaloExchange::pack_all(void *stream) const {
+  std::vector<kern::BoxDesc> bs;
+  for (int i = 0; i < ndirs(); ++i) bs.push_back(pack_box(i));
+  for (size_t k = 0; k < bs.size(); k += kern::kMaxBoxes)
+    kern::box_copy_many(grid(), bs.data() + k, int(std::min<size_t>(kern::kMaxBoxes, bs.size() - k)),
+                        false, stream);
+}
+
+void HaloExchange::unpack_all(void *stream) const {
+  std::vector<kern::BoxDesc> bs;
+  for (int i = 0; i < ndirs(); ++i) bs.push_back(unpack_box(i));
+  for (size_t k = 0; k < bs.size(); k += kern::kMaxBoxes)
+    kern::box_copy_many(grid(), bs.data() + k, int(std::min<size_t>(kern::kMaxBoxes, bs.size() - k)),
+                        true, stream);
+}
+
+void HaloExchange::shift_all(void *stream) const {
+  if (useRccl_) {
+    std::vector<RcclComm::Xfer> xs;
+    for (int i = 0; i < ndirs(); ++i) {
+      const int o = opp_[i];
+      const size_t n = box_elems(i);
+      xs.push_back({send_[i].get(), n, nbr_[i], recv_[o].get(), n, nbr_[o]});
+    }
+    comms_[0]->exchange(xs, 1, stream);
+  } else {
+    for (int i = 0; i < ndirs(); ++i) shift(i, stream);
+  }
+}
+
+void HaloExchange::add_to_graph(Graph &g) {
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  const bool fusePack = a_.fuse == "pack" || a_.fuse == "all";
+  const bool fuseShift = a_.fuse == "all";
+  TZ_CHECK(a_.fuse == "none" || fusePack, "fuse must be none, pack or all");
+  OpPtr packAll, shiftAll, unpackAll;
+  if (fusePack) {
+    packAll = std::make_shared<HaloStageAll>(self, HaloStageAll::Pack);
+    unpackAll = std::make_shared<HaloStageAll>(self, HaloStageAll::Unpack);
+    g.start_then(packAll);
+    g.then_finish(unpackAll);
+  }
+  if (fuseShift) {
+    shiftAll = std::make_shared<HaloStageAll>(self, HaloStageAll::Shift);
+    g.then(packAll, shiftAll);
+    g.then(shiftAll, unpackAll);
+    return;
+  }
+  std::vector<OpPtr> packs, shifts, unpacks;
+  for (int i = 0; i < ndirs(); ++i) {
+    packs.push_back(fusePack ? packAll : std::make_shared<HaloPack>(self, i));
+    shifts.push_back(std::make_shared<HaloShift>(self, i));
+    unpacks.push_back(fusePack ? unpackAll : std::make_shared<HaloUnpack>(self, i));
+  }
+  for (int i = 0; i < ndirs(); ++i) {
+    if (!fusePack) g.start_then(packs[i]);
+    g.then(packs[i], shifts[i]);
+    g.then(shifts[i], unpacks[opp_[i]]);
+    if (!fusePack) g.then_finish(unpacks[opp_[i]]);
+  }
+}
+
+} // namespace tz

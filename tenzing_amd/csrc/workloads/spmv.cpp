@@ -1,0 +1,349 @@
+#include "workloads.hpp"
+
+#include "core/util.hpp"
+#include "hip/hip_runtime.hpp"
+#include "hip/rccl_comm.hpp"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <random>
+
+namespace tz {
+
+Json SpmvArgs::json() const {
+  Json j;
+  j["m"] = m;
+  j["bw"] = bw;
+  j["nnz"] = nnz;
+  j["seed"] = int64_t(seed);
+  j["rank"] = rank;
+  j["size"] = size;
+  j["compound"] = compound;
+  j["kernel_choice"] = kernel_choice;
+  return j;
+}
+
+CsrHost random_band_matrix(int64_t n, int64_t bw, int64_t nnz, uint64_t seed) {
+  TZ_CHECK(n > 0 && bw > 0 && nnz >= 0, "bad band matrix parameters");
+  std::mt19937_64 rng(seed);
+  std::vector<int64_t> keys;
+  keys.reserve(size_t(nnz));
+  for (int64_t k = 0; k < nnz; ++k) {
+    const int64_t r = int64_t(rng() % uint64_t(n));
+    const int64_t lo = std::max<int64_t>(0, r - bw + 1), hi = std::min<int64_t>(n - 1, r + bw - 1);
+    const int64_t c = lo + int64_t(rng() % uint64_t(hi - lo + 1));
+    keys.push_back(r * n + c);
+  }
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  CsrHost A;
+  A.rows = A.cols = n;
+  A.rowPtr.assign(size_t(n + 1), 0);
+  A.colInd.reserve(keys.size());
+  A.val.reserve(keys.size());
+  std::mt19937_64 vrng(seed ^ 0x9E3779B97F4A7C15ull);
+  std::uniform_real_distribution<float> u(-1.f, 1.f);
+  for (int64_t key : keys) {
+    const int64_t r = key / n, c = key % n;
+    A.rowPtr[size_t(r + 1)]++;
+    A.colInd.push_back(int32_t(c));
+    A.val.push_back(u(vrng));
+  }
+  for (int64_t r = 0; r < n; ++r) A.rowPtr[size_t(r + 1)] += A.rowPtr[size_t(r)];
+  return A;
+}
+
+std::pair<int64_t, int64_t> row_partition(int64_t n, int rank, int size) {
+  const int64_t base = n / size, rem = n % size;
+  const int64_t r0 = rank * base + std::min<int64_t>(rank, rem);
+  return {r0, r0 + base + (rank < rem ? 1 : 0)};
+}
+
+static int owner_of(int64_t col, int64_t n, int size) {
+  // inverse of row_partition
+  const int64_t base = n / size, rem = n % size;
+  const int64_t cut = rem * (base + 1);
+  if (col < cut) return int(col / (base + 1));
+  return int(rem + (col - cut) / std::max<int64_t>(base, 1));
+}
+
+static float x_value(int64_t g) { return float(int64_t((uint64_t(g) * 2654435761ull) % 2000ull) - 1000) / 1000.f; }
+
+namespace {
+
+class SpmvLocal : public GpuOp {
+public:
+  SpmvLocal(std::shared_ptr<const DistSpmv> s, std::string name, int lanes)
+      : s_(std::move(s)), name_(std::move(name)), lanes_(lanes) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "SpmvLocal"; }
+  double bytes() const override { return 12.0 * double(s_->local_nnz()) + 8.0 * double(s_->local_rows()); }
+  double cost_us() const override { return 4.0 + bytes() / 3.0e6; }
+  void launch(void *st, Executor &) const override { s_->spmv_local(lanes_, st); }
+
+private:
+  std::shared_ptr<const DistSpmv> s_;
+  std::string name_;
+  int lanes_;
+};
+
+class SpmvRemote : public GpuOp {
+public:
+  SpmvRemote(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "SpmvRemote"; }
+  double bytes() const override { return 12.0 * double(s_->remote_nnz()) + 8.0 * double(s_->local_rows()); }
+  double cost_us() const override { return 4.0 + bytes() / 3.0e6; }
+  void launch(void *st, Executor &) const override { s_->spmv_remote(st); }
+
+private:
+  std::shared_ptr<const DistSpmv> s_;
+  std::string name_;
+};
+
+class SpmvScatter : public GpuOp {
+public:
+  SpmvScatter(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "SpmvScatter"; }
+  double cost_us() const override { return 3.0 + 12.0 * double(s_->send_elems()) / 2.0e6; }
+  void launch(void *st, Executor &) const override { s_->scatter(st); }
+
+private:
+  std::shared_ptr<const DistSpmv> s_;
+  std::string name_;
+};
+
+class SpmvExchange : public GpuOp {
+public:
+  SpmvExchange(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "SpmvExchange"; }
+  double cost_us() const override { return s_->num_peers() ? 10.0 + 4.0 * double(s_->send_elems()) / 5.0e4 : 0.5; }
+  void launch(void *st, Executor &) const override { s_->exchange(st); }
+
+private:
+  std::shared_ptr<const DistSpmv> s_;
+  std::string name_;
+};
+
+class SpmvAdd : public GpuOp {
+public:
+  SpmvAdd(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "VectorAdd"; }
+  double cost_us() const override { return 3.0 + 12.0 * double(s_->local_rows()) / 4.0e6; }
+  void launch(void *st, Executor &) const override { s_->add(st); }
+
+private:
+  std::shared_ptr<const DistSpmv> s_;
+  std::string name_;
+};
+
+} // namespace
+
+DistSpmv::DistSpmv(SpmvArgs a) : a_(std::move(a)) {
+  TZ_CHECK(a_.size >= 1 && a_.rank >= 0 && a_.rank < a_.size, "bad rank/size");
+  const int64_t n = a_.m;
+  if (a_.bw <= 0) a_.bw = std::max<int64_t>(1, n / a_.size);
+  if (a_.nnz <= 0) a_.nnz = 10 * n;
+  const CsrHost A = random_band_matrix(n, a_.bw, a_.nnz, a_.seed);
+  std::tie(r0_, r1_) = row_partition(n, a_.rank, a_.size);
+
+  // split my rows into local (own x) and remote (others' x) blocks
+  std::vector<int64_t> rc;
+  for (int64_t r = r0_; r < r1_; ++r)
+    for (int32_t j = A.rowPtr[r]; j < A.rowPtr[r + 1]; ++j)
+      if (A.colInd[j] < r0_ || A.colInd[j] >= r1_) rc.push_back(A.colInd[j]);
+  std::sort(rc.begin(), rc.end());
+  rc.erase(std::unique(rc.begin(), rc.end()), rc.end());
+  remoteCols_ = rc;
+
+  const int64_t nl = r1_ - r0_;
+  local_.rows = remote_.rows = nl;
+  local_.cols = nl;
+  remote_.cols = int64_t(rc.size());
+  local_.rowPtr.assign(size_t(nl + 1), 0);
+  remote_.rowPtr.assign(size_t(nl + 1), 0);
+  yRef_.assign(size_t(nl), 0.0);
+  for (int64_t r = r0_; r < r1_; ++r) {
+    double acc = 0;
+    for (int32_t j = A.rowPtr[r]; j < A.rowPtr[r + 1]; ++j) {
+      const int64_t c = A.colInd[j];
+      acc += double(A.val[j]) * double(x_value(c));
+      if (c >= r0_ && c < r1_) {
+        local_.colInd.push_back(int32_t(c - r0_));
+        local_.val.push_back(A.val[j]);
+      } else {
+        const int64_t p = std::lower_bound(rc.begin(), rc.end(), c) - rc.begin();
+        remote_.colInd.push_back(int32_t(p));
+        remote_.val.push_back(A.val[j]);
+      }
+    }
+    yRef_[size_t(r - r0_)] = acc;
+    local_.rowPtr[size_t(r - r0_ + 1)] = int32_t(local_.colInd.size());
+    remote_.rowPtr[size_t(r - r0_ + 1)] = int32_t(remote_.colInd.size());
+  }
+
+  // receive plan: remote cols are sorted, hence grouped by owner
+  recvCount_.assign(size_t(a_.size), 0);
+  recvOff_.assign(size_t(a_.size), 0);
+  for (int64_t c : rc) recvCount_[size_t(owner_of(c, n, a_.size))]++;
+  for (int q = 1; q < a_.size; ++q) recvOff_[q] = recvOff_[q - 1] + recvCount_[q - 1];
+
+  // send plan: what every other rank q needs from my columns, in q's (sorted) order
+  sendCount_.assign(size_t(a_.size), 0);
+  sendOff_.assign(size_t(a_.size), 0);
+  for (int q = 0; q < a_.size; ++q) {
+    sendOff_[q] = int32_t(sendIdx_.size());
+    if (q == a_.rank) continue;
+    auto [q0, q1] = row_partition(n, q, a_.size);
+    std::vector<int64_t> need;
+    for (int64_t r = q0; r < q1; ++r)
+      for (int32_t j = A.rowPtr[r]; j < A.rowPtr[r + 1]; ++j)
+        if (A.colInd[j] >= r0_ && A.colInd[j] < r1_) need.push_back(A.colInd[j]);
+    std::sort(need.begin(), need.end());
+    need.erase(std::unique(need.begin(), need.end()), need.end());
+    for (int64_t c : need) sendIdx_.push_back(int32_t(c - r0_));
+    sendCount_[q] = int32_t(need.size());
+  }
+  xLocal_.resize(size_t(nl));
+  for (int64_t i = 0; i < nl; ++i) xLocal_[size_t(i)] = x_value(r0_ + i);
+  const double avg = nl ? double(local_.nnz() + remote_.nnz()) / double(nl) : 1;
+  lanes_ = avg > 24 ? 16 : (avg > 6 ? 8 : 4);
+}
+
+DistSpmv::~DistSpmv() = default;
+
+int DistSpmv::num_peers() const {
+  int n = 0;
+  for (int q = 0; q < a_.size; ++q) n += (recvCount_[q] > 0 || sendCount_[q] > 0);
+  return n;
+}
+
+void DistSpmv::setup(Ctrl *ctrl) {
+  if (ready()) return;
+  if (a_.device >= 0) TZ_HIP(hipSetDevice(a_.device));
+  auto up = [](DeviceBuffer &d, const void *p, size_t bytes) {
+    d = DeviceBuffer(std::max<size_t>(bytes, 16));
+    d.upload(p, bytes);
+  };
+  up(dLocalRow_, local_.rowPtr.data(), local_.rowPtr.size() * 4);
+  up(dLocalCol_, local_.colInd.data(), local_.colInd.size() * 4);
+  up(dLocalVal_, local_.val.data(), local_.val.size() * 4);
+  up(dRemoteRow_, remote_.rowPtr.data(), remote_.rowPtr.size() * 4);
+  up(dRemoteCol_, remote_.colInd.data(), remote_.colInd.size() * 4);
+  up(dRemoteVal_, remote_.val.data(), remote_.val.size() * 4);
+  up(dX_, xLocal_.data(), xLocal_.size() * 4);
+  up(dSendIdx_, sendIdx_.data(), sendIdx_.size() * 4);
+  const size_t nl = size_t(local_rows());
+  dSend_ = DeviceBuffer(std::max<size_t>(sendIdx_.size() * 4, 16));
+  dXr_ = DeviceBuffer(std::max<size_t>(remoteCols_.size() * 4, 16));
+  dYl_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));
+  dYr_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));
+  dY_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));
+  TZ_HIP(hipMemset(dYr_.get(), 0, dYr_.bytes()));
+  if (a_.size > 1) {
+    TZ_CHECK(ctrl && ctrl->size() == a_.size, "SpMV needs a control plane of size " << a_.size);
+    int dev = 0;
+    TZ_HIP(hipGetDevice(&dev));
+    comm_ = std::make_shared<RcclComm>(*ctrl, dev);
+  }
+  TZ_HIP(hipDeviceSynchronize());
+}
+
+void DistSpmv::reset_y(void *stream) {
+  TZ_HIP(hipMemsetAsync(dY_.get(), 0, dY_.bytes(), static_cast<hipStream_t>(stream)));
+}
+
+double DistSpmv::check(void *stream) {
+  TZ_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  std::vector<float> y(static_cast<size_t>(local_rows()));
+  dY_.download(y.data(), y.size() * 4);
+  double err = 0;
+  for (size_t i = 0; i < y.size(); ++i)
+    err = std::max(err, std::abs(double(y[i]) - yRef_[i]) / std::max(1.0, std::abs(yRef_[i])));
+  return err;
+}
+
+void DistSpmv::scatter(void *stream) const {
+  kern::gather_f32(int(sendIdx_.size()), dX_.as<float>(), dSendIdx_.as<int32_t>(), dSend_.as<float>(), stream);
+}
+
+void DistSpmv::exchange(void *stream) const {
+  if (!comm_) return;
+  std::vector<RcclComm::Xfer> xs;
+  for (int q = 0; q < a_.size; ++q) {
+    if (q == a_.rank || (sendCount_[q] == 0 && recvCount_[q] == 0)) continue;
+    RcclComm::Xfer x;
+    x.send = dSend_.as<float>() + sendOff_[q];
+    x.sendCount = size_t(sendCount_[q]);
+    x.sendPeer = q;
+    x.recv = dXr_.as<float>() + recvOff_[q];
+    x.recvCount = size_t(recvCount_[q]);
+    x.recvPeer = q;
+    xs.push_back(x);
+  }
+  comm_->exchange(xs, 0, stream);
+}
+
+void DistSpmv::spmv_local(int lanes, void *stream) const {
+  kern::csr_spmv(int(local_rows()), dLocalRow_.as<int32_t>(), dLocalCol_.as<int32_t>(),
+                 dLocalVal_.as<float>(), dX_.as<float>(), dYl_.as<float>(), lanes > 0 ? lanes : lanes_,
+                 false, stream);
+}
+
+void DistSpmv::spmv_remote(void *stream) const {
+  kern::csr_spmv(int(local_rows()), dRemoteRow_.as<int32_t>(), dRemoteCol_.as<int32_t>(),
+                 dRemoteVal_.as<float>(), dXr_.as<float>(), dYr_.as<float>(), lanes_, false, stream);
+}
+
+void DistSpmv::add(void *stream) const {
+  kern::vector_add_f32(int(local_rows()), dYl_.as<float>(), dYr_.as<float>(), dY_.as<float>(), stream);
+}
+
+std::shared_ptr<const Graph> DistSpmv::op_graph() {
+  if (inner_) return inner_;
+  auto self = std::const_pointer_cast<const DistSpmv>(shared_from_this());
+  const std::string p = a_.prefix;
+  auto g = std::make_shared<Graph>();
+  OpPtr yl;
+  if (a_.kernel_choice) {
+    std::vector<OpPtr> ch;
+    for (int w : {4, 8, 16}) ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w));
+    yl = std::make_shared<StaticChoiceOp>(p + "yl", ch);
+  } else {
+    yl = std::make_shared<SpmvLocal>(self, p + "yl", 0);
+  }
+  auto scatter = std::make_shared<SpmvScatter>(self, p + "Pack");
+  auto xchg = std::make_shared<SpmvExchange>(self, p + "exchange");
+  auto yr = std::make_shared<SpmvRemote>(self, p + "yr");
+  auto y = std::make_shared<SpmvAdd>(self, p + "y");
+  g->start_then(yl);
+  g->start_then(scatter);
+  g->then(scatter, xchg);
+  g->then(xchg, yr);
+  g->then(yl, y);
+  g->then(yr, y);
+  g->then_finish(y);
+  inner_ = g;
+  return inner_;
+}
+
+void DistSpmv::add_to_graph(Graph &g) {
+  auto inner = op_graph();
+  if (a_.compound) {
+    auto c = std::make_shared<StaticCompoundOp>(a_.prefix + "spmv", inner);
+    g.start_then(c);
+    g.then_finish(c);
+  } else {
+    // splice the inner graph into g
+    for (int v : inner->vertices()) {
+      for (int s : inner->succs(v)) g.then(inner->op(v), inner->op(s));
+    }
+  }
+}
+
+} // namespace tz

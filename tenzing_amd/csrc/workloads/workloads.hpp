@@ -1,0 +1,242 @@
+// Workload op libraries ("model families"): 3-D halo exchange and distributed CSR SpMV, plus
+// small generic GPU ops for user-built graphs.
+//
+// Parity:
+//   halo: include/tenzing/halo_exchange/ops_halo_exchange.hpp:22-186,
+//         src/halo_exchange/ops_halo_exchange.cu:33-257 (HaloExchange::add_to_graph, Pack,
+//         Unpack, OwningIsend/OwningIrecv, MultiWait), tenzing-mcts/examples/
+//         halo_run_strategy.hpp:42-131 (config, rank grid from prime factors, coord maps)
+//   spmv: include/tenzing/spmv/ops_spmv.cuh:61-436 (SpMVKernel, Scatter, VectorAdd, PostSend/
+//         PostRecv/WaitSend/WaitRecv, SpMV CompoundOp), row_part_spmv.cuh:105-445 (RowPartSpmv),
+//         csr_mat.hpp:301-370 (random band matrix), partition.hpp, split_mat.hpp
+// MI355X redesign:
+//   * halo: per direction d a chain Pack(d) -> Shift(d) -> Unpack(-d). Shift is one grouped
+//     RCCL send(S_d -> nbr(d)) + recv(R_-d <- nbr(-d)) on direction d's communicator (the MPI
+//     Isend/Irecv/Wait triple of the reference collapses into one stream-ordered op; no host
+//     round trip between pack and send). Faces (6) or faces+edges+corners (26, 27-point stencil).
+//     Optional fused variants pack/shift/unpack every direction in one op. Single rank: Shift is
+//     a device-to-device copy (periodic self-neighbour) unless RCCL is forced.
+//     Grid layout is x-padded so interior rows start 64-byte aligned (dwordx4 pack/unpack).
+//   * spmv: the matrix is generated deterministically on every rank (no setup communication);
+//     the compound op holds Scatter -> Exchange (one grouped RCCL exchange with every peer) ->
+//     remote SpMV, local SpMV (a ChoiceOp over lanes-per-row variants), and a real VectorAdd.
+#pragma once
+
+#include "core/ctrl.hpp"
+#include "core/graph.hpp"
+#include "kernels/kernels.hpp"
+
+#include <array>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace tz {
+
+class RcclComm;
+
+/// hipMalloc'd memory (RAII)
+class DeviceBuffer {
+public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(size_t bytes);
+  ~DeviceBuffer();
+  DeviceBuffer(DeviceBuffer &&o) noexcept : p_(o.p_), bytes_(o.bytes_) {
+    o.p_ = nullptr;
+    o.bytes_ = 0;
+  }
+  DeviceBuffer &operator=(DeviceBuffer &&o) noexcept;
+  DeviceBuffer(const DeviceBuffer &) = delete;
+  DeviceBuffer &operator=(const DeviceBuffer &) = delete;
+  void *get() const { return p_; }
+  template <typename T> T *as() const { return static_cast<T *>(p_); }
+  size_t bytes() const { return bytes_; }
+  void upload(const void *src, size_t bytes);
+  void download(void *dst, size_t bytes) const;
+
+private:
+  void *p_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+// ------------------------------------------------------------------ generic GPU ops
+
+/// launches an empty kernel (reference test/test_gpu_graph.cu KernelOp)
+class EmptyKernelOp : public GpuOp {
+public:
+  explicit EmptyKernelOp(std::string name) : name_(std::move(name)) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "EmptyKernel"; }
+  double cost_us() const override { return 2.0; }
+  void launch(void *stream, Executor &) const override;
+
+private:
+  std::string name_;
+};
+
+/// a kernel that occupies `blocks` workgroups for `us` microseconds
+class BusyKernelOp : public GpuOp {
+public:
+  BusyKernelOp(std::string name, double us, int blocks = 1)
+      : name_(std::move(name)), us_(us), blocks_(blocks) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "BusyKernel"; }
+  double cost_us() const override { return us_; }
+  Json json() const override;
+  void launch(void *stream, Executor &) const override;
+
+private:
+  std::string name_;
+  double us_;
+  int blocks_;
+};
+
+// ------------------------------------------------------------------ halo exchange
+
+struct HaloArgs {
+  int nx = 512, ny = 512, nz = 512, nq = 3, ghost = 3;
+  int neighbors = 6;              // 6 (faces) or 26 (faces, edges, corners)
+  std::string order = "xyzq";     // "xyzq" (x fastest, q slowest) or "qxyz"
+  std::string transport = "auto"; // "rccl", "copy" (self-neighbour only), "auto"
+  std::string fuse = "none";      // "none", "pack" (fused pack+unpack), "all" (one op each stage)
+  int comms = 0;                  // RCCL communicators (0 = one per direction)
+  int rank = 0, size = 1;
+  int px = 0, py = 0, pz = 0;     // rank grid (0 = from prime factors, reference style)
+  int device = -1;
+  Json json() const;
+};
+
+class HaloExchange : public std::enable_shared_from_this<HaloExchange> {
+public:
+  struct Dir {
+    int dx, dy, dz;
+    std::string name() const;
+  };
+
+  explicit HaloExchange(HaloArgs a);
+  ~HaloExchange();
+
+  const HaloArgs &args() const { return a_; }
+  int ndirs() const { return int(dirs_.size()); }
+  const Dir &dir(int i) const { return dirs_[i]; }
+  int opposite(int i) const { return opp_[i]; }
+  int neighbor(int i) const { return nbr_[i]; }
+  std::array<int, 3> coords() const { return {cx_, cy_, cz_}; }
+  std::array<int, 3> rank_grid() const { return {a_.px, a_.py, a_.pz}; }
+  int coord_to_rank(int x, int y, int z) const;
+  kern::BoxDesc pack_box(int i) const;   // interior slab facing direction i (buf filled later)
+  kern::BoxDesc unpack_box(int i) const; // ghost region on side i
+  size_t box_elems(int i) const;
+  size_t grid_elems() const { return gridElems_; }
+  double exchange_bytes() const; // bytes sent per exchange by this rank
+  kern::HaloGeom geom() const;
+
+  /// allocate device memory and (for RCCL) communicators; collective over ctrl when size > 1
+  void setup(Ctrl *ctrl);
+  bool ready() const { return grid_.get() != nullptr; }
+  /// add the exchange's ops and edges to g (Start -> packs ... unpacks -> Finish)
+  void add_to_graph(Graph &g);
+
+  // device data
+  double *grid() const { return grid_.as<double>(); }
+  void init_grid(void *stream = nullptr);
+  /// number of wrong elements after an exchange (0 = all ghosts correct, interior untouched)
+  uint64_t check_grid(void *stream = nullptr);
+
+  // op bodies
+  void pack(int i, void *stream) const;
+  void unpack(int i, void *stream) const;
+  void shift(int i, void *stream) const;
+  void pack_all(void *stream) const;
+  void unpack_all(void *stream) const;
+  void shift_all(void *stream) const;
+  bool uses_rccl() const { return useRccl_; }
+
+private:
+  HaloArgs a_;
+  std::vector<Dir> dirs_;
+  std::vector<int> opp_, nbr_;
+  int cx_ = 0, cy_ = 0, cz_ = 0;
+  int64_t xoff_ = 0, pitch_ = 0, sy_ = 0, sz_ = 0, sq_ = 0;
+  size_t gridElems_ = 0;
+  bool useRccl_ = false;
+  DeviceBuffer grid_;
+  std::vector<DeviceBuffer> send_, recv_;
+  std::vector<std::shared_ptr<RcclComm>> comms_;
+  DeviceBuffer count_;
+};
+
+// ------------------------------------------------------------------ distributed SpMV
+
+struct CsrHost {
+  int64_t rows = 0, cols = 0;
+  std::vector<int32_t> rowPtr, colInd;
+  std::vector<float> val;
+  int64_t nnz() const { return int64_t(colInd.size()); }
+};
+
+/// deterministic random band matrix: `nnz` entries with |row - col| < bw, values in [-1,1)
+/// (reference csr_mat.hpp:334-370 uses rand() and all-ones values)
+CsrHost random_band_matrix(int64_t n, int64_t bw, int64_t nnz, uint64_t seed);
+/// rows [r0, r1) owned by rank (remainder to low ranks, reference partition.hpp:21-76)
+std::pair<int64_t, int64_t> row_partition(int64_t n, int rank, int size);
+
+struct SpmvArgs {
+  int64_t m = 150000;
+  int64_t bw = 0;  // 0 = m / size (reference spmv_run_strategy.cuh:67)
+  int64_t nnz = 0; // 0 = 10 * m
+  uint64_t seed = 1;
+  int rank = 0, size = 1;
+  int device = -1;
+  bool compound = true;     // wrap in an expandable CompoundOp (reference SpMV CompoundOp)
+  bool kernel_choice = true; // local SpMV as a ChoiceOp over lanes-per-row variants
+  std::string prefix = "";  // op-name prefix (to combine several workloads in one graph)
+  Json json() const;
+};
+
+class DistSpmv : public std::enable_shared_from_this<DistSpmv> {
+public:
+  explicit DistSpmv(SpmvArgs a);
+  ~DistSpmv();
+  const SpmvArgs &args() const { return a_; }
+  int64_t local_rows() const { return r1_ - r0_; }
+  int64_t local_nnz() const { return local_.nnz(); }
+  int64_t remote_nnz() const { return remote_.nnz(); }
+  int64_t remote_cols() const { return int64_t(remoteCols_.size()); }
+  int64_t send_elems() const { return int64_t(sendIdx_.size()); }
+  int num_peers() const;
+
+  void setup(Ctrl *ctrl);
+  bool ready() const { return dLocalRow_.get() != nullptr; }
+  void add_to_graph(Graph &g);
+  std::shared_ptr<const Graph> op_graph(); // the compound op's inner graph
+
+  /// max |y - y_ref| / max(1,|y_ref|) over local rows after a run
+  double check(void *stream = nullptr);
+  void reset_y(void *stream = nullptr);
+
+  // op bodies
+  void scatter(void *stream) const;
+  void exchange(void *stream) const;
+  void spmv_local(int lanes, void *stream) const;
+  void spmv_remote(void *stream) const;
+  void add(void *stream) const;
+
+private:
+  SpmvArgs a_;
+  int64_t r0_ = 0, r1_ = 0;
+  CsrHost local_, remote_;
+  std::vector<int64_t> remoteCols_;          // global col of each remote x entry
+  std::vector<int32_t> recvCount_, recvOff_; // per peer, into x_remote
+  std::vector<int32_t> sendCount_, sendOff_; // per peer, into send buffer
+  std::vector<int32_t> sendIdx_;             // local x index of each send entry
+  std::vector<float> xLocal_;
+  std::vector<double> yRef_;
+  int lanes_ = 8;
+  DeviceBuffer dLocalRow_, dLocalCol_, dLocalVal_, dRemoteRow_, dRemoteCol_, dRemoteVal_;
+  DeviceBuffer dX_, dXr_, dSendIdx_, dSend_, dYl_, dYr_, dY_;
+  std::shared_ptr<RcclComm> comm_;
+  std::shared_ptr<const Graph> inner_;
+};
+
+} // namespace tz

@@ -1,0 +1,54 @@
+"""3-D halo exchange workload.
+
+Reference driver config (tenzing-mcts/examples/halo_run_strategy.hpp:42-49): nQ=3,
+nX=nY=nZ=512, nGhost=3, XYZQ storage, 6 face neighbours, 2 streams. BASELINE.json's headline
+adds the 27-point stencil (26 neighbours) and 4 streams per rank on 8 GPUs.
+
+Graph per direction d: ``he_pack_<d> -> he_shift_<d> -> he_unpack_<-d>`` (see
+csrc/workloads/workloads.hpp for the RCCL design).
+"""
+from __future__ import annotations
+
+import dataclasses
+
+from .. import _tz
+
+
+@dataclasses.dataclass
+class HaloConfig:
+    n: int = 512          # interior cells per rank per axis (nX = nY = nZ)
+    nq: int = 3           # quantities per cell
+    ghost: int = 3        # ghost width
+    neighbors: int = 26   # 6 = faces, 26 = faces + edges + corners (27-point stencil)
+    order: str = "xyzq"   # storage order
+    transport: str = "auto"  # rccl | copy | auto
+    fuse: str = "none"    # none | pack | all
+    comms: int = 0        # RCCL communicators (0 = one per direction)
+
+    def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":
+        a = _tz.HaloArgs()
+        a.nx = a.ny = a.nz = self.n
+        a.nq = self.nq
+        a.ghost = self.ghost
+        a.neighbors = self.neighbors
+        a.order = self.order
+        a.transport = self.transport
+        a.fuse = self.fuse
+        a.comms = self.comms
+        a.rank, a.size, a.device = rank, size, device
+        return a
+
+
+def build_halo(cfg: HaloConfig, ctrl=None, device: int = -1, setup: bool = True, graph=None):
+    """Create the halo workload for this rank and add it to ``graph`` (new graph if None).
+
+    ``setup=False`` builds the op graph only (no GPU needed: simulated / replayed searches).
+    Returns (halo, graph)."""
+    rank = ctrl.rank if ctrl is not None else 0
+    size = ctrl.size if ctrl is not None else 1
+    h = _tz.HaloExchange(cfg.args(rank, size, device))
+    if setup:
+        h.setup(ctrl)
+    g = graph if graph is not None else _tz.Graph()
+    h.add_to_graph(g)
+    return h, g

@@ -1,0 +1,74 @@
+"""Multi-process bootstrap.
+
+One process per GPU (``torchrun --nproc-per-node N``; RANK / WORLD_SIZE / LOCAL_RANK /
+MASTER_ADDR / MASTER_PORT from the environment). The launcher's rendezvous (torch.distributed
+with the gloo backend) is used exactly once: rank 0 opens the native TCP control-plane listener on
+an ephemeral port and broadcasts the port; every rank then joins the native star
+(``tenzing_amd._tz.TcpCtrl``). RCCL communicators for the data plane are created later by the
+workloads, with their unique ids broadcast over that control plane.
+
+Reference: MPI_Init + MPI_COMM_WORLD everywhere (tenzing-mcts/examples/halo_min_time.cu:11,
+spmv_run_strategy.cuh:81-90 rank -> device = rank % ndev).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+
+from .. import _tz
+
+
+@dataclasses.dataclass
+class DistEnv:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    master_addr: str = "127.0.0.1"
+    master_port: int = 29500
+
+
+def env() -> DistEnv:
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    return DistEnv(rank, world, local, os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   int(os.environ.get("MASTER_PORT", 29500)))
+
+
+def init_ctrl(rank: int | None = None, world: int | None = None, master_addr: str | None = None,
+              timeout_s: float = 300.0) -> "_tz.Ctrl":
+    """Create the native control plane for this process (SelfCtrl for a single process)."""
+    e = env()
+    rank = e.rank if rank is None else rank
+    world = e.world if world is None else world
+    _tz.set_log_rank(rank)
+    if world == 1:
+        return _tz.SelfCtrl()
+    import datetime
+
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    ctrl = _tz.TcpCtrl(rank, world)
+    port = ctrl.listen(0) if rank == 0 else 0
+    box = [port]
+    dist.broadcast_object_list(box, src=0)
+    ctrl.connect(master_addr or e.master_addr, int(box[0]), timeout_s)
+    return ctrl
+
+
+def select_device(local_rank: int | None = None) -> int:
+    """Bind this process to GPU ``local_rank % device_count`` (-1 when no GPU is visible)."""
+    n = _tz.hip_device_count()
+    if n == 0:
+        return -1
+    lr = env().local_rank if local_rank is None else local_rank
+    return lr % n
+
+
+def init(timeout_s: float = 300.0):
+    """(ctrl, device) for this process."""
+    ctrl = init_ctrl(timeout_s=timeout_s)
+    return ctrl, select_device()

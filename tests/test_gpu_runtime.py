@@ -1,0 +1,162 @@
+"""HIP runtime, workloads and solvers on a real MI355X (1 GPU)."""
+import json
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _small_halo(tz, neighbors=26, fuse="none", order="xyzq", transport="auto", n=24):
+    from tenzing_amd.models import HaloConfig, build_halo
+
+    cfg = HaloConfig(n=n, neighbors=neighbors, fuse=fuse, order=order, transport=transport)
+    return build_halo(cfg, tz.SelfCtrl(), device=0)
+
+
+def test_device_and_native_loaded(tz, gpu):
+    rt = tz.HipRuntime(device=0, n_streams=2)
+    assert "gfx950" in rt.device_name()
+    assert tz.native_loaded().endswith(".so")
+
+
+def test_gpu_graph_decisions_real_streams(tz, gpu):
+    """reference test/test_gpu_graph.cu:41-118 with real HIP streams and an empty kernel."""
+    g = tz.Graph()
+    k1, k2, k3 = (tz.EmptyKernelOp(f"kernel{i}") for i in (1, 2, 3))
+    g.start_then(k1)
+    g.then(k1, k2)
+    g.then(k1, k3)
+    g.then_finish(k2)
+    g.then_finish(k3)
+    plat = tz.Platform(2, symmetric_streams=False)
+    s = tz.State(g, plat)
+    ds = s.get_decisions()
+    assert sorted(d.stream for d in ds if d.kind == "Assign") == [0, 1]
+    seqs = tz.get_all_sequences(g, tz.Platform(2))
+    rt = tz.HipRuntime(device=0, n_streams=2)
+    for seq in seqs:
+        rt.prepare(seq)
+        rt.run(3)
+    rt.device_sync()
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+@pytest.mark.parametrize("fuse", ["none", "pack", "all"])
+@pytest.mark.parametrize("neighbors", [6, 26])
+def test_halo_exchange_correct(tz, gpu, mode, fuse, neighbors):
+    halo, g = _small_halo(tz, neighbors=neighbors, fuse=fuse)
+    m = tz.ExecMode.Graph if mode == "graph" else tz.ExecMode.Eager
+    rt = tz.HipRuntime(device=0, n_streams=3, mode=m)
+    for seed in range(3):
+        seq = tz.random_rollout(tz.State(g, tz.Platform(3)), seed)
+        seq, _ = tz.remove_redundant_syncs(seq, _final_graph(tz, g), 3)
+        halo.init_grid()
+        rt.device_sync()
+        assert halo.check_grid() > 0  # ghosts not yet filled
+        rt.prepare(seq)
+        assert rt.effective_mode == m
+        rt.run(1)
+        rt.device_sync()
+        assert halo.check_grid() == 0, seq.desc()
+
+
+def _final_graph(tz, g):
+    g2 = g.clone()
+    g2.normalize()
+    return g2
+
+
+def test_halo_qxyz_order(tz, gpu):
+    halo, g = _small_halo(tz, neighbors=26, order="qxyz")
+    rt = tz.HipRuntime(device=0, n_streams=2)
+    seq = tz.random_rollout(tz.State(g, tz.Platform(2)), 1)
+    halo.init_grid()
+    rt.prepare(seq)
+    rt.run(2)
+    rt.device_sync()
+    assert halo.check_grid() == 0
+
+
+def test_halo_rccl_self_exchange(tz, gpu):
+    """RCCL transport on a 1-rank communicator (self send/recv in a group)."""
+    halo, g = _small_halo(tz, neighbors=6, transport="rccl")
+    assert halo.uses_rccl()
+    for m in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+        rt = tz.HipRuntime(device=0, n_streams=2, mode=m)
+        seq = tz.random_rollout(tz.State(g, tz.Platform(2)), 4)
+        halo.init_grid()
+        rt.prepare(seq)
+        rt.run(1)
+        rt.device_sync()
+        assert halo.check_grid() == 0
+
+
+def test_spmv_workload_correct(tz, gpu):
+    from tenzing_amd.models import SpmvConfig, build_spmv
+
+    sp, g = build_spmv(SpmvConfig(m=20000), tz.SelfCtrl(), device=0)
+    rt = tz.HipRuntime(device=0, n_streams=2)
+    seqs = tz.get_all_sequences(g, tz.Platform(2), max_seqs=40)
+    assert len(seqs) >= 4
+    for m in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+        rt.set_mode(m)
+        for seq in seqs[:10]:
+            sp.reset_y()
+            rt.prepare(seq)
+            rt.run(1)
+            rt.device_sync()
+            assert sp.check() < 1e-4
+
+
+def test_mcts_halo_on_gpu(tz, gpu):
+    halo, g = _small_halo(tz, neighbors=6, n=64)
+    rt = tz.HipRuntime(device=0, n_streams=2, watchdog_s=60.0)
+    ctrl = tz.SelfCtrl()
+    bench = tz.EmpiricalBenchmarker(rt, ctrl)
+    o = tz.MctsOpts()
+    o.n_iters = 8
+    o.bench = tz.BenchOpts(n_iters=5, max_retries=1, target_secs=0.001)
+    res = tz.mcts_explore(g, tz.Platform(2), bench, ctrl, o)
+    assert len(res.sims) == 8
+    best = res.sims[res.best()]
+    assert 0 < best.res.pct10 < 0.01
+    csv = res.dump_csv().splitlines()
+    assert json.loads(csv[0])["mcts__Opts"]["nIters"] == 8
+    assert len(csv) == 9
+
+
+def test_dfs_spmv_on_gpu(tz, gpu):
+    """BASELINE config 2: CSR SpMV op-graph on 1 MI355X, DFS over 2 HIP streams."""
+    from tenzing_amd.models import SpmvConfig, build_spmv
+
+    sp, g = build_spmv(SpmvConfig(m=150_000), tz.SelfCtrl(), device=0)
+    rt = tz.HipRuntime(device=0, n_streams=2)
+    o = tz.DfsOpts()
+    o.max_seqs = 30
+    o.bench = tz.BenchOpts(n_iters=3, max_retries=1, target_secs=0.001)
+    res = tz.dfs_explore(g, tz.Platform(2), tz.EmpiricalBenchmarker(rt, tz.SelfCtrl()), tz.SelfCtrl(), o)
+    assert len(res.sims) == 30
+    assert min(s.res.pct10 for s in res.sims) > 0
+
+
+def test_pygpuop_torch_on_schedule_stream(tz, gpu):
+    torch = pytest.importorskip("torch")
+    x = torch.zeros(1 << 20, device="cuda")
+
+    def add_one(stream_ptr):
+        s = torch.cuda.ExternalStream(stream_ptr)
+        with torch.cuda.stream(s):
+            x.add_(1.0)
+
+    g = tz.Graph()
+    a = tz.PyGpuOp("a", add_one, 5.0, False)
+    b = tz.PyGpuOp("b", add_one, 5.0, False)
+    g.start_then(a)
+    g.then(a, b)
+    g.then_finish(b)
+    rt = tz.HipRuntime(device=0, n_streams=2)
+    seq = tz.random_rollout(tz.State(g, tz.Platform(2)), 0)
+    rt.prepare(seq)
+    rt.run(3)
+    rt.device_sync()
+    assert float(x[0]) == 6.0
