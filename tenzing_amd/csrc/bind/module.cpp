@@ -12,7 +12,11 @@
 #include "kernels/kernels.hpp"
 #include "workloads/workloads.hpp"
 
+#include <csignal>
+#include <cstdlib>
+#include <execinfo.h>
 #include <sstream>
+#include <unistd.h>
 
 namespace py = pybind11;
 using namespace tz;
@@ -106,10 +110,39 @@ py::dict box_to_dict(const kern::BoxDesc &b) {
 
 void *P(uintptr_t p) { return reinterpret_cast<void *>(p); }
 
+// native backtrace on a fatal signal, then chain to the previous handler (Python faulthandler)
+struct sigaction g_prevSegv, g_prevAbrt;
+void crash_handler(int sig, siginfo_t *si, void *uc) {
+  void *frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "\n[tz] fatal signal in native code, backtrace:\n";
+  ssize_t w = write(2, msg, sizeof(msg) - 1);
+  (void)w;
+  backtrace_symbols_fd(frames, n, 2);
+  struct sigaction &prev = sig == SIGSEGV ? g_prevSegv : g_prevAbrt;
+  sigaction(sig, &prev, nullptr);
+  if (prev.sa_flags & SA_SIGINFO) {
+    if (prev.sa_sigaction) prev.sa_sigaction(sig, si, uc);
+  } else if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN) {
+    prev.sa_handler(sig);
+  }
+  raise(sig);
+}
+void install_crash_handler() {
+  if (std::getenv("TZ_NO_CRASH_TRACE")) return;
+  struct sigaction sa {};
+  sa.sa_sigaction = crash_handler;
+  sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prevSegv);
+  sigaction(SIGABRT, &sa, &g_prevAbrt);
+}
+
 } // namespace
 
 PYBIND11_MODULE(_tz, m) {
   m.doc() = "tenzing_amd native core: schedule search over HIP streams / RCCL on MI355X";
+  install_crash_handler();
 
   py::register_exception<tz::Error>(m, "TzError");
   m.def("version", &version_string);
@@ -351,7 +384,7 @@ PYBIND11_MODULE(_tz, m) {
   py::class_<ExecutorRunner>(m, "ExecutorRunner")
       .def("prepare", &ExecutorRunner::prepare, py::call_guard<py::gil_scoped_release>())
       .def("run", &ExecutorRunner::run, py::call_guard<py::gil_scoped_release>());
-  py::class_<HostExecutor, ExecutorRunner>(m, "HostExecutor").def(py::init<int>());
+  py::class_<HostExecutor, ExecutorRunner>(m, "HostExecutor", py::multiple_inheritance()).def(py::init<int>());
   py::class_<EmpiricalBenchmarker, Benchmarker>(m, "EmpiricalBenchmarker")
       .def(py::init<ExecutorRunner &, Ctrl &>(), py::keep_alive<1, 2>(), py::keep_alive<1, 3>());
 
@@ -480,7 +513,7 @@ PYBIND11_MODULE(_tz, m) {
 
   // ------------------------------------------------------------------ HIP runtime
   py::enum_<ExecMode>(m, "ExecMode").value("Eager", ExecMode::Eager).value("Graph", ExecMode::Graph);
-  py::class_<HipRuntime, ExecutorRunner>(m, "HipRuntime")
+  py::class_<HipRuntime, ExecutorRunner>(m, "HipRuntime", py::multiple_inheritance())
       .def(py::init([](int device, int n, std::vector<int> prio, bool cu, ExecMode mode, double wd) {
         HipRuntimeOpts o;
         o.device = device;

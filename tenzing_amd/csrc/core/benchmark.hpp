@@ -70,7 +70,7 @@ private:
 };
 
 /// Host-only executor: GPU ops are launched with a null stream, synchronously (tests/CPU runs).
-class HostExecutor : public Executor, public ExecutorRunner {
+class HostExecutor : public ExecutorRunner, public Executor {
 public:
   explicit HostExecutor(int nStreams) : n_(nStreams) {}
   int num_streams() const override { return n_; }

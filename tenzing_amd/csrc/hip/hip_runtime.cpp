@@ -213,7 +213,11 @@ void HipRuntime::prepare(const Sequence &seq) {
     hipEvent_t fork = E(internal_event());
     TZ_HIP(hipEventRecord(fork, origin));
     for (size_t i = 1; i < streams_.size(); ++i) TZ_HIP(hipStreamWaitEvent(S(streams_[i]), fork, 0));
-    for (const auto &e : seq_.entries) e.op->run(*this);
+    for (const auto &e : seq_.entries) {
+      TZ_LOG(Debug, "capture: " << e.op->desc());
+      e.op->run(*this);
+    }
+    TZ_LOG(Debug, "capture: join");
     for (size_t i = 1; i < streams_.size(); ++i) {
       capture_guard(int(i));
       hipEvent_t join = E(internal_event());
@@ -232,9 +236,11 @@ void HipRuntime::prepare(const Sequence &seq) {
   hipGraph_t graph = nullptr;
   TZ_HIP(hipStreamEndCapture(origin, &graph));
   size_t n = 0;
-  hipGraphGetNodes(graph, nullptr, &n);
+  TZ_HIP(hipGraphGetNodes(graph, nullptr, &n));
+  TZ_LOG(Debug, "capture: ended, " << n << " nodes; instantiating");
   hipGraphExec_t exec = nullptr;
   TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+  TZ_LOG(Debug, "capture: instantiated");
   TZ_HIP(hipGraphDestroy(graph));
   graphExec_ = exec;
   graphNodes_ = n;

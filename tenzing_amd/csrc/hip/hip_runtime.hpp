@@ -38,7 +38,8 @@ struct HipRuntimeOpts {
   double watchdog_s = 0;       // 0 = off
 };
 
-class HipRuntime : public Executor, public ExecutorRunner {
+// ExecutorRunner first: the Python bindings expose HipRuntime through that base
+class HipRuntime : public ExecutorRunner, public Executor {
 public:
   explicit HipRuntime(const HipRuntimeOpts &opts);
   ~HipRuntime() override;

@@ -1,0 +1,193 @@
+"""Core SDP semantics through the Python API (no GPU). Mirrors the reference's doctest cases
+(src/operation.cpp:87-101, src/graph.cpp:422-501, test/test_noop_graph.cpp,
+test/test_gpu_graph.cu) and adds synchronizer / serdes / equivalence properties."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def diamond(tz, a=10, b=100, c=100, d=10):
+    g = tz.Graph()
+    k = {n: tz.SimGpuOp(n, t) for n, t in (("k1", a), ("k2", b), ("k3", c), ("k4", d))}
+    g.start_then(k["k1"])
+    g.then(k["k1"], k["k2"])
+    g.then(k["k1"], k["k3"])
+    g.then(k["k2"], k["k4"])
+    g.then(k["k3"], k["k4"])
+    g.then_finish(k["k4"])
+    return g
+
+
+def normalized(g):
+    g2 = g.clone()
+    g2.normalize()
+    return g2
+
+
+def test_native_unit_suite():
+    exe = os.path.join(ROOT, "tenzing_amd", "bin", "tz-unit")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "0 failures" in r.stderr
+
+
+def test_noop_graph(tz):
+    g = tz.Graph()
+    op1 = tz.NoOp("op1")
+    g.start_then(op1)
+    g.then_finish(op1)
+    s = tz.State(g, tz.Platform(2))
+    assert len(s.sequence) == 1
+    ds = s.get_decisions()
+    assert sum(d.kind == "Execute" and d.op.name == "op1" for d in ds) == 1
+    for d in ds:
+        assert len(s.apply(d).sequence) == 2
+
+
+def test_graph_api(tz):
+    g = diamond(tz)
+    g.normalize()
+    assert len(g) == 6 and g.num_edges() == 6
+    k2 = g.find("k2")
+    g2 = g.clone_but_replace(k2, tz.SimGpuOp("k2x", 1))
+    assert g2.find("k2x") == k2 and g.find("k2") == k2
+    dot = g.dump_graphviz("t")
+    assert "digraph" in dot and "k3" in dot
+    j = json.loads(g.json())
+    assert len(j["vertices"]) == 6
+
+
+def test_op_json_schema(tz):
+    """schedule JSON keeps the reference schema"""
+    assert json.loads(tz.EventRecord(2, 1, "x").json()) == {
+        "name": "x", "stream": 1, "event": 2, "kind": "CudaEventRecord"}
+    assert json.loads(tz.StreamWaitEvent(0, 3, "w").json())["kind"] == "CudaStreamWaitEvent"
+    assert json.loads(tz.EventSync(3, "s").json()) == {"name": "s", "event": 3, "kind": "CudaEventSync"}
+    assert json.loads(tz.NoOp("n").json()) == {"name": "n", "kind": "NoOp"}
+    b = tz.BoundGpuOp(tz.SimGpuOp("k", 1), 2)
+    assert json.loads(b.json()) == {"name": "k", "stream": 2}
+
+
+def test_rollouts_are_race_free_and_roundtrip(tz):
+    g = diamond(tz)
+    ng = normalized(g)
+    idx = tz.OpIndex(g)
+    for streams in (1, 2, 3, 4):
+        for seed in range(30):
+            seq = tz.random_rollout(tz.State(g, tz.Platform(streams)), seed)
+            assert tz.verify(seq, ng, streams) == []
+            back = idx.sequence_from_json(seq.json(True))
+            assert back.canonical_key() == seq.canonical_key()
+            pruned, k = tz.remove_redundant_syncs(seq, ng, streams)
+            assert tz.verify(pruned, ng, streams) == []
+            assert len(pruned) == len(seq) - k
+
+
+def test_verify_catches_missing_sync(tz):
+    g = diamond(tz)
+    ng = normalized(g)
+    ops = {n: ng.op(ng.find(n)) for n in ("k1", "k2", "k3", "k4")}
+    s = tz.Sequence()
+    s.append(tz.Start())
+    s.append(tz.BoundGpuOp(ops["k1"], 0))
+    s.append(tz.BoundGpuOp(ops["k2"], 1))
+    s.append(tz.BoundGpuOp(ops["k3"], 0))
+    s.append(tz.BoundGpuOp(ops["k4"], 0))
+    s.append(tz.Finish())
+    v = tz.verify(s, ng, 2)
+    assert any("k2 not ordered after k1" in x for x in v)
+    assert any("Finish" in x for x in v)
+
+
+def test_stream_symmetry_pruning(tz):
+    g = diamond(tz)
+    sym = tz.get_all_sequences(g, tz.Platform(3, symmetric_streams=True))
+    keys = {s.canonical_key() for s in sym}
+    assert len(keys) == len(sym)
+    # more streams only add schedules (relabelings of the 3-stream ones are folded)
+    sym4 = tz.get_all_sequences(g, tz.Platform(4, symmetric_streams=True))
+    assert keys <= {s.canonical_key() for s in sym4}
+    # without symmetry folding the raw enumeration is strictly larger
+    nosym = tz.get_all_sequences(g, tz.Platform(3, symmetric_streams=False))
+    assert len(nosym) >= len(sym)
+
+
+def test_transitive_host_sync_is_recognized(tz):
+    """a -> CES -> b on another stream needs no extra CSWE (vector-clock synchronizer)."""
+    g = tz.Graph()
+    a, b = tz.SimGpuOp("a", 1), tz.SimGpuOp("b", 1)
+    h = tz.NoOp("h")
+    g.start_then(a)
+    g.then(a, h)
+    g.then(a, b)
+    g.then(h, b)
+    g.then_finish(b)
+    s = tz.State(g, tz.Platform(2, symmetric_streams=False))
+
+    def step(pred):
+        for d in s.get_decisions():
+            if pred(d):
+                return s.apply(d)
+        raise AssertionError([d.desc() for d in s.get_decisions()])
+
+    s = step(lambda d: d.kind == "Assign" and d.stream == 0)   # a -> s0
+    s = step(lambda d: d.kind == "Execute" and d.op.name == "a")
+    s = step(lambda d: d.kind == "Execute" and d.op.kind == "CudaEventRecord")
+    s = step(lambda d: d.kind == "Execute" and d.op.kind == "CudaEventSync")
+    s = step(lambda d: d.kind == "Execute" and d.op.name == "h")
+    s = step(lambda d: d.kind == "Assign" and d.stream == 1)   # b -> s1
+    names = [d.op.name for d in s.get_decisions() if d.kind == "Execute"]
+    assert names == ["b"]  # host already synced with a; no CSWE needed
+
+
+def test_choice_and_compound(tz):
+    sub = tz.Graph()
+    x = tz.SimGpuOp("x", 5)
+    ch = tz.StaticChoiceOp("y", [tz.SimGpuOp("y_slow", 50), tz.SimGpuOp("y_fast", 5)])
+    sub.start_then(x)
+    sub.then(x, ch)
+    sub.then_finish(ch)
+    g = tz.Graph()
+    comp = tz.StaticCompoundOp("comp", sub)
+    g.start_then(comp)
+    g.then_finish(comp)
+    s = tz.State(g, tz.Platform(2))
+    ds = s.get_decisions()
+    assert [d.kind for d in ds] == ["Expand"]
+    s = s.apply(ds[0])
+    assert s.graph.find("comp") < 0 and s.graph.find("x") > 0
+    seqs = tz.get_all_sequences(g, tz.Platform(2))
+    names = {op.name for seq in seqs for op in seq.ops()}
+    assert {"y_slow", "y_fast"} <= names
+
+
+def test_equivalence(tz):
+    g = diamond(tz)
+    s = tz.State(g, tz.Platform(2, symmetric_streams=False))
+    ds = [d for d in s.get_decisions() if d.kind == "Assign"]
+    assert len(ds) == 2
+    a, b = s.apply(ds[0]), s.apply(ds[1])
+    # distinguishable streams (priorities / CU masks): bindings are not interchangeable
+    assert not a.equivalent(b)
+    # ... but the executed sequences are equivalent under a stream bijection (reference
+    # get_equivalence(Seq, Seq))
+    a = a.apply([d for d in a.get_decisions() if d.kind == "Execute"][0])
+    b = b.apply([d for d in b.get_decisions() if d.kind == "Execute"][0])
+    assert a.sequence.equivalent(b.sequence)
+
+
+def test_prime_factors_and_runs_test(tz):
+    assert tz._tz.prime_factors(8) == [2, 2, 2]
+    assert tz._tz.prime_factors(12) == [3, 2, 2]
+    assert tz._tz.runs_test(list(range(40)))
+    assert not tz._tz.runs_test([1.0, 2.0, 3.0])
+    assert tz._tz.runs_test([1.0, 2.0, 3.0], reject_small=True)
+
+
+def test_bench_result_percentiles(tz):
+    r = tz.BenchResult.from_times([float(i) for i in range(100)])
+    assert r.pct01 == 1 and r.pct10 == 10 and r.pct50 == 50 and r.pct99 == 99

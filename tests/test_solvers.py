@@ -1,0 +1,141 @@
+"""Solvers, benchmarkers, replay and checkpointing without hardware."""
+import json
+import os
+
+import pytest
+
+from test_core import diamond
+
+
+@pytest.mark.parametrize("strategy", ["FastMin", "Coverage", "Random", "AvgTime", "Unvisited",
+                                      "AntiCorrelation", "NormalizedAntiCorrelation",
+                                      "NormRootCorr", "BalanceHistogram"])
+def test_all_strategies_run(tz, strategy):
+    assert strategy in tz.strategy_names()
+    g = diamond(tz)
+    o = tz.MctsOpts()
+    o.n_iters = 40
+    o.strategy = strategy
+    o.seed = 3
+    o.bench = tz.BenchOpts(n_iters=3)
+    p = tz.SimParams()
+    p.launch_us = 1.0
+    r = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2, p), tz.SelfCtrl(), o)
+    assert 1 <= len(r.sims) <= 40
+    assert r.best() >= 0
+
+
+def test_fastmin_finds_overlap(tz):
+    g = diamond(tz)
+    p = tz.SimParams()
+    p.launch_us = 1.0
+    o = tz.MctsOpts()
+    o.n_iters = 60
+    o.bench = tz.BenchOpts(n_iters=2)
+    r = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2, p), tz.SelfCtrl(), o)
+    best = r.sims[r.best()]
+    assert best.res.pct10 < 180e-6
+    streams = {op.stream for op in best.seq.ops() if op.op_class == "BoundGpu"}
+    assert len(streams) == 2
+
+
+def test_dfs_and_csv_replay(tz, tmp_path):
+    g = diamond(tz)
+    o = tz.DfsOpts()
+    o.bench = tz.BenchOpts(n_iters=2)
+    r = tz.dfs_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), o)
+    lines = r.dump_csv().splitlines()
+    assert json.loads(lines[0]) == {"dfs__Opts": {"maxSeqs": -1}}
+    row = lines[1].split("|")
+    assert row[0] == "0" and len(row) > 8 and json.loads(row[7])["name"] == "Start"
+    path = tmp_path / "r.csv"
+    path.write_text(r.dump_csv())
+    cb = tz.CsvBenchmarker(str(path), g)
+    assert len(cb) == len(r.sims)
+    # MCTS driven purely by recorded timings (reference mcts_csv drivers)
+    mo = tz.MctsOpts()
+    mo.n_iters = 30
+    mr = tz.mcts_explore(g, tz.Platform(2), cb, tz.SelfCtrl(), mo)
+    assert min(s.res.pct10 for s in mr.sims) == pytest.approx(min(s.res.pct10 for s in r.sims))
+
+
+def test_max_seqs_cap(tz):
+    g = diamond(tz)
+    assert len(tz.get_all_sequences(g, tz.Platform(3), max_seqs=5)) == 5
+
+
+def test_checkpoint_resume(tz, tmp_path):
+    g = diamond(tz)
+    o = tz.MctsOpts()
+    o.n_iters = 15
+    o.bench = tz.BenchOpts(n_iters=2)
+    o.checkpoint_path = str(tmp_path / "ck.json")
+    r1 = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), o)
+    ck = json.loads((tmp_path / "ck.json").read_text())
+    assert len(ck["sims"]) == len(r1.sims)
+    o2 = tz.MctsOpts()
+    o2.n_iters = 25
+    o2.bench = o.bench
+    o2.resume_path = o.checkpoint_path
+    r2 = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), o2)
+    assert len(r2.sims) > len(r1.sims)
+
+
+def test_host_ops_empirical(tz):
+    """Hardware-free empirical benchmarking with host sleep ops (reference legacy
+    src_mcts_test SlowFirst/FastFirst)."""
+    g = tz.Graph()
+    a, b = tz.SleepOp("slow", 300.0), tz.SleepOp("fast", 100.0)
+    g.start_then(a)
+    g.start_then(b)
+    g.then_finish(a)
+    g.then_finish(b)
+    ctrl = tz.SelfCtrl()
+    ex = tz.HostExecutor(1)
+    bench = tz.EmpiricalBenchmarker(ex, ctrl)
+    o = tz.DfsOpts()
+    o.bench = tz.BenchOpts(n_iters=3, max_retries=1, target_secs=0.002)
+    r = tz.dfs_explore(g, tz.Platform(1), bench, ctrl, o)
+    assert len(r.sims) == 2
+    for s in r.sims:
+        assert 350e-6 < s.res.pct50 < 5e-3
+
+
+def test_pycpuop_callback(tz):
+    calls = []
+    g = tz.Graph()
+    op = tz.PyCpuOp("py", lambda: calls.append(1))
+    g.start_then(op)
+    g.then_finish(op)
+    seq = tz.get_all_sequences(g, tz.Platform(1))[0]
+    ex = tz.HostExecutor(1)
+    ex.prepare(seq)
+    ex.run(5)
+    assert len(calls) == 5
+
+
+def test_tree_dump_and_counters(tz, tmp_path):
+    g = diamond(tz)
+    o = tz.MctsOpts()
+    o.n_iters = 12
+    o.dump_tree = True
+    o.dump_tree_prefix = str(tmp_path / "mcts_")
+    o.bench = tz.BenchOpts(n_iters=2)
+    r = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), o)
+    assert (tmp_path / "mcts_0.dot").exists()
+    c = r.counters()
+    for k in ("SELECT", "EXPAND", "ROLLOUT", "BENCHMARK", "BACKPROP"):
+        assert k in c
+    assert r.tree_size > 1
+    lines = r.dump_jsonl().splitlines()
+    assert len(lines) == len(r.sims) and "result" in json.loads(lines[0])
+
+
+def test_time_budget_stop(tz):
+    g = diamond(tz)
+    o = tz.MctsOpts()
+    o.n_iters = 0
+    o.time_budget_s = 0.2
+    o.bench = tz.BenchOpts(n_iters=2)
+    r = tz.mcts_explore(g, tz.Platform(4), tz.SimBenchmarker(4), tz.SelfCtrl(), o)
+    assert r.stop_reason in ("time_budget", "full_tree")
