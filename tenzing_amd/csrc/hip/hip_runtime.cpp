@@ -117,10 +117,31 @@ void HipRuntime::capture_guard(int stream) {
   for (size_t k = 0; k < hostSynced_.size(); ++k) {
     if (ap.size() <= k) ap.resize(hostSynced_.size(), 0);
     if (!ap[k]) {
-      TZ_HIP(hipStreamWaitEvent(S(streams_[stream]), E(event(hostSynced_[k])), 0));
       ap[k] = 1;
+      wait(stream, event(hostSynced_[k]));
     }
   }
+}
+
+// During capture, HIP (ROCm 7.2) crashes in hipStreamEndCapture when a stream waits on an event
+// it recorded itself; such waits (and repeated waits on the same recording) are redundant by
+// stream order, so they are dropped while capturing.
+void HipRuntime::record(void *ev, int stream) {
+  TZ_HIP(hipEventRecord(E(ev), S(native_stream(stream))));
+  if (capturing_) {
+    capRec_[ev] = stream;
+    for (auto it = capWaited_.begin(); it != capWaited_.end();)
+      it = it->second == ev ? capWaited_.erase(it) : std::next(it);
+  }
+}
+
+void HipRuntime::wait(int stream, void *ev) {
+  if (capturing_) {
+    auto it = capRec_.find(ev);
+    if (it == capRec_.end() || it->second == stream) return;
+    if (!capWaited_.insert({stream, ev}).second) return;
+  }
+  TZ_HIP(hipStreamWaitEvent(S(native_stream(stream)), E(ev), 0));
 }
 
 void HipRuntime::launch(const GpuOp &op, int stream) {
@@ -130,12 +151,12 @@ void HipRuntime::launch(const GpuOp &op, int stream) {
 
 void HipRuntime::event_record(int e, int stream) {
   capture_guard(stream);
-  TZ_HIP(hipEventRecord(E(event(e)), S(native_stream(stream))));
+  record(event(e), stream);
 }
 
 void HipRuntime::stream_wait_event(int stream, int e) {
   capture_guard(stream);
-  TZ_HIP(hipStreamWaitEvent(S(native_stream(stream)), E(event(e)), 0));
+  wait(stream, event(e));
 }
 
 void HipRuntime::event_sync(int e) {
@@ -150,8 +171,7 @@ void HipRuntime::stream_sync(int stream) {
   if (capturing_) {
     // host waits for the stream: represent as an internal event the later enqueues depend on
     const int e = int(events_.size());
-    event(e);
-    TZ_HIP(hipEventRecord(E(events_[e]), S(streams_[stream])));
+    record(event(e), stream);
     hostSynced_.push_back(e);
     return;
   }
@@ -161,9 +181,9 @@ void HipRuntime::stream_sync(int stream) {
 void HipRuntime::stream_wait(int waiter, int waitee) {
   capture_guard(waiter);
   capture_guard(waitee);
-  hipEvent_t ev = E(internal_event());
-  TZ_HIP(hipEventRecord(ev, S(native_stream(waitee))));
-  TZ_HIP(hipStreamWaitEvent(S(native_stream(waiter)), ev, 0));
+  void *ev = internal_event();
+  record(ev, waitee);
+  wait(waiter, ev);
 }
 
 void HipRuntime::device_sync() { TZ_HIP(hipDeviceSynchronize()); }
@@ -209,22 +229,23 @@ void HipRuntime::prepare(const Sequence &seq) {
   capturing_ = true;
   hostSynced_.clear();
   applied_.assign(streams_.size(), {});
+  capRec_.clear();
+  capWaited_.clear();
   try {
-    hipEvent_t fork = E(internal_event());
-    TZ_HIP(hipEventRecord(fork, origin));
-    for (size_t i = 1; i < streams_.size(); ++i) TZ_HIP(hipStreamWaitEvent(S(streams_[i]), fork, 0));
+    void *fork = internal_event();
+    record(fork, 0);
+    for (size_t i = 1; i < streams_.size(); ++i) wait(int(i), fork);
     for (const auto &e : seq_.entries) {
       TZ_LOG(Debug, "capture: " << e.op->desc());
       e.op->run(*this);
     }
-    TZ_LOG(Debug, "capture: join");
+    // join every stream into the origin (host syncs at the end need no extra edges: the join
+    // already orders all work before the graph's completion)
     for (size_t i = 1; i < streams_.size(); ++i) {
-      capture_guard(int(i));
-      hipEvent_t join = E(internal_event());
-      TZ_HIP(hipEventRecord(join, S(streams_[i])));
-      TZ_HIP(hipStreamWaitEvent(origin, join, 0));
+      void *join = internal_event();
+      record(join, int(i));
+      wait(0, join);
     }
-    capture_guard(0);
   } catch (...) {
     capturing_ = false;
     hipGraph_t g = nullptr;
@@ -234,10 +255,12 @@ void HipRuntime::prepare(const Sequence &seq) {
   }
   capturing_ = false;
   hipGraph_t graph = nullptr;
+  TZ_LOG(Debug, "capture: end capture");
   TZ_HIP(hipStreamEndCapture(origin, &graph));
+  TZ_LOG(Debug, "capture: ended");
   size_t n = 0;
-  TZ_HIP(hipGraphGetNodes(graph, nullptr, &n));
-  TZ_LOG(Debug, "capture: ended, " << n << " nodes; instantiating");
+  if (std::getenv("TZ_GRAPH_COUNT_NODES")) TZ_HIP(hipGraphGetNodes(graph, nullptr, &n));
+  TZ_LOG(Debug, "capture: " << n << " nodes; instantiating");
   hipGraphExec_t exec = nullptr;
   TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
   TZ_LOG(Debug, "capture: instantiated");

@@ -20,7 +20,9 @@
 #include "core/benchmark.hpp"
 
 #include <atomic>
+#include <map>
 #include <memory>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -94,6 +96,10 @@ private:
   bool capturing_ = false;
   std::vector<int> hostSynced_;              // events the host "waited" on during capture
   std::vector<std::vector<char>> applied_;   // [stream][k] hostSynced_[k] applied to stream
+  std::map<void *, int> capRec_;             // event -> stream that last recorded it (capture)
+  std::set<std::pair<int, void *>> capWaited_; // (stream, event) waits issued since the record
+  void record(void *ev, int stream);
+  void wait(int stream, void *ev);
 
   double watchdogS_ = 0;
   std::atomic<double> deadline_{0};
