@@ -531,6 +531,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_property_readonly("device", &HipRuntime::device)
       .def("device_name", &HipRuntime::device_name)
       .def("graph_nodes", &HipRuntime::graph_nodes)
+      .def("graph_edges", &HipRuntime::graph_edges)
       .def("num_streams", &HipRuntime::num_streams)
       .def("native_stream", [](HipRuntime &r, int s) { return reinterpret_cast<uintptr_t>(r.native_stream(s)); })
       .def("device_sync", &HipRuntime::device_sync, py::call_guard<py::gil_scoped_release>())

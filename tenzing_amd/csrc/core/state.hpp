@@ -23,6 +23,7 @@
 
 #include "graph.hpp"
 
+#include <algorithm>
 #include <random>
 #include <set>
 #include <string>
@@ -92,6 +93,10 @@ public:
   int covering_event(int t, int k) const;
   int num_events() const { return int(evStream_.size()); }
   bool event_recorded(int e) const { return e < num_events() && evStream_[e] >= 0; }
+  /// number of GPU ops of stream t known complete before the next op enqueued on stream s
+  /// (t != s); used to turn a schedule into explicit graph dependencies
+  int known(int s, int t) const { return std::max(vc(s, t), vc(S_, t)); }
+  int count(int s) const { return cnt_[s]; }
 
 private:
   void ensure_event(int e);

@@ -5,6 +5,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -111,79 +112,24 @@ void *HipRuntime::native_stream(int stream) {
   return streams_[stream];
 }
 
-void HipRuntime::capture_guard(int stream) {
-  if (!capturing_) return;
-  auto &ap = applied_[stream];
-  for (size_t k = 0; k < hostSynced_.size(); ++k) {
-    if (ap.size() <= k) ap.resize(hostSynced_.size(), 0);
-    if (!ap[k]) {
-      ap[k] = 1;
-      wait(stream, event(hostSynced_[k]));
-    }
-  }
-}
-
-// During capture, HIP (ROCm 7.2) crashes in hipStreamEndCapture when a stream waits on an event
-// it recorded itself; such waits (and repeated waits on the same recording) are redundant by
-// stream order, so they are dropped while capturing.
-void HipRuntime::record(void *ev, int stream) {
-  TZ_HIP(hipEventRecord(E(ev), S(native_stream(stream))));
-  if (capturing_) {
-    capRec_[ev] = stream;
-    for (auto it = capWaited_.begin(); it != capWaited_.end();)
-      it = it->second == ev ? capWaited_.erase(it) : std::next(it);
-  }
-}
-
-void HipRuntime::wait(int stream, void *ev) {
-  if (capturing_) {
-    auto it = capRec_.find(ev);
-    if (it == capRec_.end() || it->second == stream) return;
-    if (!capWaited_.insert({stream, ev}).second) return;
-  }
-  TZ_HIP(hipStreamWaitEvent(S(native_stream(stream)), E(ev), 0));
-}
-
-void HipRuntime::launch(const GpuOp &op, int stream) {
-  capture_guard(stream);
-  op.launch(native_stream(stream), *this);
-}
+void HipRuntime::launch(const GpuOp &op, int stream) { op.launch(native_stream(stream), *this); }
 
 void HipRuntime::event_record(int e, int stream) {
-  capture_guard(stream);
-  record(event(e), stream);
+  TZ_HIP(hipEventRecord(E(event(e)), S(native_stream(stream))));
 }
 
 void HipRuntime::stream_wait_event(int stream, int e) {
-  capture_guard(stream);
-  wait(stream, event(e));
+  TZ_HIP(hipStreamWaitEvent(S(native_stream(stream)), E(event(e)), 0));
 }
 
-void HipRuntime::event_sync(int e) {
-  if (capturing_) {
-    hostSynced_.push_back(e);
-    return;
-  }
-  TZ_HIP(hipEventSynchronize(E(event(e))));
-}
+void HipRuntime::event_sync(int e) { TZ_HIP(hipEventSynchronize(E(event(e)))); }
 
-void HipRuntime::stream_sync(int stream) {
-  if (capturing_) {
-    // host waits for the stream: represent as an internal event the later enqueues depend on
-    const int e = int(events_.size());
-    record(event(e), stream);
-    hostSynced_.push_back(e);
-    return;
-  }
-  TZ_HIP(hipStreamSynchronize(S(native_stream(stream))));
-}
+void HipRuntime::stream_sync(int stream) { TZ_HIP(hipStreamSynchronize(S(native_stream(stream)))); }
 
 void HipRuntime::stream_wait(int waiter, int waitee) {
-  capture_guard(waiter);
-  capture_guard(waitee);
-  void *ev = internal_event();
-  record(ev, waitee);
-  wait(waiter, ev);
+  hipEvent_t ev = E(internal_event());
+  TZ_HIP(hipEventRecord(ev, S(native_stream(waitee))));
+  TZ_HIP(hipStreamWaitEvent(S(native_stream(waiter)), ev, 0));
 }
 
 void HipRuntime::device_sync() { TZ_HIP(hipDeviceSynchronize()); }
@@ -192,15 +138,15 @@ void HipRuntime::destroy_graph() {
   if (graphExec_) {
     hipGraphExecDestroy(static_cast<hipGraphExec_t>(graphExec_));
     graphExec_ = nullptr;
-    graphNodes_ = 0;
+    graphNodes_ = graphEdges_ = 0;
   }
 }
 
-bool HipRuntime::capturable(const Sequence &seq) const {
+bool HipRuntime::recordable(const Sequence &seq) const {
   for (const auto &e : seq.entries) {
     const OpClass c = e.op->op_class();
     if (c == OpClass::Cpu) {
-      // only host no-ops can be captured
+      // only host no-ops can be dropped from a replay
       if (e.op->kind() != "NoOp" || e.op->cost_us() > 0) return false;
     } else if (c == OpClass::BoundGpu) {
       if (!static_cast<const BoundGpuOp &>(*e.op).unbound()->capturable()) return false;
@@ -216,64 +162,80 @@ void HipRuntime::set_mode(ExecMode m) {
   }
 }
 
+void HipRuntime::build_graph() {
+  const int nS = num_streams();
+  hipGraph_t graph = nullptr;
+  TZ_HIP(hipGraphCreate(&graph, 0));
+  SyncModel model(nS);
+  std::vector<std::vector<hipGraphNode_t>> nodes(nS); // per stream, in issue order
+  size_t edges = 0;
+  try {
+    for (const auto &e : seq_.entries) {
+      const BoundOp &op = *e.op;
+      if (op.op_class() == OpClass::BoundGpu) {
+        const auto &b = static_cast<const BoundGpuOp &>(op);
+        const int s = b.stream();
+        TZ_CHECK(s >= 0 && s < nS, "stream " << s << " out of range");
+        // dependencies: previous op on this stream + the latest op of every other stream that
+        // the schedule's events / host syncs make complete before this one is issued
+        std::vector<hipGraphNode_t> deps;
+        if (!nodes[s].empty()) deps.push_back(nodes[s].back());
+        for (int t = 0; t < nS; ++t) {
+          if (t == s) continue;
+          const int k = model.known(s, t);
+          if (k > 0) deps.push_back(nodes[t][size_t(k) - 1]);
+        }
+        // record the op alone on its own stream
+        hipStream_t st = S(streams_[s]);
+        TZ_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        hipGraph_t child = nullptr;
+        try {
+          b.unbound()->launch(st, *this);
+        } catch (...) {
+          hipStreamEndCapture(st, &child);
+          if (child) hipGraphDestroy(child);
+          throw;
+        }
+        TZ_HIP(hipStreamEndCapture(st, &child));
+        size_t nChild = 0;
+        TZ_HIP(hipGraphGetNodes(child, nullptr, &nChild));
+        hipGraphNode_t node = nullptr;
+        if (nChild == 0) {
+          TZ_HIP(hipGraphAddEmptyNode(&node, graph, deps.data(), deps.size()));
+        } else {
+          TZ_HIP(hipGraphAddChildGraphNode(&node, graph, deps.data(), deps.size(), child));
+        }
+        TZ_HIP(hipGraphDestroy(child));
+        nodes[s].push_back(node);
+        edges += deps.size();
+      }
+      model.apply(op);
+    }
+    size_t n = 0;
+    for (auto &v : nodes) n += v.size();
+    hipGraphExec_t exec = nullptr;
+    TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    TZ_HIP(hipGraphDestroy(graph));
+    graph = nullptr;
+    graphExec_ = exec;
+    graphNodes_ = n;
+    graphEdges_ = edges;
+    TZ_LOG(Debug, "graph mode: " << n << " nodes, " << edges << " edges");
+  } catch (...) {
+    if (graph) hipGraphDestroy(graph);
+    throw;
+  }
+  // upload once so the first timed launch does not pay for it
+  TZ_HIP(hipGraphUpload(static_cast<hipGraphExec_t>(graphExec_), S(streams_[0])));
+  TZ_HIP(hipStreamSynchronize(S(streams_[0])));
+}
+
 void HipRuntime::prepare(const Sequence &seq) {
   destroy_graph();
   seq_ = seq;
   internalUsed_ = 0;
   event(std::max(0, seq.num_events() - 1)); // provision the event pool
-  if (mode_ != ExecMode::Graph || !capturable(seq)) return;
-
-  // record the whole schedule into one hipGraph by capturing stream 0 and forking the others
-  hipStream_t origin = S(streams_[0]);
-  TZ_HIP(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
-  capturing_ = true;
-  hostSynced_.clear();
-  applied_.assign(streams_.size(), {});
-  capRec_.clear();
-  capWaited_.clear();
-  try {
-    void *fork = internal_event();
-    record(fork, 0);
-    for (size_t i = 1; i < streams_.size(); ++i) wait(int(i), fork);
-    for (const auto &e : seq_.entries) {
-      TZ_LOG(Debug, "capture: " << e.op->desc());
-      e.op->run(*this);
-    }
-    // join every stream into the origin (host syncs at the end need no extra edges: the join
-    // already orders all work before the graph's completion)
-    for (size_t i = 1; i < streams_.size(); ++i) {
-      void *join = internal_event();
-      record(join, int(i));
-      wait(0, join);
-    }
-  } catch (...) {
-    capturing_ = false;
-    hipGraph_t g = nullptr;
-    hipStreamEndCapture(origin, &g);
-    if (g) hipGraphDestroy(g);
-    throw;
-  }
-  capturing_ = false;
-  hipGraph_t graph = nullptr;
-  TZ_LOG(Debug, "capture: end capture");
-  TZ_HIP(hipStreamEndCapture(origin, &graph));
-  TZ_LOG(Debug, "capture: ended");
-  size_t n = 0;
-  if (std::getenv("TZ_GRAPH_COUNT_NODES")) TZ_HIP(hipGraphGetNodes(graph, nullptr, &n));
-  TZ_LOG(Debug, "capture: " << n << " nodes; instantiating");
-  hipGraphExec_t exec = nullptr;
-  TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-  TZ_LOG(Debug, "capture: instantiated");
-  TZ_HIP(hipGraphDestroy(graph));
-  graphExec_ = exec;
-  graphNodes_ = n;
-  // upload once so the first timed launch does not pay for it
-  TZ_HIP(hipGraphUpload(exec, origin));
-  TZ_HIP(hipStreamSynchronize(origin));
-}
-
-void HipRuntime::run_eager_once() {
-  for (const auto &e : seq_.entries) e.op->run(*this);
+  if (mode_ == ExecMode::Graph && recordable(seq)) build_graph();
 }
 
 void HipRuntime::run(int64_t n) {
@@ -286,7 +248,7 @@ void HipRuntime::run(int64_t n) {
   } else {
     for (int64_t i = 0; i < n; ++i) {
       internalUsed_ = 0;
-      run_eager_once();
+      for (const auto &e : seq_.entries) e.op->run(*this);
     }
   }
   deadline_ = 0;

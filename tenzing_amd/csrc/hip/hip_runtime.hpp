@@ -9,10 +9,12 @@
 //    turning "which CUs" into a schedulable resource);
 //  * a pool of timing-disabled hipEvents indexed by the schedule's abstract event ids;
 //  * two execution modes for one schedule: Eager (host issues every op each iteration, like the
-//    reference) and Graph (the whole multi-stream schedule, RCCL calls included, is recorded
-//    once by stream capture into a hipGraph and replayed with one hipGraphLaunch per
-//    iteration). In Graph mode host synchronizations (CES / StreamSync) become graph joins: every
-//    later enqueue on any stream waits for the events the host had synchronized on;
+//    reference) and Graph (the schedule is compiled once into a hipGraph and replayed with one
+//    hipGraphLaunch per iteration). Graph mode does not rely on multi-stream stream capture:
+//    the schedule's happens-before relation is replayed in the same vector-clock model the
+//    synchronizer uses, every GPU op is captured alone on its stream into a child graph, and
+//    the child-graph nodes get exactly the dependencies the schedule's events / host syncs
+//    imply. Host synchronizations therefore cost nothing inside a replay;
 //  * a watchdog: a schedule whose iteration exceeds `watchdog_s` (e.g. an RCCL deadlock) aborts
 //    the process with a diagnostic instead of hanging the search.
 #pragma once
@@ -20,9 +22,7 @@
 #include "core/benchmark.hpp"
 
 #include <atomic>
-#include <map>
 #include <memory>
-#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -32,7 +32,7 @@ namespace tz {
 enum class ExecMode { Eager, Graph };
 
 struct HipRuntimeOpts {
-  int device = -1;            // -1: keep current device
+  int device = -1;             // -1: keep current device
   int n_streams = 2;
   std::vector<int> priorities; // optional per-stream priorities
   bool cu_partition = false;   // give each stream a disjoint, XCD-balanced CU mask
@@ -66,40 +66,32 @@ public:
   void set_mode(ExecMode m);
   ExecMode mode() const { return mode_; }
   /// mode actually used for the prepared sequence (Graph falls back to Eager when a host op
-  /// cannot be captured)
+  /// cannot be recorded)
   ExecMode effective_mode() const { return graphExec_ ? ExecMode::Graph : ExecMode::Eager; }
   int device() const { return device_; }
   std::string device_name() const;
-  /// number of nodes of the captured graph (0 in eager mode)
+  /// number of top-level nodes of the compiled graph (0 in eager mode)
   size_t graph_nodes() const { return graphNodes_; }
+  /// number of dependency edges of the compiled graph
+  size_t graph_edges() const { return graphEdges_; }
   void set_watchdog(double s) { watchdogS_ = s; }
 
 private:
   void *event(int e);
   void *internal_event();
-  void capture_guard(int stream);
   void destroy_graph();
-  bool capturable(const Sequence &seq) const;
-  void run_eager_once();
+  bool recordable(const Sequence &seq) const;
+  void build_graph();
 
   int device_ = 0;
   ExecMode mode_;
   std::vector<void *> streams_;
   std::vector<void *> events_;   // schedule events
-  std::vector<void *> internal_; // capture / StreamWait helpers
+  std::vector<void *> internal_; // StreamWait helpers
   size_t internalUsed_ = 0;
   Sequence seq_;
   void *graphExec_ = nullptr;
-  size_t graphNodes_ = 0;
-
-  // graph-capture host-sync emulation
-  bool capturing_ = false;
-  std::vector<int> hostSynced_;              // events the host "waited" on during capture
-  std::vector<std::vector<char>> applied_;   // [stream][k] hostSynced_[k] applied to stream
-  std::map<void *, int> capRec_;             // event -> stream that last recorded it (capture)
-  std::set<std::pair<int, void *>> capWaited_; // (stream, event) waits issued since the record
-  void record(void *ev, int stream);
-  void wait(int stream, void *ev);
+  size_t graphNodes_ = 0, graphEdges_ = 0;
 
   double watchdogS_ = 0;
   std::atomic<double> deadline_{0};
