@@ -664,6 +664,9 @@ PYBIND11_MODULE(_tz, m) {
     kern::iota_f64(n, base, scale, reinterpret_cast<double *>(a), P(s));
   }, py::arg("n"), py::arg("base"), py::arg("scale"), py::arg("a"), py::arg("stream") = 0);
   k.def("empty", [](uintptr_t s) { kern::empty(P(s)); }, py::arg("stream") = 0);
+  k.def("copy_bytes", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
+    kern::copy_bytes(P(dst), P(src), n, P(s));
+  }, py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("stream") = 0);
   k.def("busy_wait", [](int64_t t, int b, uintptr_t s) { kern::busy_wait(t, b, P(s)); },
         py::arg("ticks"), py::arg("blocks") = 1, py::arg("stream") = 0);
 }

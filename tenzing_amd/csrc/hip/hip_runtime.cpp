@@ -185,27 +185,37 @@ void HipRuntime::build_graph() {
           const int k = model.known(s, t);
           if (k > 0) deps.push_back(nodes[t][size_t(k) - 1]);
         }
-        // record the op alone on its own stream
+        // record the op alone on its own stream, directly into the schedule graph behind its
+        // dependencies (flat graph: no child-graph indirection at replay)
         hipStream_t st = S(streams_[s]);
-        TZ_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        hipGraph_t child = nullptr;
+        TZ_HIP(hipStreamBeginCaptureToGraph(st, graph, deps.data(), nullptr, deps.size(),
+                                            hipStreamCaptureModeThreadLocal));
+        hipGraph_t captured = nullptr;
+        std::vector<hipGraphNode_t> tails;
         try {
           b.unbound()->launch(st, *this);
+          hipStreamCaptureStatus cs;
+          const hipGraphNode_t *d = nullptr;
+          size_t nd = 0;
+          TZ_HIP(hipStreamGetCaptureInfo_v2(st, &cs, nullptr, nullptr, &d, &nd));
+          tails.assign(d, d + nd);
         } catch (...) {
-          hipStreamEndCapture(st, &child);
-          if (child) hipGraphDestroy(child);
+          hipStreamEndCapture(st, &captured);
           throw;
         }
-        TZ_HIP(hipStreamEndCapture(st, &child));
-        size_t nChild = 0;
-        TZ_HIP(hipGraphGetNodes(child, nullptr, &nChild));
+        TZ_HIP(hipStreamEndCapture(st, &captured));
         hipGraphNode_t node = nullptr;
-        if (nChild == 0) {
+        std::vector<hipGraphNode_t> sd = deps, st2 = tails;
+        std::sort(sd.begin(), sd.end());
+        std::sort(st2.begin(), st2.end());
+        if (tails.size() == 1 && sd != st2) {
+          node = tails[0]; // the op is one node (or a chain ending in one node)
+        } else if (sd == st2) {
+          // the op enqueued nothing: keep an empty placeholder so later edges stay valid
           TZ_HIP(hipGraphAddEmptyNode(&node, graph, deps.data(), deps.size()));
         } else {
-          TZ_HIP(hipGraphAddChildGraphNode(&node, graph, deps.data(), deps.size(), child));
+          TZ_HIP(hipGraphAddEmptyNode(&node, graph, tails.data(), tails.size()));
         }
-        TZ_HIP(hipGraphDestroy(child));
         nodes[s].push_back(node);
         edges += deps.size();
       }

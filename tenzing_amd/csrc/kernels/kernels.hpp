@@ -28,6 +28,9 @@ void box_copy(double *grid, const BoxDesc &d, bool unpack, void *stream);
 /// pack/unpack up to kMaxBoxes boxes in ONE launch (fused multi-face halo pack/unpack)
 void box_copy_many(double *grid, const BoxDesc *d, int n, bool unpack, void *stream);
 
+/// dst = src, `bytes` (16-B aligned pointers; the transport copy of self-neighbour exchanges)
+void copy_bytes(void *dst, const void *src, size_t bytes, void *stream);
+
 /// y[r] = sum_j A[r,j] x[j] for CSR A (f32 values, i32 indices). `lanesPerRow` in {1,2,4,8,16,32,64}
 /// (0 = pick from nnz/row). When `accumulate`, y[r] += ... instead.
 void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,

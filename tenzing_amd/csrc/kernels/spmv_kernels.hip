@@ -87,6 +87,25 @@ __global__ __launch_bounds__(kThreads) void iota_k(int64_t n, double base, doubl
     a[i] = base + scale * double(i);
 }
 
+// 16 B per lane, 4 independent 16-B loads in flight per lane before the stores
+__global__ __launch_bounds__(kThreads) void copy16_k(int4 *__restrict__ dst,
+                                                     const int4 *__restrict__ src, int64_t n16) {
+  const int64_t stride = int64_t(gridDim.x) * kThreads;
+  int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const int4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+__global__ void copy_tail_k(char *__restrict__ dst, const char *__restrict__ src, int n) {
+  if (int(threadIdx.x) < n) dst[threadIdx.x] = src[threadIdx.x];
+}
+
 __global__ void empty_k() {}
 
 __global__ void busy_k(int64_t ticks) {
@@ -154,6 +173,25 @@ void iota_f64(int64_t n, double base, double scale, double *a, void *stream) {
   hipLaunchKernelGGL(iota_k, dim3(grid_for(n, 4)), dim3(kThreads), 0,
                      static_cast<hipStream_t>(stream), n, base, scale, a);
   TZ_HIP_LAUNCH_CHECK();
+}
+
+void copy_bytes(void *dst, const void *src, size_t bytes, void *stream) {
+  if (!bytes) return;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) % 16)
+    throw std::runtime_error("copy_bytes: pointers must be 16-byte aligned");
+  const int64_t n16 = int64_t(bytes / 16);
+  if (n16) {
+    hipLaunchKernelGGL(copy16_k, dim3(grid_for(n16, 4)), dim3(kThreads), 0, s,
+                       static_cast<int4 *>(dst), static_cast<const int4 *>(src), n16);
+    TZ_HIP_LAUNCH_CHECK();
+  }
+  const int tail = int(bytes % 16);
+  if (tail) {
+    hipLaunchKernelGGL(copy_tail_k, dim3(1), dim3(64), 0, s, static_cast<char *>(dst) + n16 * 16,
+                       static_cast<const char *>(src) + n16 * 16, tail);
+    TZ_HIP_LAUNCH_CHECK();
+  }
 }
 
 void empty(void *stream) {
