@@ -18,7 +18,21 @@ import sys
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def _load_torch_first():
+    """The extension and PyTorch-ROCm must share ONE HIP runtime in a process: both link
+    libamdhip64.so.7 / librccl.so.1 by soname, so whichever is loaded first serves both. Loading
+    torch first makes the process use torch's bundled runtime, so torch tensors, streams and our
+    schedules interoperate (torch ops on our streams fail with invalid-argument otherwise)."""
+    if os.environ.get("TZ_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def _load_native():
+    _load_torch_first()
     try:
         return importlib.import_module("tenzing_amd._tz")
     except ImportError as first:

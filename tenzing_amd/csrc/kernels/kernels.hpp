@@ -30,6 +30,13 @@ void box_copy_many(double *grid, const BoxDesc *d, int n, bool unpack, void *str
 
 /// dst = src, `bytes` (16-B aligned pointers; the transport copy of self-neighbour exchanges)
 void copy_bytes(void *dst, const void *src, size_t bytes, void *stream);
+struct CopyDesc {
+  void *dst = nullptr;
+  const void *src = nullptr;
+  size_t bytes = 0; // multiple of 16, 16-B aligned pointers
+};
+/// up to kMaxBoxes copies in one launch
+void copy_many(const CopyDesc *d, int n, void *stream);
 
 /// y[r] = sum_j A[r,j] x[j] for CSR A (f32 values, i32 indices). `lanesPerRow` in {1,2,4,8,16,32,64}
 /// (0 = pick from nnz/row). When `accumulate`, y[r] += ... instead.

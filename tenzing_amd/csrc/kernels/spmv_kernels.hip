@@ -15,6 +15,7 @@
 
 #include "kernels.hpp"
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -100,6 +101,36 @@ __global__ __launch_bounds__(kThreads) void copy16_k(int4 *__restrict__ dst,
     dst[i + 3 * stride] = d;
   }
   for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+struct CopyBatch {
+  int4 *dst[kMaxBoxes];
+  const int4 *src[kMaxBoxes];
+  int64_t n16[kMaxBoxes];
+  int32_t tail8[kMaxBoxes]; // 1 if an 8-byte remainder follows the 16-byte part
+  uint32_t block_start[kMaxBoxes + 1];
+  int32_t n;
+};
+
+__global__ __launch_bounds__(kThreads) void copy_many_k(CopyBatch b) {
+  int c = 0;
+  while (c + 1 < b.n && blockIdx.x >= b.block_start[c + 1]) ++c;
+  const int64_t nb = b.block_start[c + 1] - b.block_start[c];
+  const int64_t stride = nb * kThreads;
+  int4 *__restrict__ dst = b.dst[c];
+  const int4 *__restrict__ src = b.src[c];
+  const int64_t n16 = b.n16[c];
+  int64_t i = int64_t(blockIdx.x - b.block_start[c]) * kThreads + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const int4 x0 = src[i], x1 = src[i + stride], x2 = src[i + 2 * stride], x3 = src[i + 3 * stride];
+    dst[i] = x0;
+    dst[i + stride] = x1;
+    dst[i + 2 * stride] = x2;
+    dst[i + 3 * stride] = x3;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+  if (b.tail8[c] && blockIdx.x == b.block_start[c] && threadIdx.x == 0)
+    reinterpret_cast<double *>(dst + n16)[0] = reinterpret_cast<const double *>(src + n16)[0];
 }
 
 __global__ void copy_tail_k(char *__restrict__ dst, const char *__restrict__ src, int n) {
@@ -192,6 +223,30 @@ void copy_bytes(void *dst, const void *src, size_t bytes, void *stream) {
                        static_cast<const char *>(src) + n16 * 16, tail);
     TZ_HIP_LAUNCH_CHECK();
   }
+}
+
+void copy_many(const CopyDesc *d, int n, void *stream) {
+  if (n <= 0) return;
+  if (n > kMaxBoxes) throw std::runtime_error("copy_many: too many copies");
+  CopyBatch b{};
+  uint32_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    if (d[i].bytes == 0) continue;
+    if ((reinterpret_cast<uintptr_t>(d[i].dst) | reinterpret_cast<uintptr_t>(d[i].src)) % 16 ||
+        d[i].bytes % 8)
+      throw std::runtime_error("copy_many: 16-byte aligned pointers and 8-byte sizes required");
+    const int k = b.n++;
+    b.dst[k] = static_cast<int4 *>(d[i].dst);
+    b.src[k] = static_cast<const int4 *>(d[i].src);
+    b.n16[k] = int64_t(d[i].bytes / 16);
+    b.tail8[k] = int32_t((d[i].bytes % 16) / 8);
+    b.block_start[k] = total;
+    total += uint32_t(grid_for(std::max<int64_t>(b.n16[k], 1), 4));
+  }
+  if (b.n == 0) return;
+  b.block_start[b.n] = total;
+  hipLaunchKernelGGL(copy_many_k, dim3(total), dim3(kThreads), 0, static_cast<hipStream_t>(stream), b);
+  TZ_HIP_LAUNCH_CHECK();
 }
 
 void empty(void *stream) {

@@ -85,32 +85,38 @@ private:
   int i_;
 };
 
-class HaloStageAll : public GpuOp {
+/// one op for a whole group of directions (single kernel launch / single RCCL group)
+class HaloStageGroup : public GpuOp {
 public:
   enum Stage { Pack, Shift, Unpack };
-  HaloStageAll(std::shared_ptr<const HaloExchange> h, Stage st) : h_(std::move(h)), st_(st) {}
+  HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag)
+      : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
   std::string name() const override {
-    return st_ == Pack ? "he_pack_all" : (st_ == Shift ? "he_shift_all" : "he_unpack_all");
+    return std::string(st_ == Pack ? "he_pack_" : (st_ == Shift ? "he_shift_" : "he_unpack_")) + tag_;
   }
   std::string kind() const override {
-    return st_ == Pack ? "HaloPackAll" : (st_ == Shift ? "HaloShiftAll" : "HaloUnpackAll");
+    return st_ == Pack ? "HaloPackGroup" : (st_ == Shift ? "HaloShiftGroup" : "HaloUnpackGroup");
   }
   double bytes() const override {
-    return (st_ == Shift ? 1.0 : 2.0) * h_->exchange_bytes();
+    double b = 0;
+    for (int i : dirs_) b += 8.0 * double(h_->box_elems(i));
+    return (st_ == Shift ? 1.0 : 2.0) * b;
   }
   double cost_us() const override {
     if (st_ == Shift) return h_->uses_rccl() ? 10.0 + bytes() / 3.0e5 : 3.0 + bytes() / 2.5e6;
     return copy_cost_us(bytes());
   }
   void launch(void *s, Executor &) const override {
-    if (st_ == Pack) h_->pack_all(s);
-    else if (st_ == Shift) h_->shift_all(s);
-    else h_->unpack_all(s);
+    if (st_ == Pack) h_->pack_group(dirs_, s);
+    else if (st_ == Shift) h_->shift_group(dirs_, s);
+    else h_->unpack_group(dirs_, s);
   }
 
 private:
   std::shared_ptr<const HaloExchange> h_;
   Stage st_;
+  std::vector<int> dirs_;
+  std::string tag_;
 };
 
 } // namespace
@@ -325,70 +331,136 @@ void HaloExchange::shift(int i, void *stream) const {
     const RcclComm &c = *comms_[size_t(i) % comms_.size()];
     c.sendrecv(send_[i].get(), n, nbr_[i], recv_[o].get(), n, nbr_[o], 1, stream);
   } else {
-    TZ_HIP(hipMemcpyAsync(recv_[o].get(), send_[i].get(), n * sizeof(double),
-                          hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    // self neighbour: device copy kernel (captures as a kernel node, unlike hipMemcpyAsync)
+    kern::CopyDesc c{recv_[o].get(), send_[i].get(), n * sizeof(double)};
+    kern::copy_many(&c, 1, stream);
   }
 }
 
-void HaloExchange::pack_all(void *stream) const {
+std::vector<int> HaloExchange::all_dirs() const {
+  std::vector<int> v;
+  for (int i = 0; i < ndirs(); ++i) v.push_back(i);
+  return v;
+}
+
+std::vector<int> HaloExchange::group_dirs(int k) const {
+  // k = 1: faces, k = 2: edges, k = 3: corners, k = 0: edges + corners
+  std::vector<int> v;
+  for (int i = 0; i < ndirs(); ++i) {
+    const int a = (dirs_[i].dx != 0) + (dirs_[i].dy != 0) + (dirs_[i].dz != 0);
+    if (a == k || (k == 0 && a >= 2)) v.push_back(i);
+  }
+  return v;
+}
+
+void HaloExchange::pack_group(const std::vector<int> &dirs, void *stream) const {
   std::vector<kern::BoxDesc> bs;
-  for (int i = 0; i < ndirs(); ++i) bs.push_back(pack_box(i));
+  for (int i : dirs) bs.push_back(pack_box(i));
   for (size_t k = 0; k < bs.size(); k += kern::kMaxBoxes)
     kern::box_copy_many(grid(), bs.data() + k, int(std::min<size_t>(kern::kMaxBoxes, bs.size() - k)),
                         false, stream);
 }
 
-void HaloExchange::unpack_all(void *stream) const {
+void HaloExchange::unpack_group(const std::vector<int> &dirs, void *stream) const {
+  // the ghosts filled by the shifts of `dirs` are those on the opposite sides
   std::vector<kern::BoxDesc> bs;
-  for (int i = 0; i < ndirs(); ++i) bs.push_back(unpack_box(i));
+  for (int i : dirs) bs.push_back(unpack_box(opp_[i]));
   for (size_t k = 0; k < bs.size(); k += kern::kMaxBoxes)
     kern::box_copy_many(grid(), bs.data() + k, int(std::min<size_t>(kern::kMaxBoxes, bs.size() - k)),
                         true, stream);
 }
 
-void HaloExchange::shift_all(void *stream) const {
+void HaloExchange::shift_group(const std::vector<int> &dirs, void *stream) const {
+  if (dirs.empty()) return;
   if (useRccl_) {
     std::vector<RcclComm::Xfer> xs;
-    for (int i = 0; i < ndirs(); ++i) {
+    for (int i : dirs) {
       const int o = opp_[i];
       const size_t n = box_elems(i);
       xs.push_back({send_[i].get(), n, nbr_[i], recv_[o].get(), n, nbr_[o]});
     }
-    comms_[0]->exchange(xs, 1, stream);
+    // one communicator per group (the group's first direction's), so concurrently scheduled
+    // groups never share a communicator
+    comms_[size_t(dirs.front()) % comms_.size()]->exchange(xs, 1, stream);
   } else {
-    for (int i = 0; i < ndirs(); ++i) shift(i, stream);
+    std::vector<kern::CopyDesc> cs;
+    for (int i : dirs) cs.push_back({recv_[opp_[i]].get(), send_[i].get(), box_elems(i) * sizeof(double)});
+    for (size_t k = 0; k < cs.size(); k += kern::kMaxBoxes)
+      kern::copy_many(cs.data() + k, int(std::min<size_t>(kern::kMaxBoxes, cs.size() - k)), stream);
   }
+}
+
+void HaloExchange::pack_all(void *stream) const { pack_group(all_dirs(), stream); }
+void HaloExchange::unpack_all(void *stream) const { unpack_group(all_dirs(), stream); }
+void HaloExchange::shift_all(void *stream) const { shift_group(all_dirs(), stream); }
+
+void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs) {
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  for (int i : dirs) {
+    auto p = std::make_shared<HaloPack>(self, i);
+    auto s = std::make_shared<HaloShift>(self, i);
+    auto u = std::make_shared<HaloUnpack>(self, opp_[i]);
+    g.start_then(p);
+    g.then(p, s);
+    g.then(s, u);
+    g.then_finish(u);
+  }
+}
+
+void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag) {
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, tag);
+  auto s = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Shift, dirs, tag);
+  auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, dirs, tag);
+  g.start_then(p);
+  g.then(p, s);
+  g.then(s, u);
+  g.then_finish(u);
 }
 
 void HaloExchange::add_to_graph(Graph &g) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
-  const bool fusePack = a_.fuse == "pack" || a_.fuse == "all";
-  const bool fuseShift = a_.fuse == "all";
-  TZ_CHECK(a_.fuse == "none" || fusePack, "fuse must be none, pack or all");
-  OpPtr packAll, shiftAll, unpackAll;
-  if (fusePack) {
-    packAll = std::make_shared<HaloStageAll>(self, HaloStageAll::Pack);
-    unpackAll = std::make_shared<HaloStageAll>(self, HaloStageAll::Unpack);
-    g.start_then(packAll);
-    g.then_finish(unpackAll);
-  }
-  if (fuseShift) {
-    shiftAll = std::make_shared<HaloStageAll>(self, HaloStageAll::Shift);
-    g.then(packAll, shiftAll);
-    g.then(shiftAll, unpackAll);
-    return;
-  }
-  std::vector<OpPtr> packs, shifts, unpacks;
-  for (int i = 0; i < ndirs(); ++i) {
-    packs.push_back(fusePack ? packAll : std::make_shared<HaloPack>(self, i));
-    shifts.push_back(std::make_shared<HaloShift>(self, i));
-    unpacks.push_back(fusePack ? unpackAll : std::make_shared<HaloUnpack>(self, i));
-  }
-  for (int i = 0; i < ndirs(); ++i) {
-    if (!fusePack) g.start_then(packs[i]);
-    g.then(packs[i], shifts[i]);
-    g.then(shifts[i], unpacks[opp_[i]]);
-    if (!fusePack) g.then_finish(unpacks[opp_[i]]);
+  const std::string &f = a_.fuse;
+  if (f == "none") {
+    add_chains(g, all_dirs());
+  } else if (f == "all") {
+    add_fused(g, all_dirs(), "all");
+  } else if (f == "pack") {
+    // fused pack / unpack kernels, per-direction transfers
+    auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, all_dirs(), "all");
+    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, all_dirs(), "all");
+    g.start_then(p);
+    g.then_finish(u);
+    for (int i = 0; i < ndirs(); ++i) {
+      auto s = std::make_shared<HaloShift>(self, i);
+      g.then(p, s);
+      g.then(s, u);
+    }
+  } else if (f == "groups" || f == "choice") {
+    // faces and (for 26 neighbours) edges+corners form independent groups; each group is
+    // either one chain per direction or one fused chain. With "choice" the search decides
+    // (ChoiceOp of two CompoundOps; the group touches no other op, so choosing at the group
+    // boundary loses no dependency precision).
+    std::vector<std::pair<std::string, std::vector<int>>> groups = {{"faces", group_dirs(1)}};
+    if (a_.neighbors == 26) groups.push_back({"small", group_dirs(0)});
+    for (auto &gr : groups) {
+      if (f == "groups") {
+        add_fused(g, gr.second, gr.first);
+        continue;
+      }
+      auto split = std::make_shared<Graph>();
+      add_chains(*split, gr.second);
+      auto fused = std::make_shared<Graph>();
+      add_fused(*fused, gr.second, gr.first);
+      std::vector<OpPtr> alts = {
+          std::make_shared<StaticCompoundOp>("he_" + gr.first + "_split", split),
+          std::make_shared<StaticCompoundOp>("he_" + gr.first + "_fused", fused)};
+      auto choice = std::make_shared<StaticChoiceOp>("he_" + gr.first, alts);
+      g.start_then(choice);
+      g.then_finish(choice);
+    }
+  } else {
+    TZ_THROW("fuse must be none, pack, all, groups or choice (got " << f << ")");
   }
 }
 

@@ -98,7 +98,10 @@ struct HaloArgs {
   int neighbors = 6;              // 6 (faces) or 26 (faces, edges, corners)
   std::string order = "xyzq";     // "xyzq" (x fastest, q slowest) or "qxyz"
   std::string transport = "auto"; // "rccl", "copy" (self-neighbour only), "auto"
-  std::string fuse = "none";      // "none", "pack" (fused pack+unpack), "all" (one op each stage)
+  // "choice": per group (faces / edges+corners) the search chooses per-direction or fused ops;
+  // "none": per-direction ops; "groups": fused per group; "pack": fused pack+unpack with
+  // per-direction transfers; "all": one op per stage
+  std::string fuse = "choice";
   int comms = 0;                  // RCCL communicators (0 = one per direction)
   int rank = 0, size = 1;
   int px = 0, py = 0, pz = 0;     // rank grid (0 = from prime factors, reference style)
@@ -150,9 +153,18 @@ public:
   void pack_all(void *stream) const;
   void unpack_all(void *stream) const;
   void shift_all(void *stream) const;
+  /// one launch / one RCCL group for a set of directions (unpack: their opposite ghosts)
+  void pack_group(const std::vector<int> &dirs, void *stream) const;
+  void unpack_group(const std::vector<int> &dirs, void *stream) const;
+  void shift_group(const std::vector<int> &dirs, void *stream) const;
+  std::vector<int> all_dirs() const;
+  /// k = 1 faces, 2 edges, 3 corners, 0 edges + corners
+  std::vector<int> group_dirs(int k) const;
   bool uses_rccl() const { return useRccl_; }
 
 private:
+  void add_chains(Graph &g, const std::vector<int> &dirs);
+  void add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag);
   HaloArgs a_;
   std::vector<Dir> dirs_;
   std::vector<int> opp_, nbr_;

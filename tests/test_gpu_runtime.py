@@ -41,15 +41,15 @@ def test_gpu_graph_decisions_real_streams(tz, gpu):
 
 
 @pytest.mark.parametrize("mode", ["eager", "graph"])
-@pytest.mark.parametrize("fuse", ["none", "pack", "all"])
+@pytest.mark.parametrize("fuse", ["none", "pack", "all", "groups", "choice"])
 @pytest.mark.parametrize("neighbors", [6, 26])
 def test_halo_exchange_correct(tz, gpu, mode, fuse, neighbors):
     halo, g = _small_halo(tz, neighbors=neighbors, fuse=fuse)
     m = tz.ExecMode.Graph if mode == "graph" else tz.ExecMode.Eager
     rt = tz.HipRuntime(device=0, n_streams=3, mode=m)
     for seed in range(3):
-        seq = tz.random_rollout(tz.State(g, tz.Platform(3)), seed)
-        seq, _ = tz.remove_redundant_syncs(seq, _final_graph(tz, g), 3)
+        final = _rollout_state(tz, g, 3, seed)
+        seq, _ = tz.remove_redundant_syncs(final.sequence, final.graph, 3)
         halo.init_grid()
         rt.device_sync()
         assert halo.check_grid() > 0  # ghosts not yet filled
@@ -58,6 +58,16 @@ def test_halo_exchange_correct(tz, gpu, mode, fuse, neighbors):
         rt.run(1)
         rt.device_sync()
         assert halo.check_grid() == 0, seq.desc()
+
+
+def _rollout_state(tz, g, streams, seed):
+    import random
+
+    rng = random.Random(seed)
+    s = tz.State(g, tz.Platform(streams))
+    while not s.complete():
+        s = s.apply(rng.choice(s.get_decisions()))
+    return s
 
 
 def _final_graph(tz, g):
