@@ -34,7 +34,8 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=512, help="interior cells per axis per rank")
     ap.add_argument("--neighbors", type=int, default=26)
     ap.add_argument("--streams", type=int, default=4)
-    ap.add_argument("--fuse", default="none")
+    ap.add_argument("--fuse", default="choice",
+                    help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=40)
     ap.add_argument("--search-budget-s", type=float, default=120.0)
     ap.add_argument("--bench-iters", type=int, default=20)
