@@ -34,6 +34,8 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=512, help="interior cells per axis per rank")
     ap.add_argument("--neighbors", type=int, default=26)
     ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--order", default="xyzq", choices=["xyzq", "qxyz"],
+                    help="grid storage order (reference halo driver: xyzq)")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=40)
@@ -59,7 +61,7 @@ def main() -> int:
         print(f"bench.py: warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
     t_setup = time.time()
-    cfg = HaloConfig(n=args.n, neighbors=args.neighbors, fuse=args.fuse)
+    cfg = HaloConfig(n=args.n, neighbors=args.neighbors, fuse=args.fuse, order=args.order)
     halo, graph = build_halo(cfg, ctrl, device)
     mode = tz.ExecMode.Graph if args.search_mode == "graph" else tz.ExecMode.Eager
     rt = tz.HipRuntime(device=device, n_streams=args.streams, mode=mode, watchdog_s=120.0)

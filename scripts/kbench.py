@@ -34,9 +34,11 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--neighbors", type=int, default=26)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--order", default="xyzq")
     args = ap.parse_args()
     torch.zeros(1, device="cuda")
-    h, _ = build_halo(HaloConfig(n=args.n, neighbors=args.neighbors), tz.SelfCtrl(), device=0)
+    h, _ = build_halo(HaloConfig(n=args.n, neighbors=args.neighbors, order=args.order), tz.SelfCtrl(), device=0)
+    print(json.dumps({"order": args.order, "grid_bytes": h.grid_elems() * 8}), flush=True)
     st = torch.cuda.current_stream().cuda_stream
     out = []
 

@@ -188,7 +188,7 @@ __device__ __forceinline__ double halo_expect(const HaloGeom &g, int64_t lin, in
   const int64_t z = r % Z;
   const int q = int(r / Z);
   if (g.order == 0) idx = q * g.sq + z * g.sz + y * g.sy + x + g.xoff;
-  else idx = q + int64_t(g.nq) * (x + X * (y + Y * z));
+  else idx = q + int64_t(g.nq) * (x + g.xoff) + y * g.sy + z * g.sz;
   const int gx = (x < g.g || x >= g.nx + g.g), gy = (y < g.g || y >= g.ny + g.g),
             gz = (z < g.g || z >= g.nz + g.g);
   const int k = gx + gy + gz;
