@@ -104,7 +104,19 @@ def main() -> int:
 
     def timed(m):
         rt.set_mode(m)
-        rt.prepare(best)
+        # every rank must agree on the mode (a failed graph build on one rank would otherwise
+        # leave the others blocked in a collective)
+        ok = 1.0
+        try:
+            rt.prepare(best)
+            ok = 1.0 if rt.effective_mode == m else 0.0
+        except Exception as e:  # noqa: BLE001
+            print(f"bench.py: rank {rank}: {m} preparation failed: {e}", file=sys.stderr)
+            ok = 0.0
+        if ctrl.allreduce_max([1.0 - ok])[0] > 0:
+            rt.set_mode(tz.ExecMode.Eager)
+            rt.prepare(best)
+            return None, tz.ExecMode.Eager
         rt.run(args.warmup)
         rt.device_sync()
         ctrl.barrier()
@@ -117,7 +129,7 @@ def main() -> int:
 
     t_eager, _ = timed(tz.ExecMode.Eager)
     t_graph, eff = timed(tz.ExecMode.Graph)
-    graph_ok = eff == tz.ExecMode.Graph
+    graph_ok = t_graph is not None and eff == tz.ExecMode.Graph
     use_graph = graph_ok and t_graph < t_eager
     t = t_graph if use_graph else t_eager
     ms = t / args.steps * 1e3
