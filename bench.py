@@ -34,7 +34,7 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=512, help="interior cells per axis per rank")
     ap.add_argument("--neighbors", type=int, default=26)
     ap.add_argument("--streams", type=int, default=4)
-    ap.add_argument("--order", default="xyzq", choices=["xyzq", "qxyz"],
+    ap.add_argument("--order", default="qxyz", choices=["xyzq", "qxyz"],
                     help="grid storage order (reference halo driver: xyzq)")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
@@ -159,6 +159,8 @@ def main() -> int:
                 "streams": args.streams,
                 "neighbors": args.neighbors,
                 "rank_grid": list(halo.rank_grid()),
+                "storage_order": args.order,
+                "fuse": args.fuse,
                 "strategy": args.strategy,
             },
             "search_wall_s": search_wall,
