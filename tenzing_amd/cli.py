@@ -1,0 +1,182 @@
+"""``python -m tenzing_amd`` — search / replay / rules / env.
+
+  python -m tenzing_amd search --workload halo --solver mcts --strategy FastMin --iters 100
+  python -m tenzing_amd search --workload spmv --solver dfs --max-seqs 15000 --csv spmv.csv
+  python -m tenzing_amd search --workload halo --replay halo.csv      # MCTS on recorded timings
+  python -m tenzing_amd search --workload fused --sim                  # hardware-free (cost model)
+  python -m tenzing_amd rules spmv.csv --out spmv_                     # design rules
+  python -m tenzing_amd env --topology
+
+Multi-GPU: ``torchrun --nproc-per-node 8 -m tenzing_amd search ...`` (one process per GPU).
+Reference drivers: tenzing-mcts/examples/{halo,spmv}_*.cu, tenzing-dfs/examples/spmv.cu,
+tenzing-mcts/examples/mcts_csv_*.cu (CSV replay, not built in the reference).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+
+
+def _build_workload(a, ctrl, device, setup):
+    import tenzing_amd as tz
+    from tenzing_amd.models import HaloConfig, SpmvConfig, build_fused, build_halo, build_spmv
+
+    hc = HaloConfig(n=a.halo_n, nq=a.nq, ghost=a.ghost, neighbors=a.neighbors, order=a.order,
+                    fuse=a.fuse, transport=a.transport)
+    sc = SpmvConfig(m=a.spmv_m)
+    if a.workload == "halo":
+        h, g = build_halo(hc, ctrl, device, setup)
+        return g, {"halo": h}
+    if a.workload == "spmv":
+        s, g = build_spmv(sc, ctrl, device, setup)
+        return g, {"spmv": s}
+    if a.workload == "fused":
+        h, s, g = build_fused(hc, sc, ctrl, device, setup)
+        return g, {"halo": h, "spmv": s}
+    if a.workload == "diamond":
+        g = tz.Graph()
+        k = [tz.BusyKernelOp(f"k{i}", us) for i, us in enumerate((20, 100, 100, 20), 1)]
+        g.start_then(k[0])
+        g.then(k[0], k[1])
+        g.then(k[0], k[2])
+        g.then(k[1], k[3])
+        g.then(k[2], k[3])
+        g.then_finish(k[3])
+        return g, {}
+    raise SystemExit(f"unknown workload {a.workload}")
+
+
+def cmd_search(a) -> int:
+    import tenzing_amd as tz
+    from tenzing_amd.parallel import init_ctrl, select_device
+
+    ctrl = init_ctrl()
+    hw = not (a.sim or a.replay)
+    device = select_device() if hw else -1
+    if hw and device < 0:
+        raise SystemExit("no GPU visible: use --sim or --replay")
+    if hw and a.bind_cpus:
+        from tenzing_amd.utils.env import bind_local_cpus
+
+        bind_local_cpus(device)
+    g, wl = _build_workload(a, ctrl, device, hw)
+    if a.dump_graph and ctrl.rank == 0:
+        with open(a.dump_graph, "w") as f:
+            f.write(g.dump_graphviz(a.workload))
+    plat = tz.Platform(a.streams)
+    bo = tz.BenchOpts(n_iters=a.bench_iters, max_retries=a.max_retries, target_secs=a.target_secs)
+    rt = None
+    if a.replay:
+        bench = tz.CsvBenchmarker(a.replay, g)
+    elif a.sim:
+        bench = tz.SimBenchmarker(a.streams)
+    else:
+        mode = tz.ExecMode.Graph if a.mode == "graph" else tz.ExecMode.Eager
+        rt = tz.HipRuntime(device=device, n_streams=a.streams, mode=mode, watchdog_s=a.watchdog)
+        bench = tz.EmpiricalBenchmarker(rt, ctrl)
+    t0 = time.time()
+    if a.solver == "dfs":
+        o = tz.DfsOpts()
+        o.max_seqs = a.max_seqs
+        o.bench = bo
+        res = tz.dfs_explore(g, plat, bench, ctrl, o)
+    else:
+        o = tz.MctsOpts()
+        o.n_iters = a.iters
+        o.time_budget_s = a.time_budget
+        o.strategy = a.strategy
+        o.seed = a.seed
+        o.expand_rollout = not a.no_expand_rollout
+        o.dump_tree = a.dump_tree
+        o.bench = bo
+        if a.checkpoint:
+            o.checkpoint_path = a.checkpoint
+            o.checkpoint_every = 10
+        if a.resume:
+            o.resume_path = a.resume
+        res = tz.mcts_explore(g, plat, bench, ctrl, o)
+    if ctrl.rank == 0:
+        if a.csv:
+            with open(a.csv, "w") as f:
+                f.write(res.dump_csv())
+        if a.jsonl:
+            with open(a.jsonl, "w") as f:
+                f.write(res.dump_jsonl())
+        b = res.best()
+        summary = {"workload": a.workload, "solver": a.solver, "ranks": ctrl.size,
+                   "streams": a.streams, "candidates": len(res.sims), "search_wall_s": res.wall_s,
+                   "stop_reason": res.stop_reason, "counters": res.counters(),
+                   "elapsed_s": time.time() - t0}
+        if b >= 0:
+            summary["best_pct10_ms"] = res.sims[b].res.pct10 * 1e3
+            summary["best_schedule"] = json.loads(res.sims[b].seq.json())
+        print(json.dumps(summary))
+    return 0
+
+
+def cmd_rules(a) -> int:
+    from tenzing_amd.utils import postprocess
+
+    return postprocess.main([a.results] + (["--out", a.out] if a.out else []))
+
+
+def cmd_env(a) -> int:
+    from tenzing_amd.utils.env import env_report
+
+    import tenzing_amd as tz
+
+    print(json.dumps(env_report(0 if tz.hip_device_count() else None, a.topology), indent=1))
+    return 0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m tenzing_amd", description=__doc__.splitlines()[0])
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    s = sub.add_parser("search")
+    s.add_argument("--workload", default="halo", choices=["halo", "spmv", "fused", "diamond"])
+    s.add_argument("--solver", default="mcts", choices=["mcts", "dfs"])
+    s.add_argument("--strategy", default="FastMin")
+    s.add_argument("--iters", type=int, default=300)
+    s.add_argument("--time-budget", type=float, default=0.0)
+    s.add_argument("--max-seqs", type=int, default=15000)
+    s.add_argument("--streams", type=int, default=2)
+    s.add_argument("--bench-iters", type=int, default=50)
+    s.add_argument("--max-retries", type=int, default=10)
+    s.add_argument("--target-secs", type=float, default=0.01)
+    s.add_argument("--mode", default="eager", choices=["eager", "graph"])
+    s.add_argument("--sim", action="store_true", help="discrete-event cost model, no GPU")
+    s.add_argument("--replay", default="", help="results CSV to replay instead of running")
+    s.add_argument("--seed", type=int, default=0)
+    s.add_argument("--no-expand-rollout", action="store_true")
+    s.add_argument("--dump-tree", action="store_true")
+    s.add_argument("--dump-graph", default="")
+    s.add_argument("--checkpoint", default="")
+    s.add_argument("--resume", default="")
+    s.add_argument("--csv", default="")
+    s.add_argument("--jsonl", default="")
+    s.add_argument("--watchdog", type=float, default=120.0)
+    s.add_argument("--bind-cpus", action="store_true")
+    s.add_argument("--halo-n", type=int, default=512)
+    s.add_argument("--nq", type=int, default=3)
+    s.add_argument("--ghost", type=int, default=3)
+    s.add_argument("--neighbors", type=int, default=6)
+    s.add_argument("--order", default="xyzq")
+    s.add_argument("--fuse", default="choice")
+    s.add_argument("--transport", default="auto")
+    s.add_argument("--spmv-m", type=int, default=150_000)
+    s.set_defaults(fn=cmd_search)
+    r = sub.add_parser("rules")
+    r.add_argument("results")
+    r.add_argument("--out", default="")
+    r.set_defaults(fn=cmd_rules)
+    e = sub.add_parser("env")
+    e.add_argument("--topology", action="store_true")
+    e.set_defaults(fn=cmd_env)
+    a = ap.parse_args(argv)
+    return a.fn(a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -12,6 +12,8 @@
 #include "kernels/kernels.hpp"
 #include "workloads/workloads.hpp"
 
+#include <hip/hip_runtime_api.h>
+
 #include <csignal>
 #include <cstdlib>
 #include <execinfo.h>
@@ -150,6 +152,11 @@ PYBIND11_MODULE(_tz, m) {
   m.def("set_log_level", [](int l) { set_log_level(LogLevel(l)); });
   m.def("set_log_rank", [](int r) { log_rank() = r; });
   m.def("hip_device_count", &hip_device_count);
+  m.def("pci_bus_id", [](int dev) {
+    char buf[64] = {0};
+    if (hipDeviceGetPCIBusId(buf, sizeof(buf), dev) != hipSuccess) return std::string();
+    return std::string(buf);
+  });
   m.def("rccl_version", &RcclComm::version);
   m.def("strategy_names", &strategy_names);
   m.def("prime_factors", &prime_factors);
