@@ -1,0 +1,14 @@
+"""Torch-tensor front ends of the hand-written gfx950 kernels (``tenzing_amd._tz.kernels``).
+
+Every function checks device, dtype, contiguity and sizes on the host before launching (the
+kernels index raw pointers), then launches on torch's current stream. They fail loudly when the
+native extension or a GPU is missing; there is no silent PyTorch fallback.
+"""
+from .kernels import (  # noqa: F401
+    box_pack,
+    box_unpack,
+    copy_,
+    csr_spmv,
+    gather,
+    vector_add,
+)
