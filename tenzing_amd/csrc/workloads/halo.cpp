@@ -171,11 +171,28 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
     sq_ = sz_ * Z;
     gridElems_ = size_t(sq_ * a_.nq);
   } else {
-    // (q,x) runs are contiguous; pad x so the interior run starts 64-B aligned and pad rows to
-    // whole 128-B lines: y/z-face rows are then dwordx4-vectorizable and an x-face row is one
-    // 72-byte run (vs 3 x 24-byte runs a whole 4 KB apart in XYZQ)
-    xoff_ = 0;
-    while ((int64_t(a_.nq) * (xoff_ + a_.ghost)) % 8 != 0) ++xoff_;
+    // (q,x) runs are contiguous, so an x-face row is ONE nq*ghost run (72 B for 3x3) instead of
+    // nq runs 4 KB apart (XYZQ). Rows are padded to whole 128-B lines and the x padding is
+    // chosen so that (1) each of the four x runs (interior low/high, ghost low/high) touches as
+    // few 128-B lines as possible — every x-face row then costs one line fetch — and (2) the
+    // interior run is 16-B aligned (dwordx4 y/z-face rows), preferring 128-B alignment.
+    const int64_t q = a_.nq, g = a_.ghost, n = a_.nx;
+    auto lines = [&](int64_t x0, int64_t len) { // 128-B lines touched by elements [x0,x0+len)
+      const int64_t b0 = x0 * 8, b1 = (x0 + len) * 8 - 1;
+      return b1 / 128 - b0 / 128 + 1;
+    };
+    int64_t best = -1, bestCost = 0;
+    for (int64_t off = 0; off < 16; ++off) {
+      if ((q * (off + g)) % 2 != 0) continue;
+      int64_t cost = lines(q * (off + g), q * g) + lines(q * (off + n), q * g) + lines(q * off, q * g) +
+                     lines(q * (off + n + g), q * g);
+      cost = cost * 4 + ((q * (off + g)) % 16 == 0 ? 0 : ((q * (off + g)) % 8 == 0 ? 1 : 2));
+      if (best < 0 || cost < bestCost) {
+        best = off;
+        bestCost = cost;
+      }
+    }
+    xoff_ = best < 0 ? 0 : best;
     pitch_ = round_up(int64_t(a_.nq) * (xoff_ + X), 16);
     sy_ = pitch_;
     sz_ = pitch_ * Y;
@@ -451,11 +468,13 @@ void HaloExchange::add_to_graph(Graph &g) {
     // boundary loses no dependency precision).
     std::vector<std::pair<std::string, std::vector<int>>> groups = {{"faces", group_dirs(1)}};
     if (a_.neighbors == 26) groups.push_back({"small", group_dirs(0)});
+    if (f == "groups") {
+      for (auto &gr : groups) add_fused(g, gr.second, gr.first);
+      return;
+    }
+    // per group: split chains vs one fused chain
+    auto grouped = std::make_shared<Graph>();
     for (auto &gr : groups) {
-      if (f == "groups") {
-        add_fused(g, gr.second, gr.first);
-        continue;
-      }
       auto split = std::make_shared<Graph>();
       add_chains(*split, gr.second);
       auto fused = std::make_shared<Graph>();
@@ -464,9 +483,23 @@ void HaloExchange::add_to_graph(Graph &g) {
           std::make_shared<StaticCompoundOp>("he_" + gr.first + "_split", split),
           std::make_shared<StaticCompoundOp>("he_" + gr.first + "_fused", fused)};
       auto choice = std::make_shared<StaticChoiceOp>("he_" + gr.first, alts);
-      g.start_then(choice);
-      g.then_finish(choice);
+      grouped->start_then(choice);
+      grouped->then_finish(choice);
     }
+    if (groups.size() == 1) {
+      g.start_then(std::make_shared<StaticCompoundOp>("he_grouped", grouped));
+      g.then_finish(g.op(g.find("he_grouped")));
+      return;
+    }
+    // 26 neighbours: additionally one chain for every direction (a single launch per stage
+    // avoids the two groups' kernels competing for CUs)
+    auto all = std::make_shared<Graph>();
+    add_fused(*all, all_dirs(), "all");
+    std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>("he_grouped", grouped),
+                              std::make_shared<StaticCompoundOp>("he_allfused", all)};
+    auto choice = std::make_shared<StaticChoiceOp>("he_exchange", top);
+    g.start_then(choice);
+    g.then_finish(choice);
   } else {
     TZ_THROW("fuse must be none, pack, all, groups or choice (got " << f << ")");
   }
