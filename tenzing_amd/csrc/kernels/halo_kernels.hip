@@ -29,6 +29,11 @@
 namespace tz {
 namespace kern {
 
+BoxTuning &box_tuning() {
+  static BoxTuning t;
+  return t;
+}
+
 namespace {
 
 #define TZ_HIP_LAUNCH_CHECK()                                                                      \
@@ -67,7 +72,6 @@ struct DevBatch {
 };
 
 constexpr int kThreads = 256;
-constexpr int kUnroll = 4;
 
 DevDesc make_dev(const BoxDesc &b) {
   DevDesc d{};
@@ -93,14 +97,25 @@ DevDesc make_dev(const BoxDesc &b) {
 }
 
 uint32_t blocks_for(const DevDesc &d) {
-  const uint64_t per = uint64_t(kThreads) * kUnroll;
+  const BoxTuning &t = box_tuning();
+  const uint64_t per = uint64_t(kThreads) * uint64_t(t.unroll);
   uint64_t b = (uint64_t(d.items) + per - 1) / per;
-  return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(b, 4096)));
+  return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(b, uint64_t(t.max_blocks))));
 }
 
+typedef double dbl2_t __attribute__((ext_vector_type(2)));
 template <int VEC> struct Vec;
 template <> struct Vec<1> { using T = double; };
-template <> struct Vec<2> { using T = double2; };
+template <> struct Vec<2> { using T = dbl2_t; };
+
+template <bool NT, typename T> __device__ __forceinline__ T ld(const T *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename T> __device__ __forceinline__ void st(T *p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 
 template <int VEC>
 __device__ __forceinline__ int64_t grid_index(const DevDesc &d, uint32_t it) {
@@ -114,45 +129,45 @@ __device__ __forceinline__ int64_t grid_index(const DevDesc &d, uint32_t it) {
          int64_t(xv) * VEC;
 }
 
-template <int VEC, bool UNPACK>
+template <int VEC, bool UNPACK, int U, bool NT>
 __device__ __forceinline__ void box_body(double *__restrict__ grid, const DevDesc &d, uint32_t tid,
                                          uint32_t nthreads) {
   using T = typename Vec<VEC>::T;
   T *__restrict__ buf = reinterpret_cast<T *>(d.buf);
   uint32_t it = tid;
-  for (; it + (kUnroll - 1) * nthreads < d.items; it += kUnroll * nthreads) {
-    T v[kUnroll];
-    int64_t g[kUnroll];
+  for (; it + (U - 1) * nthreads < d.items; it += U * nthreads) {
+    T v[U];
+    int64_t g[U];
 #pragma unroll
-    for (int k = 0; k < kUnroll; ++k) g[k] = grid_index<VEC>(d, it + k * nthreads);
+    for (int k = 0; k < U; ++k) g[k] = grid_index<VEC>(d, it + k * nthreads);
     if (UNPACK) {
 #pragma unroll
-      for (int k = 0; k < kUnroll; ++k) v[k] = buf[it + k * nthreads];
+      for (int k = 0; k < U; ++k) v[k] = buf[it + k * nthreads];
 #pragma unroll
-      for (int k = 0; k < kUnroll; ++k) *reinterpret_cast<T *>(grid + g[k]) = v[k];
+      for (int k = 0; k < U; ++k) st<NT>(reinterpret_cast<T *>(grid + g[k]), v[k]);
     } else {
 #pragma unroll
-      for (int k = 0; k < kUnroll; ++k) v[k] = *reinterpret_cast<const T *>(grid + g[k]);
+      for (int k = 0; k < U; ++k) v[k] = ld<NT>(reinterpret_cast<const T *>(grid + g[k]));
 #pragma unroll
-      for (int k = 0; k < kUnroll; ++k) buf[it + k * nthreads] = v[k];
+      for (int k = 0; k < U; ++k) buf[it + k * nthreads] = v[k];
     }
   }
   for (; it < d.items; it += nthreads) {
     const int64_t g = grid_index<VEC>(d, it);
-    if (UNPACK) *reinterpret_cast<T *>(grid + g) = buf[it];
-    else buf[it] = *reinterpret_cast<const T *>(grid + g);
+    if (UNPACK) st<NT>(reinterpret_cast<T *>(grid + g), buf[it]);
+    else buf[it] = ld<NT>(reinterpret_cast<const T *>(grid + g));
   }
 }
 
-template <bool UNPACK>
+template <bool UNPACK, int U, bool NT>
 __global__ __launch_bounds__(kThreads) void box_copy_one_k(double *__restrict__ grid, DevDesc d) {
   const uint32_t tid = blockIdx.x * kThreads + threadIdx.x;
   const uint32_t nth = gridDim.x * kThreads;
-  if (d.vec == 2) box_body<2, UNPACK>(grid, d, tid, nth);
-  else box_body<1, UNPACK>(grid, d, tid, nth);
+  if (d.vec == 2) box_body<2, UNPACK, U, NT>(grid, d, tid, nth);
+  else box_body<1, UNPACK, U, NT>(grid, d, tid, nth);
 }
 
-template <bool UNPACK>
+template <bool UNPACK, int U, bool NT>
 __global__ __launch_bounds__(kThreads) void box_copy_many_k(double *__restrict__ grid, DevBatch b) {
   int box = 0;
   while (box + 1 < b.n && blockIdx.x >= b.block_start[box + 1]) ++box;
@@ -160,8 +175,42 @@ __global__ __launch_bounds__(kThreads) void box_copy_many_k(double *__restrict__
   const uint32_t nb = b.block_start[box + 1] - b.block_start[box];
   const uint32_t tid = (blockIdx.x - b.block_start[box]) * kThreads + threadIdx.x;
   const uint32_t nth = nb * kThreads;
-  if (d.vec == 2) box_body<2, UNPACK>(grid, d, tid, nth);
-  else box_body<1, UNPACK>(grid, d, tid, nth);
+  if (d.vec == 2) box_body<2, UNPACK, U, NT>(grid, d, tid, nth);
+  else box_body<1, UNPACK, U, NT>(grid, d, tid, nth);
+}
+
+// host dispatch over (unpack, unroll, nt)
+template <bool UNPACK, int U, bool NT>
+void launch_one(dim3 g, hipStream_t s, double *grid, const DevDesc &d) {
+  hipLaunchKernelGGL((box_copy_one_k<UNPACK, U, NT>), g, dim3(kThreads), 0, s, grid, d);
+}
+template <bool UNPACK, int U, bool NT>
+void launch_many(dim3 g, hipStream_t s, double *grid, const DevBatch &b) {
+  hipLaunchKernelGGL((box_copy_many_k<UNPACK, U, NT>), g, dim3(kThreads), 0, s, grid, b);
+}
+
+template <bool UNPACK>
+void dispatch_one(dim3 g, hipStream_t s, double *grid, const DevDesc &d) {
+  const BoxTuning &t = box_tuning();
+  if (t.unroll >= 8) {
+    if (t.nt_grid) launch_one<UNPACK, 8, true>(g, s, grid, d);
+    else launch_one<UNPACK, 8, false>(g, s, grid, d);
+  } else {
+    if (t.nt_grid) launch_one<UNPACK, 4, true>(g, s, grid, d);
+    else launch_one<UNPACK, 4, false>(g, s, grid, d);
+  }
+}
+
+template <bool UNPACK>
+void dispatch_many(dim3 g, hipStream_t s, double *grid, const DevBatch &b) {
+  const BoxTuning &t = box_tuning();
+  if (t.unroll >= 8) {
+    if (t.nt_grid) launch_many<UNPACK, 8, true>(g, s, grid, b);
+    else launch_many<UNPACK, 8, false>(g, s, grid, b);
+  } else {
+    if (t.nt_grid) launch_many<UNPACK, 4, true>(g, s, grid, b);
+    else launch_many<UNPACK, 4, false>(g, s, grid, b);
+  }
 }
 
 // ---- grid initialization / verification (test support; not on the timed path)
@@ -246,8 +295,8 @@ void box_copy(double *grid, const BoxDesc &b, bool unpack, void *stream) {
   if (d.items == 0) return;
   const dim3 grid_dim(blocks_for(d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (unpack) hipLaunchKernelGGL(box_copy_one_k<true>, grid_dim, dim3(kThreads), 0, s, grid, d);
-  else hipLaunchKernelGGL(box_copy_one_k<false>, grid_dim, dim3(kThreads), 0, s, grid, d);
+  if (unpack) dispatch_one<true>(grid_dim, s, grid, d);
+  else dispatch_one<false>(grid_dim, s, grid, d);
   TZ_HIP_LAUNCH_CHECK();
 }
 
@@ -268,8 +317,8 @@ void box_copy_many(double *grid, const BoxDesc *boxes, int n, bool unpack, void 
   if (b.n == 0) return;
   b.block_start[b.n] = total;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (unpack) hipLaunchKernelGGL(box_copy_many_k<true>, dim3(total), dim3(kThreads), 0, s, grid, b);
-  else hipLaunchKernelGGL(box_copy_many_k<false>, dim3(total), dim3(kThreads), 0, s, grid, b);
+  if (unpack) dispatch_many<true>(dim3(total), s, grid, b);
+  else dispatch_many<false>(dim3(total), s, grid, b);
   TZ_HIP_LAUNCH_CHECK();
 }
 

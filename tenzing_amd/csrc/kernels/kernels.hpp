@@ -23,6 +23,14 @@ struct BoxDesc {
 
 constexpr int kMaxBoxes = 32;
 
+/// launch tuning of the box kernels (process-wide; measured defaults)
+struct BoxTuning {
+  int unroll = 4;       // items in flight per lane: 4 or 8
+  bool nt_grid = false; // non-temporal grid loads (pack) / stores (unpack)
+  int max_blocks = 4096; // cap per box (grid-stride beyond)
+};
+BoxTuning &box_tuning();
+
 /// pack (grid -> buf) or unpack (buf -> grid) one box
 void box_copy(double *grid, const BoxDesc &d, bool unpack, void *stream);
 /// pack/unpack up to kMaxBoxes boxes in ONE launch (fused multi-face halo pack/unpack)
