@@ -671,14 +671,16 @@ PYBIND11_MODULE(_tz, m) {
     kern::iota_f64(n, base, scale, reinterpret_cast<double *>(a), P(s));
   }, py::arg("n"), py::arg("base"), py::arg("scale"), py::arg("a"), py::arg("stream") = 0);
   k.def("empty", [](uintptr_t s) { kern::empty(P(s)); }, py::arg("stream") = 0);
-  k.def("set_box_tuning", [](int unroll, bool nt, int maxBlocks) {
+  k.def("set_box_tuning", [](int unroll, bool ntPack, bool ntUnpack, int maxBlocks) {
     kern::box_tuning().unroll = unroll;
-    kern::box_tuning().nt_grid = nt;
+    kern::box_tuning().nt_pack = ntPack;
+    kern::box_tuning().nt_unpack = ntUnpack;
     kern::box_tuning().max_blocks = maxBlocks;
-  }, py::arg("unroll") = 4, py::arg("nt_grid") = false, py::arg("max_blocks") = 4096);
+  }, py::arg("unroll") = 4, py::arg("nt_pack") = true, py::arg("nt_unpack") = false,
+     py::arg("max_blocks") = 4096);
   k.def("get_box_tuning", []() {
     const auto &t = kern::box_tuning();
-    return py::make_tuple(t.unroll, t.nt_grid, t.max_blocks);
+    return py::make_tuple(t.unroll, t.nt_pack, t.nt_unpack, t.max_blocks);
   });
   k.def("copy_bytes", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
     kern::copy_bytes(P(dst), P(src), n, P(s));

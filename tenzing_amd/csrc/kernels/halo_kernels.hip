@@ -189,26 +189,31 @@ void launch_many(dim3 g, hipStream_t s, double *grid, const DevBatch &b) {
   hipLaunchKernelGGL((box_copy_many_k<UNPACK, U, NT>), g, dim3(kThreads), 0, s, grid, b);
 }
 
+template <bool UNPACK> bool use_nt() {
+  const BoxTuning &t = box_tuning();
+  return UNPACK ? t.nt_unpack : t.nt_pack;
+}
+
 template <bool UNPACK>
 void dispatch_one(dim3 g, hipStream_t s, double *grid, const DevDesc &d) {
-  const BoxTuning &t = box_tuning();
-  if (t.unroll >= 8) {
-    if (t.nt_grid) launch_one<UNPACK, 8, true>(g, s, grid, d);
+  const bool nt = use_nt<UNPACK>();
+  if (box_tuning().unroll >= 8) {
+    if (nt) launch_one<UNPACK, 8, true>(g, s, grid, d);
     else launch_one<UNPACK, 8, false>(g, s, grid, d);
   } else {
-    if (t.nt_grid) launch_one<UNPACK, 4, true>(g, s, grid, d);
+    if (nt) launch_one<UNPACK, 4, true>(g, s, grid, d);
     else launch_one<UNPACK, 4, false>(g, s, grid, d);
   }
 }
 
 template <bool UNPACK>
 void dispatch_many(dim3 g, hipStream_t s, double *grid, const DevBatch &b) {
-  const BoxTuning &t = box_tuning();
-  if (t.unroll >= 8) {
-    if (t.nt_grid) launch_many<UNPACK, 8, true>(g, s, grid, b);
+  const bool nt = use_nt<UNPACK>();
+  if (box_tuning().unroll >= 8) {
+    if (nt) launch_many<UNPACK, 8, true>(g, s, grid, b);
     else launch_many<UNPACK, 8, false>(g, s, grid, b);
   } else {
-    if (t.nt_grid) launch_many<UNPACK, 4, true>(g, s, grid, b);
+    if (nt) launch_many<UNPACK, 4, true>(g, s, grid, b);
     else launch_many<UNPACK, 4, false>(g, s, grid, b);
   }
 }

@@ -25,9 +25,10 @@ constexpr int kMaxBoxes = 32;
 
 /// launch tuning of the box kernels (process-wide; measured defaults)
 struct BoxTuning {
-  int unroll = 4;       // items in flight per lane: 4 or 8
-  bool nt_grid = false; // non-temporal grid loads (pack) / stores (unpack)
-  int max_blocks = 4096; // cap per box (grid-stride beyond)
+  int unroll = 4;         // items in flight per lane: 4 or 8 (8: no gain, scripts/ktune.py)
+  bool nt_pack = true;    // non-temporal grid loads in pack: -27 % pack time in pipeline context
+  bool nt_unpack = false; // non-temporal grid stores in unpack: +5 % (off)
+  int max_blocks = 4096;  // cap per box (grid-stride beyond)
 };
 BoxTuning &box_tuning();
 
