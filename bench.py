@@ -45,6 +45,8 @@ def main() -> int:
     ap.add_argument("--strategy", default="FastMin")
     ap.add_argument("--search-mode", default="eager", choices=["eager", "graph"])
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--graph-unroll", type=int, default=10,
+                    help="iterations per hipGraph launch when timing the graph-compiled schedule")
     ap.add_argument("--csv", default="", help="write the search results CSV here (rank 0)")
     args = ap.parse_args()
 
@@ -128,6 +130,7 @@ def main() -> int:
         return ctrl.allreduce_max([dt])[0], rt.effective_mode
 
     t_eager, _ = timed(tz.ExecMode.Eager)
+    rt.set_graph_unroll(args.graph_unroll)
     t_graph, eff = timed(tz.ExecMode.Graph)
     graph_ok = t_graph is not None and eff == tz.ExecMode.Graph
     use_graph = graph_ok and t_graph < t_eager
@@ -170,6 +173,7 @@ def main() -> int:
             "eager_ms_per_step": t_eager / args.steps * 1e3,
             "graph_ms_per_step": (t_graph / args.steps * 1e3) if graph_ok else None,
             "timed_mode": "hipgraph" if use_graph else "eager",
+            "graph_unroll": args.graph_unroll,
             "halo_bytes_per_iter_total": bytes_total,
             "halo_GBps_total": bytes_total / (ms * 1e-3) / 1e9,
             "schedule_ops": len(best),

@@ -521,7 +521,7 @@ PYBIND11_MODULE(_tz, m) {
   // ------------------------------------------------------------------ HIP runtime
   py::enum_<ExecMode>(m, "ExecMode").value("Eager", ExecMode::Eager).value("Graph", ExecMode::Graph);
   py::class_<HipRuntime, ExecutorRunner>(m, "HipRuntime", py::multiple_inheritance())
-      .def(py::init([](int device, int n, std::vector<int> prio, bool cu, ExecMode mode, double wd) {
+      .def(py::init([](int device, int n, std::vector<int> prio, bool cu, ExecMode mode, double wd, int unroll) {
         HipRuntimeOpts o;
         o.device = device;
         o.n_streams = n;
@@ -529,9 +529,13 @@ PYBIND11_MODULE(_tz, m) {
         o.cu_partition = cu;
         o.mode = mode;
         o.watchdog_s = wd;
+        o.graph_unroll = unroll;
         return new HipRuntime(o);
       }), py::arg("device") = -1, py::arg("n_streams") = 2, py::arg("priorities") = std::vector<int>{},
-         py::arg("cu_partition") = false, py::arg("mode") = ExecMode::Eager, py::arg("watchdog_s") = 0.0)
+         py::arg("cu_partition") = false, py::arg("mode") = ExecMode::Eager, py::arg("watchdog_s") = 0.0,
+         py::arg("graph_unroll") = 1)
+      .def("set_graph_unroll", &HipRuntime::set_graph_unroll)
+      .def_property_readonly("graph_unroll", &HipRuntime::graph_unroll)
       .def("set_mode", &HipRuntime::set_mode)
       .def_property_readonly("mode", &HipRuntime::mode)
       .def_property_readonly("effective_mode", &HipRuntime::effective_mode)

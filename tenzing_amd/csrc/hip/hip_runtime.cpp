@@ -30,7 +30,8 @@ int hip_device_count() {
 static hipStream_t S(void *p) { return static_cast<hipStream_t>(p); }
 static hipEvent_t E(void *p) { return static_cast<hipEvent_t>(p); }
 
-HipRuntime::HipRuntime(const HipRuntimeOpts &opts) : mode_(opts.mode), watchdogS_(opts.watchdog_s) {
+HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
+    : mode_(opts.mode), unroll_(std::max(1, opts.graph_unroll)), watchdogS_(opts.watchdog_s) {
   TZ_CHECK(opts.n_streams >= 1, "need at least one stream");
   if (opts.device >= 0) TZ_HIP(hipSetDevice(opts.device));
   TZ_HIP(hipGetDevice(&device_));
@@ -140,6 +141,10 @@ void HipRuntime::destroy_graph() {
     graphExec_ = nullptr;
     graphNodes_ = graphEdges_ = 0;
   }
+  if (graphExecU_) {
+    hipGraphExecDestroy(static_cast<hipGraphExec_t>(graphExecU_));
+    graphExecU_ = nullptr;
+  }
 }
 
 bool HipRuntime::recordable(const Sequence &seq) const {
@@ -162,7 +167,7 @@ void HipRuntime::set_mode(ExecMode m) {
   }
 }
 
-void HipRuntime::build_graph() {
+void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut) {
   const int nS = num_streams();
   hipGraph_t graph = nullptr;
   TZ_HIP(hipGraphCreate(&graph, 0));
@@ -170,6 +175,9 @@ void HipRuntime::build_graph() {
   std::vector<std::vector<hipGraphNode_t>> nodes(nS); // per stream, in issue order
   size_t edges = 0;
   try {
+    // replaying the sequence `iterations` times through one model orders iteration i+1 after
+    // iteration i exactly as the schedule's closing host syncs do in eager mode
+    for (int it = 0; it < iterations; ++it)
     for (const auto &e : seq_.entries) {
       const BoundOp &op = *e.op;
       if (op.op_class() == OpClass::BoundGpu) {
@@ -227,17 +235,26 @@ void HipRuntime::build_graph() {
     TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
     TZ_HIP(hipGraphDestroy(graph));
     graph = nullptr;
-    graphExec_ = exec;
-    graphNodes_ = n;
-    graphEdges_ = edges;
-    TZ_LOG(Debug, "graph mode: " << n << " nodes, " << edges << " edges");
+    nodesOut = n;
+    edgesOut = edges;
+    TZ_LOG(Debug, "graph mode: " << iterations << " iteration(s), " << n << " nodes, " << edges
+                                 << " edges");
+    // upload once so the first timed launch does not pay for it
+    TZ_HIP(hipGraphUpload(exec, S(streams_[0])));
+    TZ_HIP(hipStreamSynchronize(S(streams_[0])));
+    return exec;
   } catch (...) {
     if (graph) hipGraphDestroy(graph);
     throw;
   }
-  // upload once so the first timed launch does not pay for it
-  TZ_HIP(hipGraphUpload(static_cast<hipGraphExec_t>(graphExec_), S(streams_[0])));
-  TZ_HIP(hipStreamSynchronize(S(streams_[0])));
+}
+
+void HipRuntime::set_graph_unroll(int u) {
+  u = std::max(1, u);
+  if (u != unroll_) {
+    destroy_graph();
+    unroll_ = u;
+  }
 }
 
 void HipRuntime::prepare(const Sequence &seq) {
@@ -245,15 +262,22 @@ void HipRuntime::prepare(const Sequence &seq) {
   seq_ = seq;
   internalUsed_ = 0;
   event(std::max(0, seq.num_events() - 1)); // provision the event pool
-  if (mode_ == ExecMode::Graph && recordable(seq)) build_graph();
+  if (mode_ == ExecMode::Graph && recordable(seq)) {
+    size_t n = 0, e = 0;
+    graphExec_ = build_graph(1, graphNodes_, graphEdges_);
+    if (unroll_ > 1) graphExecU_ = build_graph(unroll_, n, e);
+  }
 }
 
 void HipRuntime::run(int64_t n) {
   if (watchdogS_ > 0) deadline_ = wtime() + watchdogS_ * double(std::max<int64_t>(1, n));
   if (graphExec_) {
     hipStream_t origin = S(streams_[0]);
-    for (int64_t i = 0; i < n; ++i)
-      TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExec_), origin));
+    int64_t i = 0;
+    if (graphExecU_)
+      for (; i + unroll_ <= n; i += unroll_)
+        TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExecU_), origin));
+    for (; i < n; ++i) TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExec_), origin));
     TZ_HIP(hipStreamSynchronize(origin));
   } else {
     for (int64_t i = 0; i < n; ++i) {

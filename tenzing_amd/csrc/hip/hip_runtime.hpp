@@ -38,6 +38,7 @@ struct HipRuntimeOpts {
   bool cu_partition = false;   // give each stream a disjoint, XCD-balanced CU mask
   ExecMode mode = ExecMode::Eager;
   double watchdog_s = 0;       // 0 = off
+  int graph_unroll = 1;        // iterations per hipGraph launch in Graph mode
 };
 
 // ExecutorRunner first: the Python bindings expose HipRuntime through that base
@@ -75,13 +76,17 @@ public:
   /// number of dependency edges of the compiled graph
   size_t graph_edges() const { return graphEdges_; }
   void set_watchdog(double s) { watchdogS_ = s; }
+  /// compile `u` consecutive iterations into one graph (amortizes the per-launch cost; the
+  /// iterations stay ordered exactly as the schedule's final host syncs order them)
+  void set_graph_unroll(int u);
+  int graph_unroll() const { return unroll_; }
 
 private:
   void *event(int e);
   void *internal_event();
   void destroy_graph();
   bool recordable(const Sequence &seq) const;
-  void build_graph();
+  void *build_graph(int iterations, size_t &nodes, size_t &edges);
 
   int device_ = 0;
   ExecMode mode_;
@@ -90,7 +95,9 @@ private:
   std::vector<void *> internal_; // StreamWait helpers
   size_t internalUsed_ = 0;
   Sequence seq_;
-  void *graphExec_ = nullptr;
+  void *graphExec_ = nullptr;  // one iteration
+  void *graphExecU_ = nullptr; // unroll_ iterations
+  int unroll_ = 1;
   size_t graphNodes_ = 0, graphEdges_ = 0;
 
   double watchdogS_ = 0;

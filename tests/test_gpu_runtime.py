@@ -87,6 +87,37 @@ def test_halo_qxyz_order(tz, gpu):
     assert halo.check_grid() == 0
 
 
+@pytest.mark.parametrize("unroll", [1, 3])
+def test_graph_mode_iteration_count(tz, gpu, unroll):
+    """every iteration of a compiled (and unrolled) graph executes every op exactly once"""
+    torch = pytest.importorskip("torch")
+    n = 4096
+    ones = torch.ones(n, dtype=torch.float64, device="cuda")
+    y = torch.zeros(n, dtype=torch.float64, device="cuda")
+    K = tz._tz.kernels
+
+    def add(stream):
+        K.axpy_f64(n, 1.0, ones.data_ptr(), y.data_ptr(), stream)
+
+    g = tz.Graph()
+    a, b, c = tz.PyGpuOp("a", add), tz.PyGpuOp("b", add), tz.PyGpuOp("c", add)
+    g.start_then(a)
+    g.then(a, b)
+    g.then(a, c)
+    g.then_finish(b)
+    g.then_finish(c)
+    rt = tz.HipRuntime(device=0, n_streams=2, mode=tz.ExecMode.Graph, graph_unroll=unroll)
+    for seed in range(3):
+        y.zero_()
+        torch.cuda.synchronize()
+        seq = tz.random_rollout(tz.State(g, tz.Platform(2)), seed)
+        rt.prepare(seq)
+        assert rt.effective_mode == tz.ExecMode.Graph
+        rt.run(7)
+        rt.device_sync()
+        assert float(y[0]) == 21.0 and float(y[-1]) == 21.0
+
+
 def test_halo_rccl_self_exchange(tz, gpu):
     """RCCL transport on a 1-rank communicator (self send/recv in a group)."""
     halo, g = _small_halo(tz, neighbors=6, transport="rccl")
