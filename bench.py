@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--order", default="qxyz", choices=["xyzq", "qxyz"],
                     help="grid storage order (reference halo driver: xyzq)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "direct", "copy", "rccl"],
+                    help="auto: direct (pack-free) moves on 1 rank, RCCL between ranks")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=40)
@@ -63,7 +65,8 @@ def main() -> int:
         print(f"bench.py: warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
     t_setup = time.time()
-    cfg = HaloConfig(n=args.n, neighbors=args.neighbors, fuse=args.fuse, order=args.order)
+    cfg = HaloConfig(n=args.n, neighbors=args.neighbors, fuse=args.fuse, order=args.order,
+                     transport=args.transport)
     halo, graph = build_halo(cfg, ctrl, device)
     mode = tz.ExecMode.Graph if args.search_mode == "graph" else tz.ExecMode.Eager
     rt = tz.HipRuntime(device=device, n_streams=args.streams, mode=mode, watchdog_s=120.0)
@@ -180,7 +183,7 @@ def main() -> int:
             "schedule_sync_ops": best.count_sync_ops(),
             "verified_bad_cells": int(bad),
             "setup_s": setup_s,
-            "transport": "rccl" if halo.uses_rccl() else "copy",
+            "transport": halo.transport(),
         }
         print(json.dumps(out), flush=True)
     return 0 if bad == 0 else 3

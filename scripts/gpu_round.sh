@@ -29,5 +29,8 @@ if [[ " $STEPS " == *" prof "* ]]; then
     > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
   if fatal $rc; then exit $rc; fi
+  # the full trace is far too large to travel back: keep a summary of the timed loop
+  python3 scripts/trace_summary.py gpurun_out/prof/run_kernel_trace.csv --last "${PROF_LAST:-300}" \
+    --timeline "${PROF_TIMELINE:-80}" --out gpurun_out/prof/timeline.txt --delete > /dev/null
 fi
 exit 0

@@ -607,7 +607,13 @@ PYBIND11_MODULE(_tz, m) {
       .def("pack_all", [](const HaloExchange &h, uintptr_t s) { h.pack_all(P(s)); })
       .def("unpack_all", [](const HaloExchange &h, uintptr_t s) { h.unpack_all(P(s)); })
       .def("shift_all", [](const HaloExchange &h, uintptr_t s) { h.shift_all(P(s)); })
-      .def("uses_rccl", &HaloExchange::uses_rccl);
+      .def("direct", [](const HaloExchange &h, int i, uintptr_t s) { h.direct(i, P(s)); })
+      .def("direct_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.direct_group(d, P(s)); })
+      .def("uses_rccl", &HaloExchange::uses_rccl)
+      .def("uses_direct", &HaloExchange::uses_direct)
+      .def("is_direct", &HaloExchange::is_direct)
+      .def("pipelined_dirs", &HaloExchange::pipelined_dirs)
+      .def("transport", &HaloExchange::transport);
 
   py::class_<SpmvArgs>(m, "SpmvArgs")
       .def(py::init<>())
@@ -675,16 +681,36 @@ PYBIND11_MODULE(_tz, m) {
     kern::iota_f64(n, base, scale, reinterpret_cast<double *>(a), P(s));
   }, py::arg("n"), py::arg("base"), py::arg("scale"), py::arg("a"), py::arg("stream") = 0);
   k.def("empty", [](uintptr_t s) { kern::empty(P(s)); }, py::arg("stream") = 0);
-  k.def("set_box_tuning", [](int unroll, bool ntPack, bool ntUnpack, int maxBlocks) {
+  k.def("box_move_many", [](std::vector<py::dict> ds, uintptr_t s) {
+    std::vector<kern::MoveDesc> ms;
+    for (auto &d : ds) {
+      kern::MoveDesc m;
+      m.src = reinterpret_cast<const double *>(d["src"].cast<uintptr_t>());
+      m.dst = reinterpret_cast<double *>(d["dst"].cast<uintptr_t>());
+      m.src_off = d["src_off"].cast<int64_t>();
+      m.dst_off = d["dst_off"].cast<int64_t>();
+      m.s1 = d.contains("s1") ? d["s1"].cast<int64_t>() : 0;
+      m.s2 = d.contains("s2") ? d["s2"].cast<int64_t>() : 0;
+      m.s3 = d.contains("s3") ? d["s3"].cast<int64_t>() : 0;
+      m.len = d["len"].cast<int32_t>();
+      m.n1 = d.contains("n1") ? d["n1"].cast<int32_t>() : 1;
+      m.n2 = d.contains("n2") ? d["n2"].cast<int32_t>() : 1;
+      m.n3 = d.contains("n3") ? d["n3"].cast<int32_t>() : 1;
+      ms.push_back(m);
+    }
+    kern::box_move_many(ms.data(), int(ms.size()), P(s));
+  }, py::arg("moves"), py::arg("stream") = 0);
+  k.def("set_box_tuning", [](int unroll, bool ntPack, bool ntUnpack, int maxBlocks, bool ntMove) {
     kern::box_tuning().unroll = unroll;
     kern::box_tuning().nt_pack = ntPack;
     kern::box_tuning().nt_unpack = ntUnpack;
     kern::box_tuning().max_blocks = maxBlocks;
+    kern::box_tuning().nt_move = ntMove;
   }, py::arg("unroll") = 4, py::arg("nt_pack") = true, py::arg("nt_unpack") = false,
-     py::arg("max_blocks") = 4096);
+     py::arg("max_blocks") = 4096, py::arg("nt_move") = true);
   k.def("get_box_tuning", []() {
     const auto &t = kern::box_tuning();
-    return py::make_tuple(t.unroll, t.nt_pack, t.nt_unpack, t.max_blocks);
+    return py::make_tuple(t.unroll, t.nt_pack, t.nt_unpack, t.max_blocks, t.nt_move);
   });
   k.def("copy_bytes", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
     kern::copy_bytes(P(dst), P(src), n, P(s));

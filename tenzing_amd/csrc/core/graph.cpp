@@ -48,7 +48,14 @@ void Graph::add_edge(int a, int b) {
   nodes_[b].preds.push_back(a);
 }
 
-void Graph::then(const OpPtr &a, const OpPtr &b) { add_edge(add(a), add(b)); }
+void Graph::then(const OpPtr &a, const OpPtr &b) {
+  // copies first: `a` / `b` may alias nodes_ storage (start_op()/finish_op()) that add() can
+  // reallocate
+  const OpPtr pa = a, pb = b;
+  const int ia = add(pa);
+  const int ib = add(pb);
+  add_edge(ia, ib);
+}
 
 void Graph::normalize() {
   for (int id = 2; id < capacity(); ++id) {

@@ -29,8 +29,24 @@ struct BoxTuning {
   bool nt_pack = true;    // non-temporal grid loads in pack: -27 % pack time in pipeline context
   bool nt_unpack = false; // non-temporal grid stores in unpack: +5 % (off)
   int max_blocks = 4096;  // cap per box (grid-stride beyond)
+  bool nt_move = true;    // non-temporal source loads in box_move (direct transfers)
 };
 BoxTuning &box_tuning();
+
+/// A box-to-box move between two arrays of the SAME pitched layout: element (x,i1,i2,i3) of
+/// the box at `src + src_off` goes to the same element of the box at `dst + dst_off`
+/// (strides s1..s3, rows of `len`). This is the pack-free "direct" halo transfer: interior
+/// slab -> ghost region of the neighbour's grid (own grid for self-neighbours, an IPC-mapped
+/// peer grid over xGMI otherwise).
+struct MoveDesc {
+  const double *src = nullptr;
+  double *dst = nullptr;
+  int64_t src_off = 0, dst_off = 0;
+  int64_t s1 = 0, s2 = 0, s3 = 0;
+  int32_t len = 0, n1 = 0, n2 = 0, n3 = 0;
+};
+/// up to kMaxBoxes moves in ONE launch
+void box_move_many(const MoveDesc *d, int n, void *stream);
 
 /// pack (grid -> buf) or unpack (buf -> grid) one box
 void box_copy(double *grid, const BoxDesc &d, bool unpack, void *stream);

@@ -232,6 +232,7 @@ void copy_many(const CopyDesc *d, int n, void *stream) {
   uint32_t total = 0;
   for (int i = 0; i < n; ++i) {
     if (d[i].bytes == 0) continue;
+    if (!d[i].dst || !d[i].src) throw std::runtime_error("copy_many: null pointer");
     if ((reinterpret_cast<uintptr_t>(d[i].dst) | reinterpret_cast<uintptr_t>(d[i].src)) % 16 ||
         d[i].bytes % 8)
       throw std::runtime_error("copy_many: 16-byte aligned pointers and 8-byte sizes required");

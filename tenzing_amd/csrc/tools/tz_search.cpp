@@ -50,7 +50,7 @@ void usage() {
          "  [--strategy NAME] [--iters N] [--time-budget S] [--streams N] [--bench-iters N]\n"
          "  [--target-secs S] [--mode eager|graph] [--sim] [--seed N] [--no-expand-rollout]\n"
          "  [--halo-n N] [--nq N] [--ghost N] [--neighbors 6|26] [--fuse none|pack|all]\n"
-         "  [--transport auto|rccl|copy] [--spmv-m N] [--max-seqs N] [--rdzv-file PATH]\n"
+         "  [--transport auto|rccl|copy|direct] [--spmv-m N] [--max-seqs N] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--watchdog S]\n";
 }

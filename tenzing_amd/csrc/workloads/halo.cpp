@@ -85,17 +85,34 @@ private:
   int i_;
 };
 
+/// direct transport of one direction: interior slab -> neighbour's ghost (no buffers)
+class HaloDirect : public GpuOp {
+public:
+  HaloDirect(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_direct_" + h_->dir(i_).name(); }
+  std::string kind() const override { return "HaloDirect"; }
+  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
+  double cost_us() const override { return copy_cost_us(bytes()); }
+  void launch(void *s, Executor &) const override { h_->direct(i_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
 /// one op for a whole group of directions (single kernel launch / single RCCL group)
 class HaloStageGroup : public GpuOp {
 public:
-  enum Stage { Pack, Shift, Unpack };
+  enum Stage { Pack, Shift, Unpack, Direct };
   HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag)
       : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
   std::string name() const override {
-    return std::string(st_ == Pack ? "he_pack_" : (st_ == Shift ? "he_shift_" : "he_unpack_")) + tag_;
+    static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_"};
+    return pre[st_] + tag_;
   }
   std::string kind() const override {
-    return st_ == Pack ? "HaloPackGroup" : (st_ == Shift ? "HaloShiftGroup" : "HaloUnpackGroup");
+    static const char *k[] = {"HaloPackGroup", "HaloShiftGroup", "HaloUnpackGroup", "HaloDirectGroup"};
+    return k[st_];
   }
   double bytes() const override {
     double b = 0;
@@ -109,7 +126,8 @@ public:
   void launch(void *s, Executor &) const override {
     if (st_ == Pack) h_->pack_group(dirs_, s);
     else if (st_ == Shift) h_->shift_group(dirs_, s);
-    else h_->unpack_group(dirs_, s);
+    else if (st_ == Unpack) h_->unpack_group(dirs_, s);
+    else h_->direct_group(dirs_, s);
   }
 
 private:
@@ -199,14 +217,19 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
     sq_ = 1;
     gridElems_ = size_t(sz_ * Z);
   }
-  std::string t = a_.transport;
-  if (t == "auto") t = a_.size == 1 ? "copy" : "rccl";
-  if (t == "copy") {
-    for (int n : nbr_) TZ_CHECK(n == a_.rank, "copy transport needs self-neighbours (1 rank)");
-  } else {
-    TZ_CHECK(t == "rccl", "unknown transport " << a_.transport);
+  const std::string &t = a_.transport;
+  TZ_CHECK(t == "auto" || t == "direct" || t == "copy" || t == "rccl",
+           "unknown transport " << t);
+  if (t == "copy" || t == "direct") {
+    for (int n : nbr_) TZ_CHECK(n == a_.rank, t << " transport needs self-neighbours (1 rank)");
   }
-  useRccl_ = t == "rccl";
+  // per direction: direct move (self-neighbour under auto/direct) or pack -> transfer -> unpack
+  for (int i = 0; i < ndirs(); ++i)
+    direct_.push_back((t == "direct" || t == "auto") && nbr_[i] == a_.rank);
+  for (int i = 0; i < ndirs(); ++i) {
+    if (direct_[i]) useDirect_ = true;
+    else if (t != "copy") useRccl_ = true;
+  }
 }
 
 HaloExchange::~HaloExchange() = default;
@@ -307,9 +330,14 @@ void HaloExchange::setup(Ctrl *ctrl) {
   if (ready()) return;
   if (a_.device >= 0) TZ_HIP(hipSetDevice(a_.device));
   grid_ = DeviceBuffer(gridElems_ * sizeof(double));
+  // staging buffers only for pipelined directions (locality is symmetric: direct_[i] ==
+  // direct_[opp(i)], so a pipelined shift(i) never touches a direct direction's buffers)
+  send_.resize(ndirs());
+  recv_.resize(ndirs());
   for (int i = 0; i < ndirs(); ++i) {
-    send_.emplace_back(box_elems(i) * sizeof(double));
-    recv_.emplace_back(box_elems(opp_[i]) * sizeof(double));
+    if (direct_[i]) continue;
+    send_[i] = DeviceBuffer(box_elems(i) * sizeof(double));
+    recv_[i] = DeviceBuffer(box_elems(opp_[i]) * sizeof(double));
   }
   count_ = DeviceBuffer(sizeof(unsigned long long));
   if (useRccl_) {
@@ -340,15 +368,25 @@ uint64_t HaloExchange::check_grid(void *stream) {
   return n;
 }
 
+void HaloExchange::check_pipelined(int i) const {
+  TZ_CHECK(i >= 0 && i < ndirs(), "direction " << i << " out of range");
+  TZ_CHECK(!direct_[i], "direction " << dirs_[i].name()
+                                     << " uses the direct transport (no pack/transfer/unpack)");
+  TZ_CHECK(ready(), "halo not set up");
+}
+
 void HaloExchange::pack(int i, void *stream) const {
+  check_pipelined(i);
   kern::box_copy(grid(), pack_box(i), false, stream);
 }
 
 void HaloExchange::unpack(int i, void *stream) const {
+  check_pipelined(i);
   kern::box_copy(grid(), unpack_box(i), true, stream);
 }
 
 void HaloExchange::shift(int i, void *stream) const {
+  check_pipelined(i);
   // send my slab facing d to nbr(d); receive nbr(-d)'s slab facing d into my ghost on side -d
   const int o = opp_[i];
   const size_t n = box_elems(i);
@@ -380,7 +418,10 @@ std::vector<int> HaloExchange::group_dirs(int k) const {
 
 void HaloExchange::pack_group(const std::vector<int> &dirs, void *stream) const {
   std::vector<kern::BoxDesc> bs;
-  for (int i : dirs) bs.push_back(pack_box(i));
+  for (int i : dirs) {
+    check_pipelined(i);
+    bs.push_back(pack_box(i));
+  }
   for (size_t k = 0; k < bs.size(); k += kern::kMaxBoxes)
     kern::box_copy_many(grid(), bs.data() + k, int(std::min<size_t>(kern::kMaxBoxes, bs.size() - k)),
                         false, stream);
@@ -389,7 +430,10 @@ void HaloExchange::pack_group(const std::vector<int> &dirs, void *stream) const 
 void HaloExchange::unpack_group(const std::vector<int> &dirs, void *stream) const {
   // the ghosts filled by the shifts of `dirs` are those on the opposite sides
   std::vector<kern::BoxDesc> bs;
-  for (int i : dirs) bs.push_back(unpack_box(opp_[i]));
+  for (int i : dirs) {
+    check_pipelined(i);
+    bs.push_back(unpack_box(opp_[i]));
+  }
   for (size_t k = 0; k < bs.size(); k += kern::kMaxBoxes)
     kern::box_copy_many(grid(), bs.data() + k, int(std::min<size_t>(kern::kMaxBoxes, bs.size() - k)),
                         true, stream);
@@ -397,6 +441,7 @@ void HaloExchange::unpack_group(const std::vector<int> &dirs, void *stream) cons
 
 void HaloExchange::shift_group(const std::vector<int> &dirs, void *stream) const {
   if (dirs.empty()) return;
+  for (int i : dirs) check_pipelined(i);
   if (useRccl_) {
     std::vector<RcclComm::Xfer> xs;
     for (int i : dirs) {
@@ -415,13 +460,52 @@ void HaloExchange::shift_group(const std::vector<int> &dirs, void *stream) const
   }
 }
 
-void HaloExchange::pack_all(void *stream) const { pack_group(all_dirs(), stream); }
-void HaloExchange::unpack_all(void *stream) const { unpack_group(all_dirs(), stream); }
-void HaloExchange::shift_all(void *stream) const { shift_group(all_dirs(), stream); }
+void HaloExchange::direct_group(const std::vector<int> &dirs, void *stream) const {
+  std::vector<kern::MoveDesc> ms;
+  for (int i : dirs) {
+    TZ_CHECK(i >= 0 && i < ndirs() && direct_[i], "direction " << i << " is not a direct (self) transfer");
+    TZ_CHECK(ready(), "halo not set up");
+    // my slab facing d lands in nbr(d)'s ghost on side -d (self-neighbours: my own grid)
+    const kern::BoxDesc s = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
+    const kern::BoxDesc d = make_box(a_, dirs_[opp_[i]], true, xoff_, sy_, sz_, sq_);
+    kern::MoveDesc m;
+    m.src = grid();
+    m.dst = grid();
+    m.src_off = s.grid_off;
+    m.dst_off = d.grid_off;
+    m.s1 = s.s1;
+    m.s2 = s.s2;
+    m.s3 = s.s3;
+    m.len = s.len;
+    m.n1 = s.n1;
+    m.n2 = s.n2;
+    m.n3 = s.n3;
+    ms.push_back(m);
+  }
+  for (size_t k = 0; k < ms.size(); k += kern::kMaxBoxes)
+    kern::box_move_many(ms.data() + k, int(std::min<size_t>(kern::kMaxBoxes, ms.size() - k)), stream);
+}
+
+std::vector<int> HaloExchange::pipelined_dirs() const {
+  std::vector<int> v;
+  for (int i = 0; i < ndirs(); ++i)
+    if (!direct_[i]) v.push_back(i);
+  return v;
+}
+
+void HaloExchange::pack_all(void *stream) const { pack_group(pipelined_dirs(), stream); }
+void HaloExchange::unpack_all(void *stream) const { unpack_group(pipelined_dirs(), stream); }
+void HaloExchange::shift_all(void *stream) const { shift_group(pipelined_dirs(), stream); }
 
 void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   for (int i : dirs) {
+    if (direct_[i]) {
+      auto d = std::make_shared<HaloDirect>(self, i);
+      g.start_then(d);
+      g.then_finish(d);
+      continue;
+    }
     auto p = std::make_shared<HaloPack>(self, i);
     auto s = std::make_shared<HaloShift>(self, i);
     auto u = std::make_shared<HaloUnpack>(self, opp_[i]);
@@ -434,29 +518,48 @@ void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs) {
 
 void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
-  auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, tag);
-  auto s = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Shift, dirs, tag);
-  auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, dirs, tag);
+  std::vector<int> local, remote;
+  for (int i : dirs) (direct_[i] ? local : remote).push_back(i);
+  if (!local.empty()) {
+    auto d = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Direct, local,
+                                              remote.empty() ? tag : tag + "_self");
+    g.start_then(d);
+    g.then_finish(d);
+  }
+  if (remote.empty()) return;
+  auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, remote, tag);
+  auto s = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Shift, remote, tag);
+  auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, remote, tag);
   g.start_then(p);
   g.then(p, s);
   g.then(s, u);
   g.then_finish(u);
 }
 
-void HaloExchange::add_to_graph(Graph &g) {
+void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   const std::string &f = a_.fuse;
+  const bool direct = direct_[dirs.front()];
+  auto subset = [&](const std::vector<int> &v) {
+    std::vector<int> r;
+    for (int i : v)
+      if (std::find(dirs.begin(), dirs.end(), i) != dirs.end()) r.push_back(i);
+    return r;
+  };
   if (f == "none") {
-    add_chains(g, all_dirs());
-  } else if (f == "all") {
-    add_fused(g, all_dirs(), "all");
+    add_chains(g, dirs);
+  } else if (f == "all" || (f == "pack" && direct)) {
+    // (direct transfers have no pack stage: "pack" degenerates to one fused move)
+    add_fused(g, dirs, "all");
   } else if (f == "pack") {
     // fused pack / unpack kernels, per-direction transfers
-    auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, all_dirs(), "all");
-    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, all_dirs(), "all");
+    std::vector<int> unp;
+    for (int i : dirs) unp.push_back(opp_[i]);
+    auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, "all");
+    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, dirs, "all");
     g.start_then(p);
     g.then_finish(u);
-    for (int i = 0; i < ndirs(); ++i) {
+    for (int i : dirs) {
       auto s = std::make_shared<HaloShift>(self, i);
       g.then(p, s);
       g.then(s, u);
@@ -466,8 +569,10 @@ void HaloExchange::add_to_graph(Graph &g) {
     // either one chain per direction or one fused chain. With "choice" the search decides
     // (ChoiceOp of two CompoundOps; the group touches no other op, so choosing at the group
     // boundary loses no dependency precision).
-    std::vector<std::pair<std::string, std::vector<int>>> groups = {{"faces", group_dirs(1)}};
-    if (a_.neighbors == 26) groups.push_back({"small", group_dirs(0)});
+    std::vector<std::pair<std::string, std::vector<int>>> groups;
+    for (auto &gr : std::vector<std::pair<std::string, std::vector<int>>>{
+             {"faces", subset(group_dirs(1))}, {"small", subset(group_dirs(0))}})
+      if (!gr.second.empty()) groups.push_back(gr);
     if (f == "groups") {
       for (auto &gr : groups) add_fused(g, gr.second, gr.first);
       return;
@@ -487,14 +592,15 @@ void HaloExchange::add_to_graph(Graph &g) {
       grouped->then_finish(choice);
     }
     if (groups.size() == 1) {
-      g.start_then(std::make_shared<StaticCompoundOp>("he_grouped", grouped));
-      g.then_finish(g.op(g.find("he_grouped")));
+      auto c = std::make_shared<StaticCompoundOp>("he_grouped", grouped);
+      g.start_then(c);
+      g.then_finish(c);
       return;
     }
-    // 26 neighbours: additionally one chain for every direction (a single launch per stage
+    // two groups: additionally one chain for every direction (a single launch per stage
     // avoids the two groups' kernels competing for CUs)
     auto all = std::make_shared<Graph>();
-    add_fused(*all, all_dirs(), "all");
+    add_fused(*all, dirs, "all");
     std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>("he_grouped", grouped),
                               std::make_shared<StaticCompoundOp>("he_allfused", all)};
     auto choice = std::make_shared<StaticChoiceOp>("he_exchange", top);
@@ -503,6 +609,21 @@ void HaloExchange::add_to_graph(Graph &g) {
   } else {
     TZ_THROW("fuse must be none, pack, all, groups or choice (got " << f << ")");
   }
+}
+
+void HaloExchange::add_to_graph(Graph &g) {
+  // self-neighbour directions moved directly and remote directions through RCCL are
+  // independent: the local moves form their own op(s), the remote chains get the fuse
+  // structure (and the search overlaps the two)
+  std::vector<int> local, remote;
+  for (int i = 0; i < ndirs(); ++i) (direct_[i] ? local : remote).push_back(i);
+  if (local.empty() || remote.empty()) {
+    add_structure(g, all_dirs());
+    return;
+  }
+  if (a_.fuse == "none") add_chains(g, local);
+  else add_fused(g, local, "self");
+  add_structure(g, remote);
 }
 
 } // namespace tz

@@ -97,7 +97,10 @@ struct HaloArgs {
   int nx = 512, ny = 512, nz = 512, nq = 3, ghost = 3;
   int neighbors = 6;              // 6 (faces) or 26 (faces, edges, corners)
   std::string order = "xyzq";     // "xyzq" (x fastest, q slowest) or "qxyz"
-  std::string transport = "auto"; // "rccl", "copy" (self-neighbour only), "auto"
+  // "rccl" (pack -> grouped RCCL send/recv -> unpack), "copy" (pack -> device copy -> unpack,
+  // self-neighbours only), "direct" (pack-free box moves straight into the neighbour's ghost
+  // region; self-neighbours only), "auto" (direct on one rank, rccl otherwise)
+  std::string transport = "auto";
   // "choice": per group (faces / edges+corners) the search chooses per-direction or fused ops;
   // "none": per-direction ops; "groups": fused per group; "pack": fused pack+unpack with
   // per-direction transfers; "all": one op per stage
@@ -158,20 +161,37 @@ public:
   void unpack_group(const std::vector<int> &dirs, void *stream) const;
   void shift_group(const std::vector<int> &dirs, void *stream) const;
   std::vector<int> all_dirs() const;
+  /// directions that go through pack -> transfer -> unpack (not direct)
+  std::vector<int> pipelined_dirs() const;
   /// k = 1 faces, 2 edges, 3 corners, 0 edges + corners
   std::vector<int> group_dirs(int k) const;
   bool uses_rccl() const { return useRccl_; }
+  bool uses_direct() const { return useDirect_; }
+  /// direction i is moved directly (self-neighbour) rather than packed and transferred
+  bool is_direct(int i) const { return direct_[i]; }
+  /// "rccl", "copy", "direct" or "direct+rccl" (self-neighbour directions direct, the rest RCCL)
+  std::string transport() const {
+    if (useDirect_) return useRccl_ ? "direct+rccl" : "direct";
+    return useRccl_ ? "rccl" : "copy";
+  }
+  /// direct transport: move the interior slab facing each direction of `dirs` straight into
+  /// the neighbour's ghost region on the opposite side (one launch)
+  void direct_group(const std::vector<int> &dirs, void *stream) const;
+  void direct(int i, void *stream) const { direct_group({i}, stream); }
 
 private:
   void add_chains(Graph &g, const std::vector<int> &dirs);
   void add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag);
+  void add_structure(Graph &g, const std::vector<int> &dirs); // fuse mode over `dirs`
+  void check_pipelined(int i) const;
   HaloArgs a_;
   std::vector<Dir> dirs_;
   std::vector<int> opp_, nbr_;
   int cx_ = 0, cy_ = 0, cz_ = 0;
   int64_t xoff_ = 0, pitch_ = 0, sy_ = 0, sz_ = 0, sq_ = 0;
   size_t gridElems_ = 0;
-  bool useRccl_ = false;
+  bool useRccl_ = false, useDirect_ = false;
+  std::vector<bool> direct_; // per direction
   DeviceBuffer grid_;
   std::vector<DeviceBuffer> send_, recv_;
   std::vector<std::shared_ptr<RcclComm>> comms_;

@@ -4,8 +4,11 @@ Reference driver config (tenzing-mcts/examples/halo_run_strategy.hpp:42-49): nQ=
 nX=nY=nZ=512, nGhost=3, XYZQ storage, 6 face neighbours, 2 streams. BASELINE.json's headline
 adds the 27-point stencil (26 neighbours) and 4 streams per rank on 8 GPUs.
 
-Graph per direction d: ``he_pack_<d> -> he_shift_<d> -> he_unpack_<-d>`` (see
-csrc/workloads/workloads.hpp for the RCCL design).
+Graph per direction d: ``he_pack_<d> -> he_shift_<d> -> he_unpack_<-d>`` (rccl / copy
+transports; see csrc/workloads/workloads.hpp for the RCCL design) or one pack-free
+``he_direct_<d>`` box move straight into the neighbour's ghost region (direct transport, the
+default on one rank). ``fuse`` groups directions into single launches / RCCL groups; "choice"
+leaves the grouping to the search (ChoiceOps).
 """
 from __future__ import annotations
 
@@ -21,8 +24,8 @@ class HaloConfig:
     ghost: int = 3        # ghost width
     neighbors: int = 26   # 6 = faces, 26 = faces + edges + corners (27-point stencil)
     order: str = "xyzq"   # storage order
-    transport: str = "auto"  # rccl | copy | auto
-    fuse: str = "none"    # none | pack | all
+    transport: str = "auto"  # rccl | copy | direct | auto (direct on 1 rank, else rccl)
+    fuse: str = "none"    # none | pack | all | groups | choice
     comms: int = 0        # RCCL communicators (0 = one per direction)
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":

@@ -191,3 +191,17 @@ def test_prime_factors_and_runs_test(tz):
 def test_bench_result_percentiles(tz):
     r = tz.BenchResult.from_times([float(i) for i in range(100)])
     assert r.pct01 == 1 and r.pct10 == 10 and r.pct50 == 50 and r.pct99 == 99
+
+
+def test_graph_then_survives_node_reallocation(tz):
+    """start_then/then_finish pass references into the node table; adding the other endpoint
+    may grow it (regression: a dangling Start reference became a null op)"""
+    g = tz.Graph()
+    ops = [tz.SimGpuOp(f"op{i}", 1.0) for i in range(300)]
+    for o in ops:
+        g.start_then(o)
+        g.then_finish(o)
+    assert len(g) == 302
+    assert g.num_edges() == 600
+    for o in ops[:5]:
+        assert g.preds(g.find(o.name)) == [0]

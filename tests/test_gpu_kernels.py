@@ -50,6 +50,33 @@ def test_box_copy_pack_unpack_matches_torch(tz, gpu, order, neighbors):
         assert torch.equal(g2, exp), f"unpack mismatch dir {h.dir_name(i)}"
 
 
+@pytest.mark.parametrize("order", ["xyzq", "qxyz"])
+def test_box_move_matches_torch(tz, gpu, order):
+    """direct transfer kernel: interior slab facing d -> ghost on side -d, all 26 at once"""
+    a = tz.HaloArgs()
+    a.nx, a.ny, a.nz, a.nq, a.ghost = 20, 12, 9, 3, 2
+    a.neighbors, a.order = 26, order
+    h = tz.HaloExchange(a)
+    grid = torch.randn(h.grid_elems(), dtype=torch.float64, device="cuda")
+    out = grid.clone()
+    exp = grid.clone()
+    moves = []
+    for i in range(h.ndirs()):
+        s, d = h.pack_box(i), h.unpack_box(h.opposite(i))
+        moves.append(dict(src=out.data_ptr(), dst=out.data_ptr(), src_off=s["grid_off"],
+                          dst_off=d["grid_off"], s1=s["s1"], s2=s["s2"], s3=s["s3"],
+                          len=s["len"], n1=s["n1"], n2=s["n2"], n3=s["n3"]))
+        for i3 in range(s["n3"]):
+            for i2 in range(s["n2"]):
+                so = s["grid_off"] + i2 * s["s2"] + i3 * s["s3"]
+                do = d["grid_off"] + i2 * s["s2"] + i3 * s["s3"]
+                exp.as_strided((s["n1"], s["len"]), (s["s1"], 1), do).copy_(
+                    grid.as_strided((s["n1"], s["len"]), (s["s1"], 1), so))
+    tz._tz.kernels.box_move_many(moves, _stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, exp)
+
+
 def test_box_copy_many_equals_single(tz, gpu):
     a = tz.HaloArgs()
     a.nx = a.ny = a.nz = 16

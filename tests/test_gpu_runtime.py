@@ -40,11 +40,13 @@ def test_gpu_graph_decisions_real_streams(tz, gpu):
     rt.device_sync()
 
 
+@pytest.mark.parametrize("transport", ["copy", "direct"])
 @pytest.mark.parametrize("mode", ["eager", "graph"])
 @pytest.mark.parametrize("fuse", ["none", "pack", "all", "groups", "choice"])
 @pytest.mark.parametrize("neighbors", [6, 26])
-def test_halo_exchange_correct(tz, gpu, mode, fuse, neighbors):
-    halo, g = _small_halo(tz, neighbors=neighbors, fuse=fuse)
+def test_halo_exchange_correct(tz, gpu, mode, fuse, neighbors, transport):
+    halo, g = _small_halo(tz, neighbors=neighbors, fuse=fuse, transport=transport)
+    assert halo.transport() == transport
     m = tz.ExecMode.Graph if mode == "graph" else tz.ExecMode.Eager
     rt = tz.HipRuntime(device=0, n_streams=3, mode=m)
     for seed in range(3):
