@@ -69,7 +69,8 @@ def main() -> int:
                      transport=args.transport)
     halo, graph = build_halo(cfg, ctrl, device)
     mode = tz.ExecMode.Graph if args.search_mode == "graph" else tz.ExecMode.Eager
-    rt = tz.HipRuntime(device=device, n_streams=args.streams, mode=mode, watchdog_s=120.0)
+    rt = tz.HipRuntime(device=device, n_streams=args.streams, mode=mode, watchdog_s=120.0,
+                       graph_unroll=args.graph_unroll if args.search_mode == "graph" else 1)
     bench = tz.EmpiricalBenchmarker(rt, ctrl)
     setup_s = time.time() - t_setup
 

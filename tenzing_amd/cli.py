@@ -25,7 +25,7 @@ def _build_workload(a, ctrl, device, setup):
 
     hc = HaloConfig(n=a.halo_n, nq=a.nq, ghost=a.ghost, neighbors=a.neighbors, order=a.order,
                     fuse=a.fuse, transport=a.transport)
-    sc = SpmvConfig(m=a.spmv_m)
+    sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form)
     if a.workload == "halo":
         h, g = build_halo(hc, ctrl, device, setup)
         return g, {"halo": h}
@@ -35,6 +35,15 @@ def _build_workload(a, ctrl, device, setup):
     if a.workload == "fused":
         h, s, g = build_fused(hc, sc, ctrl, device, setup)
         return g, {"halo": h, "spmv": s}
+    if a.workload == "noop":
+        # reference test/test_noop_graph.cpp: Start -> op1 -> Finish (here: `--noop-width`
+        # independent no-ops, so DFS has orderings and stream choices to enumerate)
+        g = tz.Graph()
+        for i in range(a.noop_width):
+            op = tz.NoOp(f"op{i + 1}")
+            g.start_then(op)
+            g.then_finish(op)
+        return g, {}
     if a.workload == "diamond":
         g = tz.Graph()
         k = [tz.BusyKernelOp(f"k{i}", us) for i, us in enumerate((20, 100, 100, 20), 1)]
@@ -53,7 +62,9 @@ def cmd_search(a) -> int:
     from tenzing_amd.parallel import init_ctrl, select_device
 
     ctrl = init_ctrl()
-    hw = not (a.sim or a.replay)
+    if a.workload == "noop":
+        a.host = True  # no GPU op in the graph: time it on the host executor
+    hw = not (a.sim or a.replay or a.host)
     device = select_device() if hw else -1
     if hw and device < 0:
         raise SystemExit("no GPU visible: use --sim or --replay")
@@ -70,11 +81,15 @@ def cmd_search(a) -> int:
     rt = None
     if a.replay:
         bench = tz.CsvBenchmarker(a.replay, g)
+    elif a.host:
+        rt = tz.HostExecutor(a.streams)
+        bench = tz.EmpiricalBenchmarker(rt, ctrl)
     elif a.sim:
         bench = tz.SimBenchmarker(a.streams)
     else:
         mode = tz.ExecMode.Graph if a.mode == "graph" else tz.ExecMode.Eager
-        rt = tz.HipRuntime(device=device, n_streams=a.streams, mode=mode, watchdog_s=a.watchdog)
+        rt = tz.HipRuntime(device=device, n_streams=a.streams, mode=mode, watchdog_s=a.watchdog,
+                           graph_unroll=a.graph_unroll)
         bench = tz.EmpiricalBenchmarker(rt, ctrl)
     t0 = time.time()
     if a.solver == "dfs":
@@ -135,7 +150,11 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m tenzing_amd", description=__doc__.splitlines()[0])
     sub = ap.add_subparsers(dest="cmd", required=True)
     s = sub.add_parser("search")
-    s.add_argument("--workload", default="halo", choices=["halo", "spmv", "fused", "diamond"])
+    s.add_argument("--workload", default="halo",
+                   choices=["halo", "spmv", "fused", "diamond", "noop"])
+    s.add_argument("--noop-width", type=int, default=1)
+    s.add_argument("--host", action="store_true",
+                   help="time schedules on the host executor (CPU-only graphs)")
     s.add_argument("--solver", default="mcts", choices=["mcts", "dfs"])
     s.add_argument("--strategy", default="FastMin")
     s.add_argument("--iters", type=int, default=300)
@@ -146,6 +165,8 @@ def main(argv=None) -> int:
     s.add_argument("--max-retries", type=int, default=10)
     s.add_argument("--target-secs", type=float, default=0.01)
     s.add_argument("--mode", default="eager", choices=["eager", "graph"])
+    s.add_argument("--graph-unroll", type=int, default=1,
+                   help="graph mode: iterations per hipGraph launch while benchmarking")
     s.add_argument("--sim", action="store_true", help="discrete-event cost model, no GPU")
     s.add_argument("--replay", default="", help="results CSV to replay instead of running")
     s.add_argument("--seed", type=int, default=0)
@@ -166,6 +187,7 @@ def main(argv=None) -> int:
     s.add_argument("--fuse", default="choice")
     s.add_argument("--transport", default="auto")
     s.add_argument("--spmv-m", type=int, default=150_000)
+    s.add_argument("--spmv-form", default="choice", choices=["choice", "split", "accum"])
     s.set_defaults(fn=cmd_search)
     r = sub.add_parser("rules")
     r.add_argument("results")

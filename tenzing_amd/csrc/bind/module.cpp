@@ -626,6 +626,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("device", &SpmvArgs::device)
       .def_readwrite("compound", &SpmvArgs::compound)
       .def_readwrite("kernel_choice", &SpmvArgs::kernel_choice)
+      .def_readwrite("form", &SpmvArgs::form)
       .def_readwrite("prefix", &SpmvArgs::prefix)
       .def("json", [](const SpmvArgs &a) { return a.json().dump(); });
   py::class_<DistSpmv, std::shared_ptr<DistSpmv>>(m, "DistSpmv")

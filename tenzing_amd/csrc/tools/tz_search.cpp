@@ -50,7 +50,7 @@ void usage() {
          "  [--strategy NAME] [--iters N] [--time-budget S] [--streams N] [--bench-iters N]\n"
          "  [--target-secs S] [--mode eager|graph] [--sim] [--seed N] [--no-expand-rollout]\n"
          "  [--halo-n N] [--nq N] [--ghost N] [--neighbors 6|26] [--fuse none|pack|all]\n"
-         "  [--transport auto|rccl|copy|direct] [--spmv-m N] [--max-seqs N] [--rdzv-file PATH]\n"
+         "  [--transport auto|rccl|copy|direct] [--spmv-m N] [--spmv-form choice|split|accum] [--max-seqs N] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--watchdog S]\n";
 }
@@ -133,6 +133,7 @@ int main(int argc, char **argv) {
       s.rank = rank;
       s.size = size;
       s.prefix = workload == "halo+spmv" ? "spmv_" : "";
+      s.form = a.get("spmv-form", "choice");
       spmv = std::make_shared<DistSpmv>(s);
       if (!sim) spmv->setup(ctrl.get());
       spmv->add_to_graph(*g);

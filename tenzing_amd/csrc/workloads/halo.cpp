@@ -355,6 +355,8 @@ void HaloExchange::setup(Ctrl *ctrl) {
 void HaloExchange::init_grid(void *stream) {
   TZ_CHECK(ready(), "halo not set up");
   kern::halo_init(grid(), geom(), stream);
+  // synchronous: schedules run on non-blocking streams that do not order after `stream`
+  TZ_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
 }
 
 uint64_t HaloExchange::check_grid(void *stream) {

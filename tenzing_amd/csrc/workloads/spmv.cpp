@@ -22,6 +22,7 @@ Json SpmvArgs::json() const {
   j["size"] = size;
   j["compound"] = compound;
   j["kernel_choice"] = kernel_choice;
+  j["form"] = form;
   return j;
 }
 
@@ -75,32 +76,37 @@ namespace {
 
 class SpmvLocal : public GpuOp {
 public:
-  SpmvLocal(std::shared_ptr<const DistSpmv> s, std::string name, int lanes)
-      : s_(std::move(s)), name_(std::move(name)), lanes_(lanes) {}
+  SpmvLocal(std::shared_ptr<const DistSpmv> s, std::string name, int lanes, bool intoY)
+      : s_(std::move(s)), name_(std::move(name)), lanes_(lanes), intoY_(intoY) {}
   std::string name() const override { return name_; }
   std::string kind() const override { return "SpmvLocal"; }
   double bytes() const override { return 12.0 * double(s_->local_nnz()) + 8.0 * double(s_->local_rows()); }
   double cost_us() const override { return 4.0 + bytes() / 3.0e6; }
-  void launch(void *st, Executor &) const override { s_->spmv_local(lanes_, st); }
+  void launch(void *st, Executor &) const override { s_->spmv_local(lanes_, st, intoY_); }
 
 private:
   std::shared_ptr<const DistSpmv> s_;
   std::string name_;
   int lanes_;
+  bool intoY_;
 };
 
 class SpmvRemote : public GpuOp {
 public:
-  SpmvRemote(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
+  SpmvRemote(std::shared_ptr<const DistSpmv> s, std::string name, bool accumulate)
+      : s_(std::move(s)), name_(std::move(name)), acc_(accumulate) {}
   std::string name() const override { return name_; }
   std::string kind() const override { return "SpmvRemote"; }
-  double bytes() const override { return 12.0 * double(s_->remote_nnz()) + 8.0 * double(s_->local_rows()); }
-  double cost_us() const override { return 4.0 + bytes() / 3.0e6; }
-  void launch(void *st, Executor &) const override { s_->spmv_remote(st); }
+  double bytes() const override {
+    return s_->remote_nnz() ? 12.0 * double(s_->remote_nnz()) + 8.0 * double(s_->local_rows()) : 0.0;
+  }
+  double cost_us() const override { return s_->remote_nnz() ? 4.0 + bytes() / 3.0e6 : 0.5; }
+  void launch(void *st, Executor &) const override { s_->spmv_remote(st, acc_); }
 
 private:
   std::shared_ptr<const DistSpmv> s_;
   std::string name_;
+  bool acc_;
 };
 
 class SpmvScatter : public GpuOp {
@@ -108,7 +114,7 @@ public:
   SpmvScatter(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
   std::string name() const override { return name_; }
   std::string kind() const override { return "SpmvScatter"; }
-  double cost_us() const override { return 3.0 + 12.0 * double(s_->send_elems()) / 2.0e6; }
+  double cost_us() const override { return s_->send_elems() ? 3.0 + 12.0 * double(s_->send_elems()) / 2.0e6 : 0.5; }
   void launch(void *st, Executor &) const override { s_->scatter(st); }
 
 private:
@@ -255,7 +261,9 @@ void DistSpmv::setup(Ctrl *ctrl) {
 }
 
 void DistSpmv::reset_y(void *stream) {
+  // synchronous: schedules run on non-blocking streams that do not order after `stream`
   TZ_HIP(hipMemsetAsync(dY_.get(), 0, dY_.bytes(), static_cast<hipStream_t>(stream)));
+  TZ_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
 }
 
 double DistSpmv::check(void *stream) {
@@ -269,6 +277,7 @@ double DistSpmv::check(void *stream) {
 }
 
 void DistSpmv::scatter(void *stream) const {
+  if (sendIdx_.empty()) return; // nothing any peer needs (e.g. one rank)
   kern::gather_f32(int(sendIdx_.size()), dX_.as<float>(), dSendIdx_.as<int32_t>(), dSend_.as<float>(), stream);
 }
 
@@ -289,45 +298,79 @@ void DistSpmv::exchange(void *stream) const {
   comm_->exchange(xs, 0, stream);
 }
 
-void DistSpmv::spmv_local(int lanes, void *stream) const {
+void DistSpmv::spmv_local(int lanes, void *stream, bool intoY) const {
   kern::csr_spmv(int(local_rows()), dLocalRow_.as<int32_t>(), dLocalCol_.as<int32_t>(),
-                 dLocalVal_.as<float>(), dX_.as<float>(), dYl_.as<float>(), lanes > 0 ? lanes : lanes_,
-                 false, stream);
+                 dLocalVal_.as<float>(), dX_.as<float>(), (intoY ? dY_ : dYl_).as<float>(),
+                 lanes > 0 ? lanes : lanes_, false, stream);
 }
 
-void DistSpmv::spmv_remote(void *stream) const {
+void DistSpmv::spmv_remote(void *stream, bool accumulate) const {
+  // an empty remote block leaves y_r at the zeros set up once (split form) and adds nothing
+  // (accumulate form)
+  if (remote_.nnz() == 0) return;
   kern::csr_spmv(int(local_rows()), dRemoteRow_.as<int32_t>(), dRemoteCol_.as<int32_t>(),
-                 dRemoteVal_.as<float>(), dXr_.as<float>(), dYr_.as<float>(), lanes_, false, stream);
+                 dRemoteVal_.as<float>(), dXr_.as<float>(), (accumulate ? dY_ : dYr_).as<float>(),
+                 lanes_, accumulate, stream);
 }
 
 void DistSpmv::add(void *stream) const {
   kern::vector_add_f32(int(local_rows()), dYl_.as<float>(), dYr_.as<float>(), dY_.as<float>(), stream);
 }
 
-std::shared_ptr<const Graph> DistSpmv::op_graph() {
-  if (inner_) return inner_;
+std::shared_ptr<Graph> DistSpmv::form_graph(bool accum, const std::string &p) {
+  // reference SpMV CompoundOp (ops_spmv.cuh:300-436): Scatter -> PostSend/PostRecv ->
+  // WaitRecv -> remote SpMV, local SpMV, VectorAdd. Here the post/wait pairs are one
+  // stream-ordered RCCL exchange.
   auto self = std::const_pointer_cast<const DistSpmv>(shared_from_this());
-  const std::string p = a_.prefix;
   auto g = std::make_shared<Graph>();
   OpPtr yl;
   if (a_.kernel_choice) {
     std::vector<OpPtr> ch;
-    for (int w : {4, 8, 16}) ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w));
+    for (int w : {4, 8, 16})
+      ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w, accum));
     yl = std::make_shared<StaticChoiceOp>(p + "yl", ch);
   } else {
-    yl = std::make_shared<SpmvLocal>(self, p + "yl", 0);
+    yl = std::make_shared<SpmvLocal>(self, p + "yl", 0, accum);
   }
   auto scatter = std::make_shared<SpmvScatter>(self, p + "Pack");
   auto xchg = std::make_shared<SpmvExchange>(self, p + "exchange");
-  auto yr = std::make_shared<SpmvRemote>(self, p + "yr");
-  auto y = std::make_shared<SpmvAdd>(self, p + "y");
+  auto yr = std::make_shared<SpmvRemote>(self, p + "yr", accum);
   g->start_then(yl);
   g->start_then(scatter);
   g->then(scatter, xchg);
   g->then(xchg, yr);
-  g->then(yl, y);
-  g->then(yr, y);
-  g->then_finish(y);
+  if (accum) {
+    // y = A_l x must land before y += A_r x_r
+    g->then(yl, yr);
+    g->then_finish(yr);
+  } else {
+    auto y = std::make_shared<SpmvAdd>(self, p + "y");
+    g->then(yl, y);
+    g->then(yr, y);
+    g->then_finish(y);
+  }
+  return g;
+}
+
+std::shared_ptr<const Graph> DistSpmv::op_graph() {
+  if (inner_) return inner_;
+  const std::string &p = a_.prefix;
+  const std::string &f = a_.form;
+  TZ_CHECK(f == "split" || f == "accum" || f == "choice",
+           "SpMV form must be split, accum or choice (got " << f << ")");
+  if (f != "choice") {
+    inner_ = form_graph(f == "accum", p);
+    return inner_;
+  }
+  // both forms as alternatives; accum-form op names carry an extra "a_" so every op name
+  // stays unique in the expanded graph
+  std::vector<OpPtr> forms = {
+      std::make_shared<StaticCompoundOp>(p + "split", form_graph(false, p)),
+      std::make_shared<StaticCompoundOp>(p + "accum", form_graph(true, p + "a_"))};
+  auto g = std::make_shared<Graph>();
+  auto c = std::make_shared<StaticChoiceOp>(p + "form", forms);
+  g->start_then(c);
+  g->then_finish(c);
   inner_ = g;
   return inner_;
 }

@@ -222,6 +222,10 @@ struct SpmvArgs {
   int device = -1;
   bool compound = true;     // wrap in an expandable CompoundOp (reference SpMV CompoundOp)
   bool kernel_choice = true; // local SpMV as a ChoiceOp over lanes-per-row variants
+  // "split": y = A_l x + A_r x_r through two partial vectors and a VectorAdd (reference
+  // structure); "accum": y = A_l x, then y += A_r x_r (no partials, no add; the remote SpMV
+  // waits for the local one); "choice": a ChoiceOp over both forms
+  std::string form = "choice";
   std::string prefix = "";  // op-name prefix (to combine several workloads in one graph)
   Json json() const;
 };
@@ -250,8 +254,11 @@ public:
   // op bodies
   void scatter(void *stream) const;
   void exchange(void *stream) const;
-  void spmv_local(int lanes, void *stream) const;
-  void spmv_remote(void *stream) const;
+  /// local block product into the partial y_l (or straight into y when `into_y`)
+  void spmv_local(int lanes, void *stream, bool into_y = false) const;
+  /// remote block product into the partial y_r (or y += ... when `accumulate`); no launch
+  /// when the remote block is empty
+  void spmv_remote(void *stream, bool accumulate = false) const;
   void add(void *stream) const;
 
 private:
@@ -269,6 +276,7 @@ private:
   DeviceBuffer dX_, dXr_, dSendIdx_, dSend_, dYl_, dYr_, dY_;
   std::shared_ptr<RcclComm> comm_;
   std::shared_ptr<const Graph> inner_;
+  std::shared_ptr<Graph> form_graph(bool accum, const std::string &p);
 };
 
 } // namespace tz

@@ -134,10 +134,11 @@ def test_halo_rccl_self_exchange(tz, gpu):
         assert halo.check_grid() == 0
 
 
-def test_spmv_workload_correct(tz, gpu):
+@pytest.mark.parametrize("form", ["split", "accum", "choice"])
+def test_spmv_workload_correct(tz, gpu, form):
     from tenzing_amd.models import SpmvConfig, build_spmv
 
-    sp, g = build_spmv(SpmvConfig(m=20000), tz.SelfCtrl(), device=0)
+    sp, g = build_spmv(SpmvConfig(m=20000, form=form), tz.SelfCtrl(), device=0)
     rt = tz.HipRuntime(device=0, n_streams=2)
     seqs = tz.get_all_sequences(g, tz.Platform(2), max_seqs=40)
     assert len(seqs) >= 4
