@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Isolated CSR SpMV kernel timings (MI355X): every lanes-per-row variant and the CSR-stream
+kernel on the SpMV workload's local block (m=150,000, nnz=10 m by default).
+
+  python scripts/spmv_bench.py [--m 150000] [--reps 200]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import tenzing_amd as tz  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=150_000)
+    ap.add_argument("--per-row", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=200)
+    a = ap.parse_args()
+    rp, ci, val = tz._tz.random_band_matrix(a.m, a.m, a.per_row * a.m, 1)
+    dev = "cuda"
+    rp_t = torch.tensor(rp, dtype=torch.int32, device=dev)
+    ci_t = torch.tensor(ci, dtype=torch.int32, device=dev)
+    v_t = torch.tensor(val, dtype=torch.float32, device=dev)
+    x = torch.randn(a.m, dtype=torch.float32, device=dev)
+    y = torch.zeros(a.m, dtype=torch.float32, device=dev)
+    nbytes = rp_t.numel() * 4 + ci_t.numel() * 8 + a.m * 8
+    st = torch.cuda.current_stream().cuda_stream
+    K = tz._tz.kernels
+    for lanes in (4, 8, 16, 32, -1):
+        def fn():
+            K.csr_spmv(a.m, rp_t.data_ptr(), ci_t.data_ptr(), v_t.data_ptr(), x.data_ptr(),
+                       y.data_ptr(), lanes, False, st)
+        for _ in range(5):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / a.reps
+        print(json.dumps({"lanes": lanes, "us": round(us, 2), "nnz": ci_t.numel(),
+                          "GBps": round(nbytes / us / 1e3, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

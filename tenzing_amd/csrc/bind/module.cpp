@@ -546,7 +546,8 @@ PYBIND11_MODULE(_tz, m) {
       .def("num_streams", &HipRuntime::num_streams)
       .def("native_stream", [](HipRuntime &r, int s) { return reinterpret_cast<uintptr_t>(r.native_stream(s)); })
       .def("device_sync", &HipRuntime::device_sync, py::call_guard<py::gil_scoped_release>())
-      .def("set_watchdog", &HipRuntime::set_watchdog);
+      .def("set_watchdog", &HipRuntime::set_watchdog)
+      .def_property("spin_sync", &HipRuntime::spin_sync, &HipRuntime::set_spin_sync);
 
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def(py::init([](Ctrl &c, int dev) { return std::make_shared<RcclComm>(c, dev); }))

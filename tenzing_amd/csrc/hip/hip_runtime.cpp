@@ -31,7 +31,9 @@ static hipStream_t S(void *p) { return static_cast<hipStream_t>(p); }
 static hipEvent_t E(void *p) { return static_cast<hipEvent_t>(p); }
 
 HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
-    : mode_(opts.mode), unroll_(std::max(1, opts.graph_unroll)), watchdogS_(opts.watchdog_s) {
+    : mode_(opts.mode), unroll_(std::max(1, opts.graph_unroll)), spinSync_(opts.spin_sync),
+      watchdogS_(opts.watchdog_s) {
+  if (const char *v = std::getenv("TZ_SPIN_SYNC")) spinSync_ = std::atoi(v) != 0;
   TZ_CHECK(opts.n_streams >= 1, "need at least one stream");
   if (opts.device >= 0) TZ_HIP(hipSetDevice(opts.device));
   TZ_HIP(hipGetDevice(&device_));
@@ -123,9 +125,30 @@ void HipRuntime::stream_wait_event(int stream, int e) {
   TZ_HIP(hipStreamWaitEvent(S(native_stream(stream)), E(event(e)), 0));
 }
 
-void HipRuntime::event_sync(int e) { TZ_HIP(hipEventSynchronize(E(event(e)))); }
+void HipRuntime::event_sync(int e) {
+  hipEvent_t ev = E(event(e));
+  if (spinSync_) {
+    // busy-poll: the host wakes as soon as the event completes (no blocking-wait latency)
+    hipError_t r;
+    while ((r = hipEventQuery(ev)) == hipErrorNotReady) {
+    }
+    TZ_HIP(r);
+  } else {
+    TZ_HIP(hipEventSynchronize(ev));
+  }
+}
 
-void HipRuntime::stream_sync(int stream) { TZ_HIP(hipStreamSynchronize(S(native_stream(stream)))); }
+void HipRuntime::stream_sync(int stream) {
+  hipStream_t s = S(native_stream(stream));
+  if (spinSync_) {
+    hipError_t r;
+    while ((r = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    TZ_HIP(r);
+  } else {
+    TZ_HIP(hipStreamSynchronize(s));
+  }
+}
 
 void HipRuntime::stream_wait(int waiter, int waitee) {
   hipEvent_t ev = E(internal_event());
@@ -172,8 +195,12 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
   hipGraph_t graph = nullptr;
   TZ_HIP(hipGraphCreate(&graph, 0));
   SyncModel model(nS);
-  std::vector<std::vector<hipGraphNode_t>> nodes(nS); // per stream, in issue order
-  size_t edges = 0;
+  // per stream, in issue order: the graph nodes that stand for each issued GPU op. An op that
+  // enqueued nothing stands for its own dependencies (no empty node: every empty node costs a
+  // barrier packet — ~10 us — at replay), an op that captured a fan-out for all its tails.
+  using NodeSet = std::vector<hipGraphNode_t>;
+  std::vector<std::vector<NodeSet>> nodes(nS);
+  size_t edges = 0, real = 0;
   try {
     // replaying the sequence `iterations` times through one model orders iteration i+1 after
     // iteration i exactly as the schedule's closing host syncs do in eager mode
@@ -186,20 +213,27 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
         TZ_CHECK(s >= 0 && s < nS, "stream " << s << " out of range");
         // dependencies: previous op on this stream + the latest op of every other stream that
         // the schedule's events / host syncs make complete before this one is issued
-        std::vector<hipGraphNode_t> deps;
-        if (!nodes[s].empty()) deps.push_back(nodes[s].back());
+        NodeSet deps;
+        if (!nodes[s].empty()) deps = nodes[s].back();
         for (int t = 0; t < nS; ++t) {
           if (t == s) continue;
           const int k = model.known(s, t);
-          if (k > 0) deps.push_back(nodes[t][size_t(k) - 1]);
+          if (k > 0) {
+            const NodeSet &d = nodes[t][size_t(k) - 1];
+            deps.insert(deps.end(), d.begin(), d.end());
+          }
         }
+        std::sort(deps.begin(), deps.end());
+        deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
         // record the op alone on its own stream, directly into the schedule graph behind its
         // dependencies (flat graph: no child-graph indirection at replay)
         hipStream_t st = S(streams_[s]);
         TZ_HIP(hipStreamBeginCaptureToGraph(st, graph, deps.data(), nullptr, deps.size(),
                                             hipStreamCaptureModeThreadLocal));
         hipGraph_t captured = nullptr;
-        std::vector<hipGraphNode_t> tails;
+        NodeSet tails;
+        size_t before = 0, after = 0;
+        TZ_HIP(hipGraphGetNodes(graph, nullptr, &before));
         try {
           b.unbound()->launch(st, *this);
           hipStreamCaptureStatus cs;
@@ -212,32 +246,25 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
           throw;
         }
         TZ_HIP(hipStreamEndCapture(st, &captured));
-        hipGraphNode_t node = nullptr;
-        std::vector<hipGraphNode_t> sd = deps, st2 = tails;
-        std::sort(sd.begin(), sd.end());
-        std::sort(st2.begin(), st2.end());
-        if (tails.size() == 1 && sd != st2) {
-          node = tails[0]; // the op is one node (or a chain ending in one node)
-        } else if (sd == st2) {
-          // the op enqueued nothing: keep an empty placeholder so later edges stay valid
-          TZ_HIP(hipGraphAddEmptyNode(&node, graph, deps.data(), deps.size()));
+        TZ_HIP(hipGraphGetNodes(graph, nullptr, &after));
+        std::sort(tails.begin(), tails.end());
+        if (after == before) {
+          nodes[s].push_back(deps); // enqueued nothing: stands for its dependencies
         } else {
-          TZ_HIP(hipGraphAddEmptyNode(&node, graph, tails.data(), tails.size()));
+          nodes[s].push_back(tails);
+          real += after - before;
+          edges += deps.size();
         }
-        nodes[s].push_back(node);
-        edges += deps.size();
       }
       model.apply(op);
     }
-    size_t n = 0;
-    for (auto &v : nodes) n += v.size();
     hipGraphExec_t exec = nullptr;
     TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
     TZ_HIP(hipGraphDestroy(graph));
     graph = nullptr;
-    nodesOut = n;
+    nodesOut = real;
     edgesOut = edges;
-    TZ_LOG(Debug, "graph mode: " << iterations << " iteration(s), " << n << " nodes, " << edges
+    TZ_LOG(Debug, "graph mode: " << iterations << " iteration(s), " << real << " nodes, " << edges
                                  << " edges");
     // upload once so the first timed launch does not pay for it
     TZ_HIP(hipGraphUpload(exec, S(streams_[0])));
@@ -278,7 +305,7 @@ void HipRuntime::run(int64_t n) {
       for (; i + unroll_ <= n; i += unroll_)
         TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExecU_), origin));
     for (; i < n; ++i) TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExec_), origin));
-    TZ_HIP(hipStreamSynchronize(origin));
+    stream_sync(0);
   } else {
     for (int64_t i = 0; i < n; ++i) {
       internalUsed_ = 0;

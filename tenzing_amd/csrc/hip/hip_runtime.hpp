@@ -39,6 +39,7 @@ struct HipRuntimeOpts {
   ExecMode mode = ExecMode::Eager;
   double watchdog_s = 0;       // 0 = off
   int graph_unroll = 1;        // iterations per hipGraph launch in Graph mode
+  bool spin_sync = true;       // host syncs busy-poll (env TZ_SPIN_SYNC=0/1 overrides)
 };
 
 // ExecutorRunner first: the Python bindings expose HipRuntime through that base
@@ -76,6 +77,8 @@ public:
   /// number of dependency edges of the compiled graph
   size_t graph_edges() const { return graphEdges_; }
   void set_watchdog(double s) { watchdogS_ = s; }
+  void set_spin_sync(bool on) { spinSync_ = on; }
+  bool spin_sync() const { return spinSync_; }
   /// compile `u` consecutive iterations into one graph (amortizes the per-launch cost; the
   /// iterations stay ordered exactly as the schedule's final host syncs order them)
   void set_graph_unroll(int u);
@@ -98,6 +101,7 @@ private:
   void *graphExec_ = nullptr;  // one iteration
   void *graphExecU_ = nullptr; // unroll_ iterations
   int unroll_ = 1;
+  bool spinSync_ = true;
   size_t graphNodes_ = 0, graphEdges_ = 0;
 
   double watchdogS_ = 0;

@@ -64,7 +64,8 @@ struct CopyDesc {
 void copy_many(const CopyDesc *d, int n, void *stream);
 
 /// y[r] = sum_j A[r,j] x[j] for CSR A (f32 values, i32 indices). `lanesPerRow` in {1,2,4,8,16,32,64}
-/// (0 = pick from nnz/row). When `accumulate`, y[r] += ... instead.
+/// (0 = 8), or -1 for the CSR-stream kernel (block-contiguous nnz streaming + LDS segmented
+/// reduction). When `accumulate`, y[r] += ... instead.
 void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,
               const float *x, float *y, int lanesPerRow, bool accumulate, void *stream);
 /// dst[i] = src[idx[i]]

@@ -328,6 +328,7 @@ std::shared_ptr<Graph> DistSpmv::form_graph(bool accum, const std::string &p) {
     std::vector<OpPtr> ch;
     for (int w : {4, 8, 16})
       ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w, accum));
+    ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_stream", -1, accum));
     yl = std::make_shared<StaticChoiceOp>(p + "yl", ch);
   } else {
     yl = std::make_shared<SpmvLocal>(self, p + "yl", 0, accum);

@@ -73,8 +73,8 @@ def csr_spmv(row_ptr: torch.Tensor, col_ind: torch.Tensor, val: torch.Tensor, x:
     _check(y, torch.float32, "y")
     if y.numel() < n:
         raise ValueError("y too small")
-    if lanes not in (0, 1, 2, 4, 8, 16, 32, 64):
-        raise ValueError("lanes must be a power of two <= 64")
+    if lanes not in (-1, 0, 1, 2, 4, 8, 16, 32, 64):
+        raise ValueError("lanes must be a power of two <= 64 (or -1: CSR-stream kernel)")
     K.csr_spmv(n, row_ptr.data_ptr(), col_ind.data_ptr(), val.data_ptr(), x.data_ptr(),
                y.data_ptr(), lanes, accumulate, _stream())
     return y

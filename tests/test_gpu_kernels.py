@@ -100,10 +100,12 @@ def test_box_copy_many_equals_single(tz, gpu):
         assert torch.equal(t1, t2)
 
 
-@pytest.mark.parametrize("lanes", [0, 1, 4, 8, 16, 64])
-def test_csr_spmv_matches_torch(tz, gpu, lanes):
+@pytest.mark.parametrize("lanes,per_row", [(0, 10), (1, 10), (4, 10), (8, 10), (16, 10),
+                                           (64, 10), (-1, 10), (-1, 90), (16, 90)])
+def test_csr_spmv_matches_torch(tz, gpu, lanes, per_row):
+    # per_row 90: a 64-row CSR-stream block holds > 4096 nnz, exercising its multi-pass path
     n = 5000
-    rp, ci, val = tz._tz.random_band_matrix(n, 300, 10 * n, 7)
+    rp, ci, val = tz._tz.random_band_matrix(n, 300, per_row * n, 7)
     rp_t = torch.tensor(rp, dtype=torch.int32, device="cuda")
     ci_t = torch.tensor(ci, dtype=torch.int32, device="cuda")
     v_t = torch.tensor(val, dtype=torch.float32, device="cuda")
