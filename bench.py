@@ -26,6 +26,23 @@ import sys
 import time
 
 
+def _start_deadline(seconds: float) -> None:
+    """A hung collective (a rank that died during communicator setup, a deadlocked transfer)
+    must not hold the node forever: past the deadline every rank exits with status 4."""
+    if seconds <= 0:
+        return
+    import threading
+
+    def fire():
+        print(f"bench.py: deadline of {seconds:.0f} s exceeded; aborting", file=sys.stderr,
+              flush=True)
+        os._exit(4)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -50,7 +67,10 @@ def main() -> int:
     ap.add_argument("--graph-unroll", type=int, default=10,
                     help="iterations per hipGraph launch when timing the graph-compiled schedule")
     ap.add_argument("--csv", default="", help="write the search results CSV here (rank 0)")
+    ap.add_argument("--deadline-s", type=float, default=1500.0,
+                    help="abort (exit 4) if the whole run takes longer (hung collective)")
     args = ap.parse_args()
+    _start_deadline(args.deadline_s)
 
     import tenzing_amd as tz
     from tenzing_amd.models import HaloConfig, build_halo

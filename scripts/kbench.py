@@ -37,7 +37,10 @@ def main():
     ap.add_argument("--order", default="xyzq")
     args = ap.parse_args()
     torch.zeros(1, device="cuda")
-    h, _ = build_halo(HaloConfig(n=args.n, neighbors=args.neighbors, order=args.order), tz.SelfCtrl(), device=0)
+    h, _ = build_halo(HaloConfig(n=args.n, neighbors=args.neighbors, order=args.order,
+                                 transport="copy"), tz.SelfCtrl(), device=0)
+    hd, _ = build_halo(HaloConfig(n=args.n, neighbors=args.neighbors, order=args.order,
+                                  transport="direct"), tz.SelfCtrl(), device=0)
     print(json.dumps({"order": args.order, "grid_bytes": h.grid_elems() * 8}), flush=True)
     st = torch.cuda.current_stream().cuda_stream
     out = []
@@ -59,7 +62,15 @@ def main():
         rec("pack", 2 * nb, timeit(lambda: h.pack(i, st), args.reps), dir=h.dir_name(i), kind=kind)
         rec("unpack", 2 * nb, timeit(lambda: h.unpack(h.opposite(i), st), args.reps), dir=h.dir_name(i), kind=kind)
         rec("shift", 2 * nb, timeit(lambda: h.shift(i, st), args.reps), dir=h.dir_name(i), kind=kind)
+        rec("direct", 2 * nb, timeit(lambda: hd.direct(i, st), args.reps), dir=h.dir_name(i), kind=kind)
     tot = h.exchange_bytes()
+    faces = [i for i in range(h.ndirs()) if sum(map(abs, h.dir(i))) == 1]
+    small = [i for i in range(h.ndirs()) if sum(map(abs, h.dir(i))) > 1]
+    fb = sum(h.box_elems(i) for i in faces) * 8
+    rec("direct_all", 2 * tot, timeit(lambda: hd.direct_group(list(range(h.ndirs())), st), max(5, args.reps // 5)))
+    rec("direct_faces", 2 * fb, timeit(lambda: hd.direct_group(faces, st), max(5, args.reps // 5)))
+    if small:
+        rec("direct_small", 2 * (tot - fb), timeit(lambda: hd.direct_group(small, st), args.reps))
     rec("pack_all", 2 * tot, timeit(lambda: h.pack_all(st), max(5, args.reps // 5)))
     rec("unpack_all", 2 * tot, timeit(lambda: h.unpack_all(st), max(5, args.reps // 5)))
     rec("shift_all", 2 * tot, timeit(lambda: h.shift_all(st), max(5, args.reps // 5)))

@@ -28,6 +28,7 @@ Json HaloArgs::json() const {
   j["px"] = px;
   j["py"] = py;
   j["pz"] = pz;
+  j["pitch_pad"] = pitch_pad;
   return j;
 }
 
@@ -145,6 +146,7 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.neighbors == 6 || a_.neighbors == 26, "neighbors must be 6 or 26");
   TZ_CHECK(a_.order == "xyzq" || a_.order == "qxyz", "order must be xyzq or qxyz");
   TZ_CHECK(a_.rank >= 0 && a_.rank < a_.size, "bad rank");
+  TZ_CHECK(a_.pitch_pad >= 0 && a_.pitch_pad % 16 == 0, "pitch_pad must be a multiple of 16");
 
   // rank grid: prime factors (descending) multiply the currently smallest dimension, ties to
   // the later dimension (reference halo_run_strategy.hpp:80-98: 2 -> 1x1x2, 4 -> 1x2x2)
@@ -183,7 +185,7 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   const int64_t X = a_.nx + 2 * a_.ghost, Y = a_.ny + 2 * a_.ghost, Z = a_.nz + 2 * a_.ghost;
   if (a_.order == "xyzq") {
     xoff_ = (8 - a_.ghost % 8) % 8;                 // interior rows start 64-B aligned
-    pitch_ = round_up(xoff_ + X, 16);                // rows are whole 128-B lines
+    pitch_ = round_up(xoff_ + X, 16) + a_.pitch_pad; // rows are whole 128-B lines
     sy_ = pitch_;
     sz_ = pitch_ * Y;
     sq_ = sz_ * Z;
@@ -211,7 +213,7 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
       }
     }
     xoff_ = best < 0 ? 0 : best;
-    pitch_ = round_up(int64_t(a_.nq) * (xoff_ + X), 16);
+    pitch_ = round_up(int64_t(a_.nq) * (xoff_ + X), 16) + a_.pitch_pad;
     sy_ = pitch_;
     sz_ = pitch_ * Y;
     sq_ = 1;

@@ -108,6 +108,7 @@ struct HaloArgs {
   int comms = 0;                  // RCCL communicators (0 = one per direction)
   int rank = 0, size = 1;
   int px = 0, py = 0, pz = 0;     // rank grid (0 = from prime factors, reference style)
+  int pitch_pad = 0;              // extra row-pitch elements (multiple of 16: keeps alignment)
   int device = -1;
   Json json() const;
 };

@@ -27,6 +27,7 @@ class HaloConfig:
     transport: str = "auto"  # rccl | copy | direct | auto (direct on 1 rank, else rccl)
     fuse: str = "none"    # none | pack | all | groups | choice
     comms: int = 0        # RCCL communicators (0 = one per direction)
+    pitch_pad: int = 0    # extra row-pitch elements (multiple of 16)
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":
         a = _tz.HaloArgs()
@@ -38,6 +39,7 @@ class HaloConfig:
         a.transport = self.transport
         a.fuse = self.fuse
         a.comms = self.comms
+        a.pitch_pad = self.pitch_pad
         a.rank, a.size, a.device = rank, size, device
         return a
 
