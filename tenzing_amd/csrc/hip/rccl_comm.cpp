@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 
 namespace tz {
@@ -36,6 +37,19 @@ RcclComm::RcclComm(Ctrl &ctrl, int device) : rank_(ctrl.rank()), size_(ctrl.size
   }
   ctrl.bcast(s, 0);
   std::memcpy(&id, s.data(), sizeof(id));
+  ncclComm_t c = nullptr;
+  TZ_NCCL(ncclCommInitRank(&c, size_, id, rank_));
+  comm_ = c;
+}
+
+RcclComm::RcclComm(const std::string &uniqueId, int rank, int size, int device)
+    : rank_(rank), size_(size) {
+  if (device >= 0) {
+    if (hipSetDevice(device) != hipSuccess) TZ_THROW("hipSetDevice failed");
+  }
+  ncclUniqueId id;
+  TZ_CHECK(uniqueId.size() == sizeof(id), "bad RCCL unique id");
+  std::memcpy(&id, uniqueId.data(), sizeof(id));
   ncclComm_t c = nullptr;
   TZ_NCCL(ncclCommInitRank(&c, size_, id, rank_));
   comm_ = c;
@@ -78,8 +92,22 @@ std::string RcclComm::version() {
 }
 
 std::vector<std::shared_ptr<RcclComm>> make_rccl_comms(Ctrl &ctrl, int device, int n) {
+  // one broadcast carries every unique id (a control-plane round trip per communicator adds
+  // up at 26 directions), then every rank initializes the communicators in the same order
+  ncclUniqueId id;
+  std::string ids(sizeof(id) * size_t(std::max(n, 0)), '\0');
+  if (ctrl.rank() == 0) {
+    for (int i = 0; i < n; ++i) {
+      TZ_NCCL(ncclGetUniqueId(&id));
+      std::memcpy(&ids[sizeof(id) * size_t(i)], &id, sizeof(id));
+    }
+  }
+  ctrl.bcast(ids, 0);
+  TZ_CHECK(ids.size() == sizeof(id) * size_t(std::max(n, 0)), "unique-id broadcast truncated");
   std::vector<std::shared_ptr<RcclComm>> out;
-  for (int i = 0; i < n; ++i) out.push_back(std::make_shared<RcclComm>(ctrl, device));
+  for (int i = 0; i < n; ++i)
+    out.push_back(std::make_shared<RcclComm>(ids.substr(sizeof(id) * size_t(i), sizeof(id)),
+                                             ctrl.rank(), ctrl.size(), device));
   return out;
 }
 

@@ -23,6 +23,8 @@ class RcclComm {
 public:
   /// collective over `ctrl`: rank 0 creates the unique id, broadcasts it, all ranks init
   RcclComm(Ctrl &ctrl, int device);
+  /// init from a unique id every rank already holds (ncclUniqueId bytes)
+  RcclComm(const std::string &uniqueId, int rank, int size, int device);
   ~RcclComm();
   RcclComm(const RcclComm &) = delete;
   RcclComm &operator=(const RcclComm &) = delete;
