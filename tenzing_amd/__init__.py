@@ -97,6 +97,7 @@ from ._tz import (  # noqa: E402,F401
     TcpCtrl,
     TzError,
     dfs_explore,
+    enable_roctx,
     get_all_sequences,
     hip_device_count,
     mcts_explore,

@@ -61,7 +61,7 @@ def _ninja_file(debug: bool) -> str:
         f"hipflags = {common} {hipdefs}",
         f"devflags = {common} --offload-arch={ARCH} -munsafe-fp-atomics -ffp-contract=fast",
         f"pyflags = -I{pybind11.get_include()} -I{py_inc}",
-        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lpthread",
+        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lpthread",
         "rule cxx",
         "  command = $cxx $cflags $extra -MMD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",

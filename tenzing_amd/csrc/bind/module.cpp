@@ -152,6 +152,8 @@ PYBIND11_MODULE(_tz, m) {
   m.def("set_log_level", [](int l) { set_log_level(LogLevel(l)); });
   m.def("set_log_rank", [](int r) { log_rank() = r; });
   m.def("hip_device_count", &hip_device_count);
+  m.def("enable_roctx", &enable_roctx, py::arg("on") = true,
+        "emit roctx ranges for MCTS phases and eager schedule ops (rocprofv3 --marker-trace)");
   m.def("pci_bus_id", [](int dev) {
     char buf[64] = {0};
     if (hipDeviceGetPCIBusId(buf, sizeof(buf), dev) != hipSuccess) return std::string();

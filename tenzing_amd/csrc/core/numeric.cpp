@@ -17,6 +17,11 @@ LogLevel g_log_level = [] {
   return LogLevel::Warn;
 }();
 LogLevel log_level() { return g_log_level; }
+
+TraceHooks &trace_hooks() {
+  static TraceHooks h;
+  return h;
+}
 void set_log_level(LogLevel lvl) { g_log_level = lvl; }
 int &log_rank() {
   static int r = 0;

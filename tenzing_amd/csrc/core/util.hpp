@@ -49,11 +49,34 @@ struct Counters {
 };
 
 /// RAII timer that adds its lifetime into a Counters entry.
+/// Optional trace-range hooks. The core stays free of ROCm dependencies; the HIP layer installs
+/// roctx push/pop here (env TZ_ROCTX=1), so rocprofv3 --marker-trace shows MCTS phases and
+/// schedule ops as named ranges next to the kernels.
+struct TraceHooks {
+  void (*push)(const char *) = nullptr;
+  void (*pop)() = nullptr;
+};
+TraceHooks &trace_hooks();
+
+struct TraceRange {
+  bool on;
+  explicit TraceRange(const char *name) : on(trace_hooks().push != nullptr) {
+    if (on) trace_hooks().push(name);
+  }
+  ~TraceRange() {
+    if (on) trace_hooks().pop();
+  }
+  TraceRange(const TraceRange &) = delete;
+  TraceRange &operator=(const TraceRange &) = delete;
+};
+
 struct ScopedTimer {
   Counters &c;
   std::string key;
   double t0;
-  ScopedTimer(Counters &c_, std::string k) : c(c_), key(std::move(k)), t0(wtime()) {}
+  TraceRange range;
+  ScopedTimer(Counters &c_, std::string k)
+      : c(c_), key(std::move(k)), t0(wtime()), range(key.c_str()) {}
   ~ScopedTimer() { c.add(key, wtime() - t0); }
 };
 

@@ -4,6 +4,7 @@
 
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime_api.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -21,6 +22,17 @@ void hip_check(int err, const char *what, const char *file, int line) {
   }
 }
 
+void enable_roctx(bool on) {
+  TraceHooks &h = trace_hooks();
+  if (on) {
+    h.push = [](const char *n) { roctxRangePushA(n); };
+    h.pop = [] { roctxRangePop(); };
+  } else {
+    h.push = nullptr;
+    h.pop = nullptr;
+  }
+}
+
 int hip_device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -34,6 +46,7 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
     : mode_(opts.mode), unroll_(std::max(1, opts.graph_unroll)), spinSync_(opts.spin_sync),
       watchdogS_(opts.watchdog_s) {
   if (const char *v = std::getenv("TZ_SPIN_SYNC")) spinSync_ = std::atoi(v) != 0;
+  if (const char *v = std::getenv("TZ_ROCTX")) enable_roctx(std::atoi(v) != 0);
   TZ_CHECK(opts.n_streams >= 1, "need at least one stream");
   if (opts.device >= 0) TZ_HIP(hipSetDevice(opts.device));
   TZ_HIP(hipGetDevice(&device_));
@@ -307,9 +320,17 @@ void HipRuntime::run(int64_t n) {
     for (; i < n; ++i) TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExec_), origin));
     stream_sync(0);
   } else {
+    const bool traced = trace_hooks().push != nullptr;
     for (int64_t i = 0; i < n; ++i) {
       internalUsed_ = 0;
-      for (const auto &e : seq_.entries) e.op->run(*this);
+      for (const auto &e : seq_.entries) {
+        if (traced) {
+          TraceRange r(e.op->name().c_str());
+          e.op->run(*this);
+        } else {
+          e.op->run(*this);
+        }
+      }
     }
   }
   deadline_ = 0;

@@ -110,6 +110,8 @@ private:
   std::thread watchdog_;
 };
 
+/// route the core's trace ranges (MCTS phases, schedule ops in eager runs) to roctx
+void enable_roctx(bool on);
 /// hipGetDeviceCount (0 if no GPU / no driver)
 int hip_device_count();
 /// throw tz::Error if `err` (a hipError_t) is not success
