@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Fixed set of kernel launches for rocprofv3 counter collection (--pmc): the halo direct move
+(all 26 directions), fused pack / unpack, and the SpMV kernels, each a few times.
+
+  rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --output-format csv -d out -- python3 scripts/pmc_targets.py
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import tenzing_amd as tz  # noqa: E402
+from tenzing_amd.models import HaloConfig, build_halo  # noqa: E402
+
+
+def main():
+    torch.zeros(1, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    hd, _ = build_halo(HaloConfig(n=512, neighbors=26, order="qxyz", transport="direct"),
+                       tz.SelfCtrl(), device=0)
+    hc, _ = build_halo(HaloConfig(n=512, neighbors=26, order="qxyz", transport="copy"),
+                       tz.SelfCtrl(), device=0)
+    alld = list(range(hd.ndirs()))
+    for _ in range(3):
+        hd.direct_group(alld, st)
+        hc.pack_all(st)
+        hc.shift_all(st)
+        hc.unpack_all(st)
+    m = 150_000
+    rp, ci, val = tz._tz.random_band_matrix(m, m, 10 * m, 1)
+    rp_t = torch.tensor(rp, dtype=torch.int32, device="cuda")
+    ci_t = torch.tensor(ci, dtype=torch.int32, device="cuda")
+    v_t = torch.tensor(val, dtype=torch.float32, device="cuda")
+    x = torch.randn(m, device="cuda")
+    y = torch.zeros(m, device="cuda")
+    for _ in range(3):
+        for lanes in (8, -1):
+            tz._tz.kernels.csr_spmv(m, rp_t.data_ptr(), ci_t.data_ptr(), v_t.data_ptr(),
+                                    x.data_ptr(), y.data_ptr(), lanes, False, st)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
