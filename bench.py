@@ -48,13 +48,17 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--n", type=int, default=512, help="interior cells per axis per rank")
+    ap.add_argument("--cells", "--n", dest="n", type=int, default=512,
+                    help="interior cells per axis per rank (use --cells under torchrun: it "
+                         "swallows --n as an abbreviation of its own options)")
     ap.add_argument("--neighbors", type=int, default=26)
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--order", default="qxyz", choices=["xyzq", "qxyz"],
                     help="grid storage order (reference halo driver: xyzq)")
-    ap.add_argument("--transport", default="auto", choices=["auto", "direct", "copy", "rccl"],
-                    help="auto: direct (pack-free) moves on 1 rank, RCCL between ranks")
+    ap.add_argument("--transport", default="auto",
+                    choices=["auto", "direct", "copy", "rccl", "ipc"],
+                    help="auto: direct (pack-free) moves for self-neighbours, RCCL between "
+                         "ranks; ipc: pack-free puts into IPC-mapped peer grids")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=40)
@@ -126,7 +130,9 @@ def main() -> int:
     rt.prepare(best)
     rt.run(1)
     rt.device_sync()
+    ctrl.barrier()  # peers may still be writing into my ghosts (ipc puts) until they synced
     bad = ctrl.allreduce_sum([float(halo.check_grid())])[0]
+    bad += ctrl.allreduce_sum([float(halo.ipc_errors())])[0]
 
     def timed(m):
         rt.set_mode(m)
@@ -161,6 +167,9 @@ def main() -> int:
     t = t_graph if use_graph else t_eager
     ms = t / args.steps * 1e3
 
+    names = [o.name for o in best.ops()]
+    via = [t for t, key in (("direct", "he_direct_"), ("rccl", "he_shift_"), ("ipc", "he_put_"))
+           if any(n.startswith(key) for n in names)]
     if rank == 0:
         bytes_total = halo.exchange_bytes() * world
         out = {
@@ -181,7 +190,7 @@ def main() -> int:
                          f"{args.n}^3 x {cfg.nq}q ghost {cfg.ghost} per rank",
                 "global_batch": world,
                 "seq_len": args.n,
-                "parallelism": f"{world} ranks x {args.streams} HIP streams (RCCL/xGMI)"
+                "parallelism": f"{world} ranks x {args.streams} HIP streams over xGMI"
                                if world > 1 else f"1 rank x {args.streams} HIP streams",
                 "streams": args.streams,
                 "neighbors": args.neighbors,
@@ -205,6 +214,8 @@ def main() -> int:
             "verified_bad_cells": int(bad),
             "setup_s": setup_s,
             "transport": halo.transport(),
+            "schedule_transport": "+".join(via),
+            "ipc_mode": halo.ipc_mode() or None,
         }
         print(json.dumps(out), flush=True)
     return 0 if bad == 0 else 3

@@ -616,6 +616,12 @@ PYBIND11_MODULE(_tz, m) {
       .def("uses_rccl", &HaloExchange::uses_rccl)
       .def("uses_direct", &HaloExchange::uses_direct)
       .def("is_direct", &HaloExchange::is_direct)
+      .def("is_ipc", &HaloExchange::is_ipc)
+      .def("uses_ipc", &HaloExchange::uses_ipc)
+      .def("ipc_mode", &HaloExchange::ipc_mode)
+      .def("put_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.put_group(d, P(s)); })
+      .def("wait_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.wait_group(d, P(s)); })
+      .def("ipc_errors", &HaloExchange::ipc_errors, py::call_guard<py::gil_scoped_release>())
       .def("pipelined_dirs", &HaloExchange::pipelined_dirs)
       .def("transport", &HaloExchange::transport);
 

@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace tz {
 namespace kern {
@@ -219,6 +220,84 @@ __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b) {
   else move_body<1, U, NT>(d, tid, nth);
 }
 
+struct DevSignal {
+  unsigned int *done;
+  unsigned long long *flag[kMaxBoxes];
+};
+
+__device__ __forceinline__ void signal_box_done(const DevSignal &sig, int box, uint32_t nb);
+
+// peer put: the move, then the box's last block publishes it with one system-scope signal
+template <int U, bool NT>
+__global__ __launch_bounds__(kThreads) void box_move_signal_k(DevBatch b, DevSignal sig) {
+  int box = 0;
+  while (box + 1 < b.n && blockIdx.x >= b.block_start[box + 1]) ++box;
+  const DevDesc &d = b.d[box];
+  const uint32_t nb = b.block_start[box + 1] - b.block_start[box];
+  const uint32_t tid = (blockIdx.x - b.block_start[box]) * kThreads + threadIdx.x;
+  const uint32_t nth = nb * kThreads;
+  if (d.vec == 2) move_body<2, U, NT>(d, tid, nth);
+  else move_body<1, U, NT>(d, tid, nth);
+  signal_box_done(sig, box, nb);
+}
+
+// the box's last block publishes every block's (peer) stores with one system-scope signal
+__device__ __forceinline__ void signal_box_done(const DevSignal &sig, int box, uint32_t nb) {
+  __threadfence_system(); // this thread's peer stores are visible system-wide ...
+  __syncthreads();        // ... for every thread of the block before it is counted
+  if (threadIdx.x == 0) {
+    const unsigned int prev = atomicAdd(&sig.done[box], 1u);
+    if (prev == nb - 1) { // last block of this box: every block's stores are fenced
+      sig.done[box] = 0;  // ready for the next iteration (kernel boundary orders it)
+      __threadfence_system();
+      __hip_atomic_fetch_add(sig.flag[box], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// IPC put into a neighbour's receive buffer: pack, then signal
+template <int U, bool NT>
+__global__ __launch_bounds__(kThreads) void box_pack_signal_k(double *__restrict__ grid, DevBatch b,
+                                                              DevSignal sig) {
+  int box = 0;
+  while (box + 1 < b.n && blockIdx.x >= b.block_start[box + 1]) ++box;
+  const DevDesc &d = b.d[box];
+  const uint32_t nb = b.block_start[box + 1] - b.block_start[box];
+  const uint32_t tid = (blockIdx.x - b.block_start[box]) * kThreads + threadIdx.x;
+  const uint32_t nth = nb * kThreads;
+  if (d.vec == 2) box_body<2, false, U, NT>(grid, d, tid, nth);
+  else box_body<1, false, U, NT>(grid, d, tid, nth);
+  signal_box_done(sig, box, nb);
+}
+
+constexpr int kMaxWaitSlots = 64;
+struct WaitArgs {
+  const unsigned long long *arrive;
+  unsigned long long *expected;
+  int *err;
+  long long timeout_ticks;
+  int n;
+  int slot[kMaxWaitSlots];
+};
+
+__global__ __launch_bounds__(64) void ipc_wait_k(WaitArgs a) {
+  const int i = threadIdx.x;
+  if (i < a.n) {
+    const int s = a.slot[i];
+    const unsigned long long want = a.expected[s] + 1;
+    a.expected[s] = want;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(&a.arrive[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > a.timeout_ticks) {
+        atomicOr(a.err, 1);
+        break;
+      }
+    }
+  }
+  __threadfence_system();
+}
+
 // host dispatch over (unpack, unroll, nt)
 template <bool UNPACK, int U, bool NT>
 void launch_one(dim3 g, hipStream_t s, double *grid, const DevDesc &d) {
@@ -370,12 +449,96 @@ void box_copy_many(double *grid, const BoxDesc *boxes, int n, bool unpack, void 
   TZ_HIP_LAUNCH_CHECK();
 }
 
+namespace {
+// the device batch of a move launch (shared by the plain and the signalling variant);
+// `keep` maps batch entries back to input boxes
+DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vector<int> &keep);
+} // namespace
+
 void box_move_many(const MoveDesc *moves, int n, void *stream) {
   if (n <= 0) return;
   if (n > kMaxBoxes) throw std::runtime_error("box_move_many: too many boxes");
+  uint32_t total = 0;
+  std::vector<int> keep;
+  const DevBatch b = make_move_batch(moves, n, total, keep);
+  if (b.n == 0) return;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 g(total);
+  if (box_tuning().nt_move) hipLaunchKernelGGL((box_move_many_k<4, true>), g, dim3(kThreads), 0, s, b);
+  else hipLaunchKernelGGL((box_move_many_k<4, false>), g, dim3(kThreads), 0, s, b);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void box_move_many_signal(const MoveDesc *moves, int n, const MoveSignal &sig, void *stream) {
+  if (n <= 0) return;
+  if (n > kMaxBoxes) throw std::runtime_error("box_move_many_signal: too many boxes");
+  if (!sig.done) throw std::runtime_error("box_move_many_signal: null block counters");
+  uint32_t total = 0;
+  std::vector<int> keep;
+  const DevBatch b = make_move_batch(moves, n, total, keep);
+  if (b.n != n) throw std::runtime_error("box_move_many_signal: empty box (nothing to signal)");
+  DevSignal ds{};
+  ds.done = sig.done;
+  for (int i = 0; i < n; ++i) {
+    if (!sig.flag[keep[i]]) throw std::runtime_error("box_move_many_signal: null flag");
+    ds.flag[i] = sig.flag[keep[i]];
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 g(total);
+  if (box_tuning().nt_move) hipLaunchKernelGGL((box_move_signal_k<4, true>), g, dim3(kThreads), 0, s, b, ds);
+  else hipLaunchKernelGGL((box_move_signal_k<4, false>), g, dim3(kThreads), 0, s, b, ds);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void box_pack_many_signal(double *grid, const BoxDesc *boxes, int n, const MoveSignal &sig,
+                          void *stream) {
+  if (n <= 0) return;
+  if (n > kMaxBoxes) throw std::runtime_error("box_pack_many_signal: too many boxes");
+  if (!grid || !sig.done) throw std::runtime_error("box_pack_many_signal: null grid or counters");
+  DevBatch b{};
+  DevSignal ds{};
+  ds.done = sig.done;
+  uint32_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!boxes[i].buf || !sig.flag[i]) throw std::runtime_error("box_pack_many_signal: null buffer/flag");
+    DevDesc d = make_dev(boxes[i]);
+    if (d.items == 0) throw std::runtime_error("box_pack_many_signal: empty box (nothing to signal)");
+    b.d[b.n] = d;
+    b.block_start[b.n] = total;
+    ds.flag[b.n] = sig.flag[i];
+    total += blocks_for(d);
+    ++b.n;
+  }
+  b.block_start[b.n] = total;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (box_tuning().nt_pack)
+    hipLaunchKernelGGL((box_pack_signal_k<4, true>), dim3(total), dim3(kThreads), 0, s, grid, b, ds);
+  else
+    hipLaunchKernelGGL((box_pack_signal_k<4, false>), dim3(total), dim3(kThreads), 0, s, grid, b, ds);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void ipc_wait(const unsigned long long *arrive, unsigned long long *expected, const int *slots,
+              int n, int *err, double timeout_s, void *stream) {
+  if (n <= 0) return;
+  if (n > kMaxWaitSlots) throw std::runtime_error("ipc_wait: too many slots");
+  if (!arrive || !expected || !err) throw std::runtime_error("ipc_wait: null pointer");
+  WaitArgs a{};
+  a.arrive = arrive;
+  a.expected = expected;
+  a.err = err;
+  a.timeout_ticks = (long long)(timeout_s * 1.0e8); // wall_clock64 runs at 100 MHz
+  a.n = n;
+  for (int i = 0; i < n; ++i) a.slot[i] = slots[i];
+  hipLaunchKernelGGL(ipc_wait_k, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+namespace {
+DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vector<int> &keep) {
   DevBatch b{};
   b.n = 0;
-  uint32_t total = 0;
+  total = 0;
   for (int i = 0; i < n; ++i) {
     const MoveDesc &m = moves[i];
     if (!m.src || !m.dst) throw std::runtime_error("box_move_many: null array");
@@ -404,17 +567,13 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
     b.d[b.n] = d;
     b.block_start[b.n] = total;
     total += blocks_for(d);
+    keep.push_back(i);
     ++b.n;
   }
-  if (b.n == 0) return;
   b.block_start[b.n] = total;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const BoxTuning &t = box_tuning();
-  const dim3 g(total);
-  if (t.nt_move) hipLaunchKernelGGL((box_move_many_k<4, true>), g, dim3(kThreads), 0, s, b);
-  else hipLaunchKernelGGL((box_move_many_k<4, false>), g, dim3(kThreads), 0, s, b);
-  TZ_HIP_LAUNCH_CHECK();
+  return b;
 }
+} // namespace
 
 } // namespace kern
 } // namespace tz

@@ -48,6 +48,26 @@ struct MoveDesc {
 /// up to kMaxBoxes moves in ONE launch
 void box_move_many(const MoveDesc *d, int n, void *stream);
 
+/// Completion signal of a move whose destination is another rank's memory (IPC peer put):
+/// when the last block of box i has stored its part, it makes every store of the box visible
+/// at system scope and adds 1 to `flag[i]` (a counter in the receiver's uncached memory).
+/// `done` holds one zero-initialized block counter per box (self-resetting).
+struct MoveSignal {
+  unsigned int *done = nullptr;
+  unsigned long long *flag[kMaxBoxes] = {};
+};
+void box_move_many_signal(const MoveDesc *d, int n, const MoveSignal &sig, void *stream);
+/// pack boxes of `grid` into their (possibly peer-mapped) dense buffers and signal each box's
+/// completion like box_move_many_signal (IPC put into a neighbour's receive buffer)
+void box_pack_many_signal(double *grid, const BoxDesc *d, int n, const MoveSignal &sig,
+                          void *stream);
+
+/// Receiver side of IPC puts: for each of the `n` slots, increment the local expected count and
+/// spin (system-scope acquire loads, s_sleep back-off) until `arrive[slot]` reaches it. A wait
+/// longer than `timeout_s` sets *err = 1 and gives up, so a lost peer cannot hang the GPU.
+void ipc_wait(const unsigned long long *arrive, unsigned long long *expected, const int *slots,
+              int n, int *err, double timeout_s, void *stream);
+
 /// pack (grid -> buf) or unpack (buf -> grid) one box
 void box_copy(double *grid, const BoxDesc &d, bool unpack, void *stream);
 /// pack/unpack up to kMaxBoxes boxes in ONE launch (fused multi-face halo pack/unpack)

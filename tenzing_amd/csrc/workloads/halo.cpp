@@ -8,6 +8,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 namespace tz {
 
@@ -101,18 +103,51 @@ private:
   int i_;
 };
 
+/// ipc transport: pack-free put of one direction into the neighbour's grid + arrival signal
+class HaloPut : public GpuOp {
+public:
+  HaloPut(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_put_" + h_->dir(i_).name(); }
+  std::string kind() const override { return "HaloPut"; }
+  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
+  // peer stores over one xGMI link (~60 GB/s effective)
+  double cost_us() const override { return 4.0 + bytes() / 2.0 / 6.0e4; }
+  void launch(void *s, Executor &) const override { h_->put_group({i_}, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+/// ipc transport: device-side wait for the neighbours' puts into my ghosts
+class HaloWait : public GpuOp {
+public:
+  HaloWait(std::shared_ptr<const HaloExchange> h, std::vector<int> dirs, std::string tag)
+      : h_(std::move(h)), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
+  std::string name() const override { return "he_wait_" + tag_; }
+  std::string kind() const override { return "HaloWait"; }
+  double cost_us() const override { return 3.0; }
+  void launch(void *s, Executor &) const override { h_->wait_group(dirs_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  std::vector<int> dirs_;
+  std::string tag_;
+};
+
 /// one op for a whole group of directions (single kernel launch / single RCCL group)
 class HaloStageGroup : public GpuOp {
 public:
-  enum Stage { Pack, Shift, Unpack, Direct };
+  enum Stage { Pack, Shift, Unpack, Direct, Put };
   HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag)
       : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
   std::string name() const override {
-    static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_"};
+    static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_", "he_put_"};
     return pre[st_] + tag_;
   }
   std::string kind() const override {
-    static const char *k[] = {"HaloPackGroup", "HaloShiftGroup", "HaloUnpackGroup", "HaloDirectGroup"};
+    static const char *k[] = {"HaloPackGroup", "HaloShiftGroup", "HaloUnpackGroup",
+                              "HaloDirectGroup", "HaloPutGroup"};
     return k[st_];
   }
   double bytes() const override {
@@ -128,7 +163,8 @@ public:
     if (st_ == Pack) h_->pack_group(dirs_, s);
     else if (st_ == Shift) h_->shift_group(dirs_, s);
     else if (st_ == Unpack) h_->unpack_group(dirs_, s);
-    else h_->direct_group(dirs_, s);
+    else if (st_ == Direct) h_->direct_group(dirs_, s);
+    else h_->put_group(dirs_, s);
   }
 
 private:
@@ -220,21 +256,32 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
     gridElems_ = size_t(sz_ * Z);
   }
   const std::string &t = a_.transport;
-  TZ_CHECK(t == "auto" || t == "direct" || t == "copy" || t == "rccl",
+  TZ_CHECK(t == "auto" || t == "direct" || t == "copy" || t == "rccl" || t == "ipc",
            "unknown transport " << t);
   if (t == "copy" || t == "direct") {
     for (int n : nbr_) TZ_CHECK(n == a_.rank, t << " transport needs self-neighbours (1 rank)");
   }
-  // per direction: direct move (self-neighbour under auto/direct) or pack -> transfer -> unpack
-  for (int i = 0; i < ndirs(); ++i)
-    direct_.push_back((t == "direct" || t == "auto") && nbr_[i] == a_.rank);
+  // per direction: direct move (self-neighbour under auto/direct/ipc), IPC put (remote under
+  // ipc) or pack -> transfer -> unpack
+  for (int i = 0; i < ndirs(); ++i) {
+    const bool self = nbr_[i] == a_.rank;
+    direct_.push_back((t == "direct" || t == "auto" || t == "ipc") && self);
+    ipc_.push_back((t == "ipc" || t == "auto") && !self);
+    pipe_.push_back(!direct_[i] && (t == "rccl" || t == "copy" || t == "auto"));
+  }
   for (int i = 0; i < ndirs(); ++i) {
     if (direct_[i]) useDirect_ = true;
-    else if (t != "copy") useRccl_ = true;
+    if (ipc_[i]) useIpc_ = true;
+    if (pipe_[i] && t != "copy") useRccl_ = true;
   }
+  ipcGrid_ = gridElems_ * sizeof(double) < (size_t(2) << 30);
+  if (const char *v = std::getenv("TZ_IPC_GRID")) ipcGrid_ = std::atoi(v) != 0;
 }
 
-HaloExchange::~HaloExchange() = default;
+HaloExchange::~HaloExchange() {
+  for (void *p : opened_) hipIpcCloseMemHandle(p);
+  if (flags_) hipFree(flags_);
+}
 
 int HaloExchange::coord_to_rank(int x, int y, int z) const {
   auto w = [](int v, int n) { return ((v % n) + n) % n; };
@@ -338,8 +385,23 @@ void HaloExchange::setup(Ctrl *ctrl) {
   recv_.resize(ndirs());
   for (int i = 0; i < ndirs(); ++i) {
     if (direct_[i]) continue;
-    send_[i] = DeviceBuffer(box_elems(i) * sizeof(double));
-    recv_[i] = DeviceBuffer(box_elems(opp_[i]) * sizeof(double));
+    if (pipe_[i]) send_[i] = DeviceBuffer(box_elems(i) * sizeof(double));
+    // ipc "buffers" mode needs the receive buffer too (the peer packs straight into it)
+    if (pipe_[i] || (ipc_[i] && !ipcGrid_))
+      recv_[i] = DeviceBuffer(box_elems(opp_[i]) * sizeof(double));
+  }
+  if (useIpc_) {
+    // collective agreement: if any rank cannot map its peers, nobody uses IPC puts (with a
+    // forced "ipc" transport that is an error; with "auto" RCCL remains)
+    const std::string why = setup_ipc(ctrl);
+    // agreement (and the barrier before anyone puts: every rank mapped its peers)
+    double failed = why.empty() ? 0.0 : 1.0;
+    ctrl->allreduce_max(&failed, 1);
+    ipcReady_ = failed == 0.0;
+    if (!ipcReady_) {
+      TZ_LOG(Warn, "ipc transport unavailable" << (why.empty() ? " on another rank" : ": " + why));
+      TZ_CHECK(a_.transport != "ipc", "ipc transport requested but unavailable: " << why);
+    }
   }
   count_ = DeviceBuffer(sizeof(unsigned long long));
   if (useRccl_) {
@@ -352,6 +414,136 @@ void HaloExchange::setup(Ctrl *ctrl) {
   }
   init_grid();
   TZ_HIP(hipDeviceSynchronize());
+}
+
+std::string HaloExchange::setup_ipc(Ctrl *ctrl) {
+  // Collective: every rank makes the same control-plane calls (one allgather) whatever fails
+  // locally, and reports failure as a string, so a rank that cannot export or map never leaves
+  // the others blocked in a mismatched collective.
+  TZ_CHECK(ctrl && ctrl->size() == a_.size, "ipc transport needs a control plane of size " << a_.size);
+  if (const char *v = std::getenv("TZ_IPC_TIMEOUT")) ipcTimeoutS_ = std::atof(v);
+  const size_t nd = size_t(ndirs());
+  const size_t H = sizeof(hipIpcMemHandle_t);
+  std::string mine, err;
+  try {
+    // arrival counters live in uncached memory: a remote GPU's system-scope atomics land in
+    // HBM and the local spin loads (system scope) see them without stale cache lines
+    TZ_HIP(hipExtMallocWithFlags(&flags_, std::max<size_t>(nd * 8, 64), hipDeviceMallocUncached));
+    TZ_HIP(hipMemset(flags_, 0, nd * 8));
+    expected_ = DeviceBuffer(nd * 8);
+    TZ_HIP(hipMemset(expected_.get(), 0, nd * 8));
+    done_ = DeviceBuffer(nd * kern::kMaxBoxes * sizeof(unsigned int));
+    TZ_HIP(hipMemset(done_.get(), 0, done_.bytes()));
+    err_ = DeviceBuffer(sizeof(int));
+    TZ_HIP(hipMemset(err_.get(), 0, sizeof(int)));
+    TZ_HIP(hipDeviceSynchronize());
+    // exported: [flags][grid] ("grid" mode) or [flags][recv buffer of every direction]
+    auto handle_of = [&](void *p) {
+      hipIpcMemHandle_t h;
+      std::memset(&h, 0, sizeof(h));
+      if (p) TZ_HIP(hipIpcGetMemHandle(&h, p));
+      return std::string(reinterpret_cast<const char *>(&h), H);
+    };
+    mine = handle_of(flags_);
+    if (ipcGrid_) {
+      mine += handle_of(grid());
+    } else {
+      for (int i = 0; i < ndirs(); ++i) mine += handle_of(ipc_[i] ? recv_[i].get() : nullptr);
+    }
+    TZ_LOG(Info, "ipc: exported " << (ipcGrid_ ? "grid" : "receive buffers") << " and flags");
+  } catch (const std::exception &e) {
+    err = std::string("export: ") + e.what();
+    mine.clear();
+  }
+  const std::vector<std::string> all = ctrl->allgather(mine);
+  if (!err.empty()) return err;
+  try {
+    TZ_CHECK(int(all.size()) == a_.size, "allgather returned " << all.size() << " entries");
+    auto open = [&](const std::string &blob, size_t k) {
+      TZ_CHECK(blob.size() >= (k + 1) * H, "a peer exported no IPC handles");
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, blob.data() + k * H, H);
+      void *p = nullptr;
+      TZ_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      opened_.push_back(p);
+      return p;
+    };
+    peerGrid_.assign(size_t(a_.size), nullptr);
+    peerFlags_.assign(size_t(a_.size), nullptr);
+    peerRecv_.assign(nd, nullptr);
+    for (int i = 0; i < ndirs(); ++i) {
+      if (!ipc_[i]) continue;
+      const int q = nbr_[i];
+      const std::string &blob = all[size_t(q)];
+      if (!peerFlags_[size_t(q)]) {
+        TZ_LOG(Info, "ipc: mapping rank " << q);
+        peerFlags_[size_t(q)] = open(blob, 0);
+        if (ipcGrid_) peerGrid_[size_t(q)] = open(blob, 1);
+      }
+      // my slab facing d_i fills q's ghost side -d_i, staged in q's recv buffer of that side
+      if (!ipcGrid_) peerRecv_[size_t(i)] = open(blob, 1 + size_t(opp_[i]));
+    }
+  } catch (const std::exception &e) {
+    return std::string("map: ") + e.what();
+  }
+  return "";
+}
+
+void HaloExchange::put_group(const std::vector<int> &dirs, void *stream) const {
+  TZ_CHECK(ready() && ipcReady_, "ipc transport not set up");
+  TZ_CHECK(!dirs.empty() && dirs.size() <= size_t(kern::kMaxBoxes), "bad put group");
+  std::vector<kern::MoveDesc> ms;
+  std::vector<kern::BoxDesc> bs;
+  kern::MoveSignal sig;
+  // block counters: one slot range per group, keyed by its first direction (groups of one
+  // schedule are disjoint, so concurrently running puts never share counters)
+  sig.done = done_.as<unsigned int>() + size_t(dirs.front()) * kern::kMaxBoxes;
+  for (size_t k = 0; k < dirs.size(); ++k) {
+    const int i = dirs[k];
+    TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i], "direction " << i << " is not an ipc put");
+    const int q = nbr_[i];
+    // the receiver counts arrivals of direction i in its slot i
+    sig.flag[k] = static_cast<unsigned long long *>(peerFlags_[size_t(q)]) + i;
+    if (!ipcGrid_) {
+      kern::BoxDesc b = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
+      b.buf = static_cast<double *>(peerRecv_[size_t(i)]);
+      bs.push_back(b);
+      continue;
+    }
+    const kern::BoxDesc s = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
+    const kern::BoxDesc d = make_box(a_, dirs_[opp_[i]], true, xoff_, sy_, sz_, sq_);
+    kern::MoveDesc m;
+    m.src = grid();
+    m.dst = static_cast<double *>(peerGrid_[size_t(q)]);
+    m.src_off = s.grid_off;
+    m.dst_off = d.grid_off;
+    m.s1 = s.s1;
+    m.s2 = s.s2;
+    m.s3 = s.s3;
+    m.len = s.len;
+    m.n1 = s.n1;
+    m.n2 = s.n2;
+    m.n3 = s.n3;
+    ms.push_back(m);
+  }
+  if (ipcGrid_) kern::box_move_many_signal(ms.data(), int(ms.size()), sig, stream);
+  else kern::box_pack_many_signal(grid(), bs.data(), int(bs.size()), sig, stream);
+}
+
+void HaloExchange::wait_group(const std::vector<int> &dirs, void *stream) const {
+  TZ_CHECK(ready() && ipcReady_, "ipc transport not set up");
+  for (int i : dirs) TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i], "direction " << i << " is not an ipc put");
+  kern::ipc_wait(static_cast<const unsigned long long *>(flags_), expected_.as<unsigned long long>(),
+                 dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream);
+}
+
+int HaloExchange::ipc_errors() {
+  if (!useIpc_ || !err_.get()) return 0;
+  int e = 0;
+  TZ_HIP(hipDeviceSynchronize());
+  err_.download(&e, sizeof(e));
+  TZ_HIP(hipMemset(err_.get(), 0, sizeof(int)));
+  return e;
 }
 
 void HaloExchange::init_grid(void *stream) {
@@ -376,6 +568,7 @@ void HaloExchange::check_pipelined(int i) const {
   TZ_CHECK(i >= 0 && i < ndirs(), "direction " << i << " out of range");
   TZ_CHECK(!direct_[i], "direction " << dirs_[i].name()
                                      << " uses the direct transport (no pack/transfer/unpack)");
+  TZ_CHECK(pipe_[i] || ipc_[i], "direction " << dirs_[i].name() << " has no staging buffers");
   TZ_CHECK(ready(), "halo not set up");
 }
 
@@ -501,11 +694,12 @@ void HaloExchange::pack_all(void *stream) const { pack_group(pipelined_dirs(), s
 void HaloExchange::unpack_all(void *stream) const { unpack_group(pipelined_dirs(), stream); }
 void HaloExchange::shift_all(void *stream) const { shift_group(pipelined_dirs(), stream); }
 
-void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs) {
+void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, bool viaIpc) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   for (int i : dirs) {
-    if (direct_[i]) {
-      auto d = std::make_shared<HaloDirect>(self, i);
+    if (direct_[i] || viaIpc) {
+      OpPtr d = direct_[i] ? OpPtr(std::make_shared<HaloDirect>(self, i))
+                           : OpPtr(std::make_shared<HaloPut>(self, i));
       g.start_then(d);
       g.then_finish(d);
       continue;
@@ -520,7 +714,8 @@ void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs) {
   }
 }
 
-void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag) {
+void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag,
+                             bool viaIpc) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   std::vector<int> local, remote;
   for (int i : dirs) (direct_[i] ? local : remote).push_back(i);
@@ -531,6 +726,12 @@ void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::
     g.then_finish(d);
   }
   if (remote.empty()) return;
+  if (viaIpc) {
+    auto d = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Put, remote, tag);
+    g.start_then(d);
+    g.then_finish(d);
+    return;
+  }
   auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, remote, tag);
   auto s = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Shift, remote, tag);
   auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, remote, tag);
@@ -540,10 +741,11 @@ void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::
   g.then_finish(u);
 }
 
-void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs) {
+void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, bool viaIpc,
+                                 const std::string &pre) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   const std::string &f = a_.fuse;
-  const bool direct = direct_[dirs.front()];
+  const bool singleStage = direct_[dirs.front()] || viaIpc;
   auto subset = [&](const std::vector<int> &v) {
     std::vector<int> r;
     for (int i : v)
@@ -551,14 +753,12 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs) {
     return r;
   };
   if (f == "none") {
-    add_chains(g, dirs);
-  } else if (f == "all" || (f == "pack" && direct)) {
-    // (direct transfers have no pack stage: "pack" degenerates to one fused move)
-    add_fused(g, dirs, "all");
+    add_chains(g, dirs, viaIpc);
+  } else if (f == "all" || (f == "pack" && singleStage)) {
+    // (direct moves and puts have no pack stage: "pack" degenerates to one fused op)
+    add_fused(g, dirs, "all", viaIpc);
   } else if (f == "pack") {
     // fused pack / unpack kernels, per-direction transfers
-    std::vector<int> unp;
-    for (int i : dirs) unp.push_back(opp_[i]);
     auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, "all");
     auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, dirs, "all");
     g.start_then(p);
@@ -578,25 +778,25 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs) {
              {"faces", subset(group_dirs(1))}, {"small", subset(group_dirs(0))}})
       if (!gr.second.empty()) groups.push_back(gr);
     if (f == "groups") {
-      for (auto &gr : groups) add_fused(g, gr.second, gr.first);
+      for (auto &gr : groups) add_fused(g, gr.second, gr.first, viaIpc);
       return;
     }
     // per group: split chains vs one fused chain
     auto grouped = std::make_shared<Graph>();
     for (auto &gr : groups) {
       auto split = std::make_shared<Graph>();
-      add_chains(*split, gr.second);
+      add_chains(*split, gr.second, viaIpc);
       auto fused = std::make_shared<Graph>();
-      add_fused(*fused, gr.second, gr.first);
+      add_fused(*fused, gr.second, gr.first, viaIpc);
       std::vector<OpPtr> alts = {
-          std::make_shared<StaticCompoundOp>("he_" + gr.first + "_split", split),
-          std::make_shared<StaticCompoundOp>("he_" + gr.first + "_fused", fused)};
-      auto choice = std::make_shared<StaticChoiceOp>("he_" + gr.first, alts);
+          std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_split", split),
+          std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_fused", fused)};
+      auto choice = std::make_shared<StaticChoiceOp>(pre + "he_" + gr.first, alts);
       grouped->start_then(choice);
       grouped->then_finish(choice);
     }
     if (groups.size() == 1) {
-      auto c = std::make_shared<StaticCompoundOp>("he_grouped", grouped);
+      auto c = std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped);
       g.start_then(c);
       g.then_finish(c);
       return;
@@ -604,10 +804,10 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs) {
     // two groups: additionally one chain for every direction (a single launch per stage
     // avoids the two groups' kernels competing for CUs)
     auto all = std::make_shared<Graph>();
-    add_fused(*all, dirs, "all");
-    std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>("he_grouped", grouped),
-                              std::make_shared<StaticCompoundOp>("he_allfused", all)};
-    auto choice = std::make_shared<StaticChoiceOp>("he_exchange", top);
+    add_fused(*all, dirs, "all", viaIpc);
+    std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped),
+                              std::make_shared<StaticCompoundOp>(pre + "he_allfused", all)};
+    auto choice = std::make_shared<StaticChoiceOp>(pre + "he_exchange", top);
     g.start_then(choice);
     g.then_finish(choice);
   } else {
@@ -615,19 +815,60 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs) {
   }
 }
 
+void HaloExchange::add_ipc_part(Graph &g, const std::vector<int> &remote) {
+  // puts never wait for anything remote, so each rank's puts all complete; the arrival wait
+  // runs after them (one spinning kernel per rank, never ahead of its own puts)
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  auto puts = std::make_shared<Graph>();
+  add_structure(*puts, remote, true, "ipc_");
+  auto c = std::make_shared<StaticCompoundOp>("he_puts", puts);
+  auto w = std::make_shared<HaloWait>(self, remote, "remote");
+  g.start_then(c);
+  g.then(c, w);
+  if (ipcGrid_) {
+    g.then_finish(w);
+  } else {
+    // "buffers" mode: my receive buffers are complete after the wait; unpack them
+    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, remote, "remote");
+    g.then(w, u);
+    g.then_finish(u);
+  }
+}
+
 void HaloExchange::add_to_graph(Graph &g) {
-  // self-neighbour directions moved directly and remote directions through RCCL are
-  // independent: the local moves form their own op(s), the remote chains get the fuse
-  // structure (and the search overlaps the two)
+  // self-neighbour directions are moved directly and remote directions go through RCCL or IPC
+  // puts; the local moves form their own op(s), the remote directions get the fuse structure
+  // (and the search overlaps the two). With both transports available ("auto" on several
+  // ranks) the transport itself is a ChoiceOp the search decides.
   std::vector<int> local, remote;
   for (int i = 0; i < ndirs(); ++i) (direct_[i] ? local : remote).push_back(i);
-  if (local.empty() || remote.empty()) {
-    add_structure(g, all_dirs());
+  if (remote.empty()) {
+    add_structure(g, all_dirs(), false, "");
     return;
   }
-  if (a_.fuse == "none") add_chains(g, local);
-  else add_fused(g, local, "self");
-  add_structure(g, remote);
+  if (!local.empty()) {
+    if (a_.fuse == "none") add_chains(g, local, false);
+    else add_fused(g, local, "self", false);
+  }
+  // graph-only builds (no setup) assume IPC can be mapped
+  const bool ipc = useIpc_ && (ipcReady_ || !ready());
+  const bool pipe = useRccl_ || a_.transport == "copy";
+  TZ_CHECK(ipc || pipe, "no transport available for the remote directions");
+  if (ipc && pipe) {
+    auto viaRccl = std::make_shared<Graph>();
+    add_structure(*viaRccl, remote, false, "");
+    auto viaIpc = std::make_shared<Graph>();
+    add_ipc_part(*viaIpc, remote);
+    std::vector<OpPtr> alts = {std::make_shared<StaticCompoundOp>("he_via_rccl", viaRccl),
+                               std::make_shared<StaticCompoundOp>("he_via_ipc", viaIpc)};
+    auto c = std::make_shared<StaticChoiceOp>("he_remote", alts);
+    g.start_then(c);
+    g.then_finish(c);
+  } else if (ipc) {
+    add_ipc_part(g, remote);
+  } else {
+    add_structure(g, remote, false, "");
+  }
 }
 
 } // namespace tz

@@ -99,7 +99,10 @@ struct HaloArgs {
   std::string order = "xyzq";     // "xyzq" (x fastest, q slowest) or "qxyz"
   // "rccl" (pack -> grouped RCCL send/recv -> unpack), "copy" (pack -> device copy -> unpack,
   // self-neighbours only), "direct" (pack-free box moves straight into the neighbour's ghost
-  // region; self-neighbours only), "auto" (direct on one rank, rccl otherwise)
+  // region; self-neighbours only), "ipc" (self-neighbours direct; remote directions are
+  // pack-free puts into the peer's IPC-mapped grid plus a device-side arrival wait — also the
+  // loopback backend for several ranks on one GPU), "auto" (direct on one rank, direct + rccl
+  // otherwise)
   std::string transport = "auto";
   // "choice": per group (faces / edges+corners) the search chooses per-direction or fused ops;
   // "none": per-direction ops; "groups": fused per group; "pack": fused pack+unpack with
@@ -168,31 +171,64 @@ public:
   std::vector<int> group_dirs(int k) const;
   bool uses_rccl() const { return useRccl_; }
   bool uses_direct() const { return useDirect_; }
+  bool uses_ipc() const { return useIpc_; }
   /// direction i is moved directly (self-neighbour) rather than packed and transferred
   bool is_direct(int i) const { return direct_[i]; }
-  /// "rccl", "copy", "direct" or "direct+rccl" (self-neighbour directions direct, the rest RCCL)
+  /// direction i is a pack-free put into the neighbour's IPC-mapped grid
+  bool is_ipc(int i) const { return ipc_[i]; }
+  /// available transports joined by "+": "direct" (self-neighbour moves), "rccl", "ipc"
+  /// (when both rccl and ipc are listed the search chooses), or "copy"
   std::string transport() const {
-    if (useDirect_) return useRccl_ ? "direct+rccl" : "direct";
-    return useRccl_ ? "rccl" : "copy";
+    std::string t;
+    auto add = [&](const char *x) { t += (t.empty() ? "" : "+") + std::string(x); };
+    if (useDirect_) add("direct");
+    if (useRccl_) add("rccl");
+    if (useIpc_ && (ipcReady_ || !ready())) add("ipc");
+    return t.empty() ? "copy" : t;
   }
+  /// ipc transport: put my slabs facing `dirs` into the neighbours' ghost regions and signal
+  /// their arrival counters (one launch)
+  void put_group(const std::vector<int> &dirs, void *stream) const;
+  /// ipc transport: wait until the ghosts filled by the neighbours' puts of `dirs` arrived
+  void wait_group(const std::vector<int> &dirs, void *stream) const;
+  /// ipc transport: number of arrival waits that timed out (0 = healthy); resets the flag
+  int ipc_errors();
+  /// ipc transport: "grid" (puts land directly in the peer's ghost cells) or "buffers" (puts
+  /// fill the peer's receive buffers, which it unpacks after the arrival wait). Grids of 2 GiB
+  /// or more use "buffers": the dmabuf IPC path of this platform cannot map allocations that
+  /// large (measured, scripts/ipc_probe.py); env TZ_IPC_GRID=0/1 forces a mode.
+  std::string ipc_mode() const { return useIpc_ ? (ipcGrid_ ? "grid" : "buffers") : ""; }
   /// direct transport: move the interior slab facing each direction of `dirs` straight into
   /// the neighbour's ghost region on the opposite side (one launch)
   void direct_group(const std::vector<int> &dirs, void *stream) const;
   void direct(int i, void *stream) const { direct_group({i}, stream); }
 
 private:
-  void add_chains(Graph &g, const std::vector<int> &dirs);
-  void add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag);
-  void add_structure(Graph &g, const std::vector<int> &dirs); // fuse mode over `dirs`
+  // graph builders; remote directions use IPC puts when `viaIpc`, else pack/transfer/unpack
+  void add_chains(Graph &g, const std::vector<int> &dirs, bool viaIpc);
+  void add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag, bool viaIpc);
+  void add_structure(Graph &g, const std::vector<int> &dirs, bool viaIpc,
+                     const std::string &pre); // fuse mode over `dirs`
+  void add_ipc_part(Graph &g, const std::vector<int> &remote);
   void check_pipelined(int i) const;
+  std::string setup_ipc(Ctrl *ctrl); // "" on success, else why IPC cannot be used
   HaloArgs a_;
   std::vector<Dir> dirs_;
   std::vector<int> opp_, nbr_;
   int cx_ = 0, cy_ = 0, cz_ = 0;
   int64_t xoff_ = 0, pitch_ = 0, sy_ = 0, sz_ = 0, sq_ = 0;
   size_t gridElems_ = 0;
-  bool useRccl_ = false, useDirect_ = false;
-  std::vector<bool> direct_; // per direction
+  bool useRccl_ = false, useDirect_ = false, useIpc_ = false;
+  std::vector<bool> direct_, ipc_, pipe_; // per direction: self move / IPC put / pack-transfer-unpack
+  bool ipcReady_ = false;
+  // ipc transport state
+  void *flags_ = nullptr;            // arrival counter per direction (uncached, IPC-exported)
+  DeviceBuffer expected_, done_, err_;
+  bool ipcGrid_ = true;
+  std::vector<void *> peerGrid_, peerFlags_; // per rank (nullptr: not a neighbour / self)
+  std::vector<void *> peerRecv_;             // per direction: the receiver's buffer ("buffers")
+  std::vector<void *> opened_;               // IPC mappings to close
+  double ipcTimeoutS_ = 10.0;                // arrival wait limit (env TZ_IPC_TIMEOUT)
   DeviceBuffer grid_;
   std::vector<DeviceBuffer> send_, recv_;
   std::vector<std::shared_ptr<RcclComm>> comms_;

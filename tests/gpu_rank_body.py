@@ -1,0 +1,81 @@
+"""Rank body for tests/test_gpu_multirank.py: one process per rank, all ranks on GPU 0 (the
+loopback setting of the ipc transport). Prints one JSON line with the rank's results."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import tenzing_amd as tz
+    from tenzing_amd.models import HaloConfig, build_halo
+    from tenzing_amd.parallel import init
+
+    case = sys.argv[1]
+    verbose = bool(os.environ.get("TZ_TEST_VERBOSE"))
+
+    def say(*a):
+        if verbose:
+            print(*a, file=sys.stderr, flush=True)
+
+    ctrl, dev = init(timeout_s=120)
+    say("init done")
+    out = {"rank": ctrl.rank, "size": ctrl.size}
+    if case == "ipc_halo":
+        n = int(os.environ.get("TZ_TEST_N", "48"))
+        res = []
+        fuses = os.environ.get("TZ_TEST_FUSES", "none,choice").split(",")
+        modes = os.environ.get("TZ_TEST_MODES", "eager,graph").split(",")
+        for fuse in fuses:
+            say("build_halo", n, fuse)
+            halo, g = build_halo(HaloConfig(n=n, neighbors=26, order="qxyz", transport="ipc",
+                                            fuse=fuse), ctrl, dev)
+            say("built")
+            rt = tz.HipRuntime(device=dev, n_streams=3, watchdog_s=60.0)
+            for mode in [tz.ExecMode.Eager if m == "eager" else tz.ExecMode.Graph for m in modes]:
+                rt.set_mode(mode)
+                rt.set_graph_unroll(3 if mode == tz.ExecMode.Graph else 1)
+                for seed in range(3):
+                    msg = ""
+                    if ctrl.rank == 0:
+                        msg = tz.random_rollout(tz.State(g, tz.Platform(3)), seed).json(True)
+                    seq = tz.OpIndex(g).sequence_from_json(ctrl.bcast(msg, 0).decode())
+                    halo.init_grid()
+                    say("init_grid", seed)
+                    ctrl.barrier()
+                    rt.prepare(seq)
+                    say("prepared", seq.desc())
+                    rt.run(1)
+                    say("ran")
+                    rt.device_sync()
+                    say("synced")
+                    ctrl.barrier()
+                    bad1 = halo.check_grid()
+                    say("checked", bad1)
+                    ctrl.barrier()
+                    rt.run(7)  # repeated exchanges keep the ghosts right
+                    rt.device_sync()
+                    ctrl.barrier()
+                    bad2 = halo.check_grid()
+                    res.append(dict(fuse=fuse, mode=str(mode), seed=seed, bad1=int(bad1),
+                                    bad2=int(bad2), err=halo.ipc_errors(),
+                                    transport=halo.transport(), ipc_mode=halo.ipc_mode()))
+            if os.environ.get("TZ_TEST_NO_MCTS"):
+                continue
+            # a short collective search over ipc schedules
+            bench = tz.EmpiricalBenchmarker(rt, ctrl)
+            o = tz.MctsOpts()
+            o.n_iters = 4
+            o.bench = tz.BenchOpts(n_iters=3, max_retries=1, target_secs=0.001)
+            rt.set_mode(tz.ExecMode.Eager)
+            r = tz.mcts_explore(g, tz.Platform(3), bench, ctrl, o)
+            out.setdefault("mcts", []).append(len(r.sims))
+            out.setdefault("mcts_err", []).append(halo.ipc_errors())
+            del rt, halo
+        out["runs"] = res
+    print("RESULT " + json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

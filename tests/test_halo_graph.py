@@ -33,13 +33,29 @@ def test_auto_transport_per_direction(tz, size, grid, n_direct):
     # locality is symmetric and means "self-neighbour"
     for i in range(h.ndirs()):
         assert h.is_direct(i) == h.is_direct(h.opposite(i)) == (h.neighbor(i) == 0)
-    names = _names(tz, g)
-    assert sum(n.startswith("he_direct_") for n in names) == n_direct
-    assert sum(n.startswith("he_pack_") for n in names) == 26 - n_direct
-    assert sum(n.startswith("he_shift_") for n in names) == 26 - n_direct
-    assert sum(n.startswith("he_unpack_") for n in names) == 26 - n_direct
-    expect = {1: "direct", 8: "rccl"}.get(size, "direct+rccl")
-    assert h.transport() == expect
+    if size == 1:
+        assert h.transport() == "direct"
+    else:
+        # remote directions: the search chooses between RCCL chains and IPC puts
+        assert h.transport() == ("rccl+ipc" if n_direct == 0 else "direct+rccl+ipc")
+        assert g.contains("he_remote")
+    via = set()
+    for seed in range(12):
+        names = _names(tz, g, seed)
+        assert sum(n.startswith("he_direct_") for n in names) == n_direct
+        n_remote = 26 - n_direct
+        if "he_wait_remote" in names:
+            via.add("ipc")
+            assert sum(n.startswith("he_put_") for n in names) == n_remote
+            assert not any(n.startswith("he_shift_") for n in names)
+        else:
+            via.add("rccl" if n_remote else "none")
+            for stage in ("he_pack_", "he_shift_", "he_unpack_"):
+                assert sum(n.startswith(stage) for n in names) == n_remote
+    assert via == ({"none"} if size == 1 else {"ipc", "rccl"})
+    # forced RCCL: every direction (self-neighbours too) goes through RCCL
+    hr, gr = _halo(tz, size, transport="rccl")
+    assert hr.transport() == "rccl" and not any(hr.is_direct(i) for i in range(hr.ndirs()))
 
 
 @pytest.mark.parametrize("fuse", ["all", "groups", "pack", "choice"])
@@ -72,3 +88,31 @@ def test_copy_and_direct_need_self_neighbours(tz):
     assert h.transport() == "copy" and not h.uses_direct()
     h, _ = _halo(tz, 2, transport="rccl")
     assert h.transport() == "rccl" and not h.uses_direct()
+
+
+@pytest.mark.parametrize("mode", ["grid", "buffers"])
+@pytest.mark.parametrize("fuse", ["none", "all", "choice"])
+@pytest.mark.parametrize("size", [2, 8])
+def test_ipc_transport_graph(tz, fuse, size, mode, monkeypatch):
+    """ipc: self-neighbour moves, pack-free puts for remote directions, one arrival wait that
+    every put precedes (and, in "buffers" mode, one unpack after the wait)"""
+    monkeypatch.setenv("TZ_IPC_GRID", "1" if mode == "grid" else "0")
+    h, g = _halo(tz, size, transport="ipc", fuse=fuse)
+    assert h.ipc_mode() == mode
+    n_ipc = sum(h.is_ipc(i) for i in range(h.ndirs()))
+    assert n_ipc == 26 - sum(h.is_direct(i) for i in range(h.ndirs()))
+    assert h.transport() == ("ipc" if size == 8 else "direct+ipc")
+    for seed in range(3):
+        names = _names(tz, g, seed)
+        assert names[-1] == "he_wait_remote" or "he_wait_remote" in names
+        w = names.index("he_wait_remote")
+        puts = [k for k, n in enumerate(names) if n.startswith("he_put_")]
+        assert puts and max(puts) < w
+        assert not any(n.startswith(("he_pack_", "he_shift_")) for n in names)
+        unpacks = [k for k, n in enumerate(names) if n.startswith("he_unpack_")]
+        if mode == "grid":
+            assert not unpacks
+        else:
+            assert [names[k] for k in unpacks] == ["he_unpack_remote"] and unpacks[0] > w
+        if fuse == "none":
+            assert len(puts) == n_ipc
