@@ -413,7 +413,49 @@ void HaloExchange::setup(Ctrl *ctrl) {
     comms_ = make_rccl_comms(*ctrl, dev, n);
   }
   init_grid();
+  if (useIpc_ && ipcReady_) ipc_preflight(ctrl);
   TZ_HIP(hipDeviceSynchronize());
+}
+
+void HaloExchange::ipc_preflight(Ctrl *ctrl) {
+  // One complete exchange through IPC before the search may use it: every ghost must arrive
+  // (no wait timeout) and be right on every rank. A mapping that "works" but does not deliver
+  // (or delivers wrong data) turns the transport off collectively instead of costing a wait
+  // timeout per iteration of every IPC candidate later.
+  std::vector<int> local, remote;
+  for (int i = 0; i < ndirs(); ++i) {
+    if (direct_[i]) local.push_back(i);
+    else if (ipc_[i]) remote.push_back(i);
+  }
+  double bad = 0;
+  std::string why;
+  const double keep = ipcTimeoutS_;
+  ipcTimeoutS_ = std::min(ipcTimeoutS_, 3.0);
+  try {
+    if (!local.empty()) direct_group(local, nullptr);
+    put_group(remote, nullptr);
+    wait_group(remote, nullptr);
+    if (!ipcGrid_) unpack_group(remote, nullptr);
+    TZ_HIP(hipDeviceSynchronize());
+    const int e = ipc_errors();
+    const uint64_t cells = check_grid();
+    if (e || cells) {
+      bad = 1;
+      why = "preflight exchange: " + std::to_string(e) + " wait timeout(s), " +
+            std::to_string(cells) + " wrong cells";
+    }
+  } catch (const std::exception &ex) {
+    bad = 1;
+    why = std::string("preflight exchange: ") + ex.what();
+  }
+  ipcTimeoutS_ = keep;
+  ctrl->allreduce_max(&bad, 1);
+  if (bad != 0) {
+    ipcReady_ = false;
+    TZ_LOG(Warn, "ipc transport disabled: " << (why.empty() ? "failed on another rank" : why));
+    TZ_CHECK(a_.transport != "ipc", "ipc transport requested but " << why);
+  }
+  init_grid();
 }
 
 std::string HaloExchange::setup_ipc(Ctrl *ctrl) {

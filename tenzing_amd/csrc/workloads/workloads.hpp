@@ -212,6 +212,7 @@ private:
   void add_ipc_part(Graph &g, const std::vector<int> &remote);
   void check_pipelined(int i) const;
   std::string setup_ipc(Ctrl *ctrl); // "" on success, else why IPC cannot be used
+  void ipc_preflight(Ctrl *ctrl);    // one verified exchange; disables IPC collectively on failure
   HaloArgs a_;
   std::vector<Dir> dirs_;
   std::vector<int> opp_, nbr_;
