@@ -49,8 +49,9 @@ void usage() {
       << "usage: tz-search [--workload halo|spmv|halo+spmv|diamond] [--solver mcts|dfs]\n"
          "  [--strategy NAME] [--iters N] [--time-budget S] [--streams N] [--bench-iters N]\n"
          "  [--target-secs S] [--mode eager|graph] [--sim] [--seed N] [--no-expand-rollout]\n"
-         "  [--halo-n N] [--nq N] [--ghost N] [--neighbors 6|26] [--fuse none|pack|all]\n"
-         "  [--transport auto|rccl|copy|direct] [--spmv-m N] [--spmv-form choice|split|accum] [--max-seqs N] [--rdzv-file PATH]\n"
+         "  [--halo-n N] [--nq N] [--ghost N] [--neighbors 6|26] [--order xyzq|qxyz]\n"
+         "  [--fuse none|pack|all|groups|choice] [--graph-unroll K]\n"
+         "  [--transport auto|rccl|ipc|copy|direct] [--spmv-m N] [--spmv-form choice|split|accum] [--max-seqs N] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--watchdog S]\n";
 }
@@ -121,6 +122,7 @@ int main(int argc, char **argv) {
       h.fuse = a.get("fuse", "none");
       h.transport = a.get("transport", "auto");
       h.order = a.get("order", "xyzq");
+      TZ_CHECK(h.order == "xyzq" || h.order == "qxyz", "--order must be xyzq or qxyz");
       h.rank = rank;
       h.size = size;
       halo = std::make_shared<HaloExchange>(h);
@@ -164,6 +166,7 @@ int main(int argc, char **argv) {
       ro.n_streams = streams;
       ro.mode = a.get("mode", "eager") == "graph" ? ExecMode::Graph : ExecMode::Eager;
       ro.watchdog_s = a.num("watchdog", 60);
+      ro.graph_unroll = int(a.num("graph-unroll", 1));
       rt = std::make_unique<HipRuntime>(ro);
       bench = std::make_unique<EmpiricalBenchmarker>(*rt, *ctrl);
     }
@@ -194,6 +197,27 @@ int main(int argc, char **argv) {
       res = mcts_explore(*g, plat, *bench, *ctrl, o);
     }
 
+    // correctness of the winning halo schedule: one exchange from a fresh grid, every cell
+    // checked on every rank (collective)
+    int64_t bad = -1;
+    if (halo && !sim) {
+      std::string js = rank == 0 && res.best() >= 0 ? res.sims[res.best()].seq.json(true).dump() : "";
+      ctrl->bcast(js, 0);
+      if (!js.empty()) {
+        const Sequence best = OpIndex(*g).sequence_from_json(Json::parse(js));
+        rt->set_mode(ExecMode::Eager);
+        halo->init_grid();
+        ctrl->barrier();
+        rt->prepare(best);
+        rt->run(1);
+        rt->device_sync();
+        ctrl->barrier();
+        double b = double(halo->check_grid()) + double(halo->ipc_errors());
+        ctrl->allreduce_sum(&b, 1);
+        bad = int64_t(b);
+      }
+    }
+
     if (rank == 0) {
       if (a.flag("csv")) {
         std::ofstream f(a.get("csv", "results.csv"));
@@ -217,12 +241,10 @@ int main(int argc, char **argv) {
         s["best_pct10_ms"] = res.sims[b].res.pct10 * 1e3;
         s["best_pct50_ms"] = res.sims[b].res.pct50 * 1e3;
       }
+      if (bad >= 0) s["verified_bad_cells"] = bad;
       std::cerr << s.dump() << "\n";
     }
-    if (halo && !sim) {
-      // one more exchange with the best schedule would be needed to check; just verify setup ok
-    }
-    return 0;
+    return bad > 0 ? 3 : 0;
   } catch (const std::exception &e) {
     std::cerr << "tz-search: error: " << e.what() << "\n";
     return 1;

@@ -204,3 +204,24 @@ def test_pygpuop_torch_on_schedule_stream(tz, gpu):
     rt.run(3)
     rt.device_sync()
     assert float(x[0]) == 6.0
+
+
+def test_native_cli_halo_and_spmv_on_gpu(tz, gpu, tmp_path):
+    """tz-search (the native driver, reference tenzing-mcts/examples/halo_*.cu and
+    tenzing-dfs/examples/spmv.cu): search, then verify the winning halo schedule on the device"""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tenzing_amd", "bin", "tz-search")
+    r = subprocess.run([exe, "--workload", "halo", "--halo-n", "64", "--neighbors", "26", "--order", "qxyz",
+                        "--fuse", "choice", "--iters", "6", "--streams", "3", "--bench-iters", "3",
+                        "--target-secs", "0.001", "--mode", "graph", "--graph-unroll", "4",
+                        "--csv", str(tmp_path / "h.csv")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    summary = json.loads(r.stderr.strip().splitlines()[-1])
+    assert summary["candidates"] == 6 and summary["verified_bad_cells"] == 0
+    r = subprocess.run([exe, "--workload", "spmv", "--solver", "dfs", "--max-seqs", "12", "--streams", "2",
+                        "--bench-iters", "3", "--target-secs", "0.001"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stderr.strip().splitlines()[-1])["candidates"] == 12
