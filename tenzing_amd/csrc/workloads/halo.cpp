@@ -413,8 +413,15 @@ void HaloExchange::setup(Ctrl *ctrl) {
     comms_ = make_rccl_comms(*ctrl, dev, n);
   }
   init_grid();
-  if (useIpc_ && ipcReady_) ipc_preflight(ctrl);
+  if (useIpc_ && ipcReady_) {
+    // a peer's preflight puts land in my ghosts: my init_grid must be complete before anyone
+    // puts, and theirs before my check (otherwise their init overwrites what I delivered)
+    TZ_HIP(hipDeviceSynchronize());
+    ctrl->barrier();
+    ipc_preflight(ctrl);
+  }
   TZ_HIP(hipDeviceSynchronize());
+  if (useIpc_ && ipcReady_) ctrl->barrier();
 }
 
 void HaloExchange::ipc_preflight(Ctrl *ctrl) {
@@ -437,16 +444,26 @@ void HaloExchange::ipc_preflight(Ctrl *ctrl) {
     wait_group(remote, nullptr);
     if (!ipcGrid_) unpack_group(remote, nullptr);
     TZ_HIP(hipDeviceSynchronize());
-    const int e = ipc_errors();
-    const uint64_t cells = check_grid();
-    if (e || cells) {
-      bad = 1;
-      why = "preflight exchange: " + std::to_string(e) + " wait timeout(s), " +
-            std::to_string(cells) + " wrong cells";
-    }
   } catch (const std::exception &ex) {
     bad = 1;
     why = std::string("preflight exchange: ") + ex.what();
+  }
+  // peers may still be putting into my ghosts until they have synchronized too (outside the
+  // try: every rank reaches this collective whatever failed locally)
+  ctrl->barrier();
+  if (bad == 0) {
+    try {
+      const int e = ipc_errors();
+      const uint64_t cells = check_grid();
+      if (e || cells) {
+        bad = 1;
+        why = "preflight exchange: " + std::to_string(e) + " wait timeout(s), " +
+              std::to_string(cells) + " wrong cells";
+      }
+    } catch (const std::exception &ex) {
+      bad = 1;
+      why = std::string("preflight check: ") + ex.what();
+    }
   }
   ipcTimeoutS_ = keep;
   ctrl->allreduce_max(&bad, 1);
