@@ -277,15 +277,21 @@ struct WaitArgs {
   int *err;
   long long timeout_ticks;
   int n;
+  int lag;  // wait for arrive[slot] >= expected[slot] + 1 - lag (then expected[slot] += 1)
+  int wait; // 0: signal only
   int slot[kMaxWaitSlots];
+  unsigned long long *signal[kMaxWaitSlots]; // after the wait: +1 (system scope), if non-null
 };
 
+// one wave: lane i waits for slot i, then (optionally) signals a peer's counter. Used for
+// arrivals (receiver waits for the peers' puts, lag 0), credits (sender waits until the peer
+// has consumed its previous put, lag 1) and releases (signal only).
 __global__ __launch_bounds__(64) void ipc_wait_k(WaitArgs a) {
   const int i = threadIdx.x;
-  if (i < a.n) {
+  if (i < a.n && a.wait) {
     const int s = a.slot[i];
-    const unsigned long long want = a.expected[s] + 1;
-    a.expected[s] = want;
+    const unsigned long long want = a.expected[s] + 1 - (unsigned long long)a.lag;
+    a.expected[s] += 1;
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(&a.arrive[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
       __builtin_amdgcn_s_sleep(2);
@@ -296,6 +302,8 @@ __global__ __launch_bounds__(64) void ipc_wait_k(WaitArgs a) {
     }
   }
   __threadfence_system();
+  if (i < a.n && a.signal[i])
+    __hip_atomic_fetch_add(a.signal[i], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // host dispatch over (unpack, unroll, nt)
@@ -519,17 +527,38 @@ void box_pack_many_signal(double *grid, const BoxDesc *boxes, int n, const MoveS
 }
 
 void ipc_wait(const unsigned long long *arrive, unsigned long long *expected, const int *slots,
-              int n, int *err, double timeout_s, void *stream) {
+              int n, int *err, double timeout_s, void *stream, int lag,
+              unsigned long long *const *signal) {
   if (n <= 0) return;
   if (n > kMaxWaitSlots) throw std::runtime_error("ipc_wait: too many slots");
   if (!arrive || !expected || !err) throw std::runtime_error("ipc_wait: null pointer");
+  if (lag < 0 || lag > 1) throw std::runtime_error("ipc_wait: lag must be 0 or 1");
   WaitArgs a{};
   a.arrive = arrive;
   a.expected = expected;
   a.err = err;
   a.timeout_ticks = (long long)(timeout_s * 1.0e8); // wall_clock64 runs at 100 MHz
   a.n = n;
-  for (int i = 0; i < n; ++i) a.slot[i] = slots[i];
+  a.lag = lag;
+  a.wait = 1;
+  for (int i = 0; i < n; ++i) {
+    a.slot[i] = slots[i];
+    a.signal[i] = signal ? signal[i] : nullptr;
+  }
+  hipLaunchKernelGGL(ipc_wait_k, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void ipc_signal(unsigned long long *const *signal, int n, void *stream) {
+  if (n <= 0) return;
+  if (n > kMaxWaitSlots) throw std::runtime_error("ipc_signal: too many counters");
+  WaitArgs a{};
+  a.n = n;
+  a.wait = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!signal[i]) throw std::runtime_error("ipc_signal: null counter");
+    a.signal[i] = signal[i];
+  }
   hipLaunchKernelGGL(ipc_wait_k, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), a);
   TZ_HIP_LAUNCH_CHECK();
 }

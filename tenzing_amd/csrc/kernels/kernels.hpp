@@ -62,11 +62,17 @@ void box_move_many_signal(const MoveDesc *d, int n, const MoveSignal &sig, void 
 void box_pack_many_signal(double *grid, const BoxDesc *d, int n, const MoveSignal &sig,
                           void *stream);
 
-/// Receiver side of IPC puts: for each of the `n` slots, increment the local expected count and
-/// spin (system-scope acquire loads, s_sleep back-off) until `arrive[slot]` reaches it. A wait
-/// longer than `timeout_s` sets *err = 1 and gives up, so a lost peer cannot hang the GPU.
+/// Device-side counter wait for IPC puts: for each of the `n` slots, spin (system-scope acquire
+/// loads, s_sleep back-off) until `arrive[slot]` reaches expected[slot] + 1 - lag, then bump
+/// expected[slot] and, if `signal` is given, add 1 to signal[k] (system scope, release).
+/// lag 0: receiver waits for this round's arrival; lag 1: sender waits for the credit of its
+/// previous put. A wait longer than `timeout_s` sets *err = 1 and gives up, so a lost peer
+/// cannot hang the GPU.
 void ipc_wait(const unsigned long long *arrive, unsigned long long *expected, const int *slots,
-              int n, int *err, double timeout_s, void *stream);
+              int n, int *err, double timeout_s, void *stream, int lag = 0,
+              unsigned long long *const *signal = nullptr);
+/// add 1 to each of `n` (peer) counters, system scope, after the stream's prior work
+void ipc_signal(unsigned long long *const *signal, int n, void *stream);
 
 /// pack (grid -> buf) or unpack (buf -> grid) one box
 void box_copy(double *grid, const BoxDesc &d, bool unpack, void *stream);

@@ -138,16 +138,18 @@ private:
 /// one op for a whole group of directions (single kernel launch / single RCCL group)
 class HaloStageGroup : public GpuOp {
 public:
-  enum Stage { Pack, Shift, Unpack, Direct, Put };
+  // UnpackRelease: unpack IPC receive buffers, then hand them back to the senders (credits)
+  enum Stage { Pack, Shift, Unpack, Direct, Put, UnpackRelease };
   HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag)
       : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
   std::string name() const override {
-    static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_", "he_put_"};
+    static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_", "he_put_",
+                                "he_unpack_"};
     return pre[st_] + tag_;
   }
   std::string kind() const override {
     static const char *k[] = {"HaloPackGroup", "HaloShiftGroup", "HaloUnpackGroup",
-                              "HaloDirectGroup", "HaloPutGroup"};
+                              "HaloDirectGroup", "HaloPutGroup", "HaloUnpackGroup"};
     return k[st_];
   }
   double bytes() const override {
@@ -164,7 +166,8 @@ public:
     else if (st_ == Shift) h_->shift_group(dirs_, s);
     else if (st_ == Unpack) h_->unpack_group(dirs_, s);
     else if (st_ == Direct) h_->direct_group(dirs_, s);
-    else h_->put_group(dirs_, s);
+    else if (st_ == Put) h_->put_group(dirs_, s);
+    else h_->ipc_unpack_group(dirs_, s);
   }
 
 private:
@@ -442,7 +445,7 @@ void HaloExchange::ipc_preflight(Ctrl *ctrl) {
     if (!local.empty()) direct_group(local, nullptr);
     put_group(remote, nullptr);
     wait_group(remote, nullptr);
-    if (!ipcGrid_) unpack_group(remote, nullptr);
+    if (!ipcGrid_) ipc_unpack_group(remote, nullptr);
     TZ_HIP(hipDeviceSynchronize());
   } catch (const std::exception &ex) {
     bad = 1;
@@ -487,10 +490,14 @@ std::string HaloExchange::setup_ipc(Ctrl *ctrl) {
   try {
     // arrival counters live in uncached memory: a remote GPU's system-scope atomics land in
     // HBM and the local spin loads (system scope) see them without stale cache lines
-    TZ_HIP(hipExtMallocWithFlags(&flags_, std::max<size_t>(nd * 8, 64), hipDeviceMallocUncached));
-    TZ_HIP(hipMemset(flags_, 0, nd * 8));
+    // [arrivals of direction i | credits of direction i]: a receiver counts the puts it got in
+    // slot i and, once it has consumed them, returns a credit to the sender's slot nd + i
+    TZ_HIP(hipExtMallocWithFlags(&flags_, std::max<size_t>(2 * nd * 8, 64), hipDeviceMallocUncached));
+    TZ_HIP(hipMemset(flags_, 0, 2 * nd * 8));
     expected_ = DeviceBuffer(nd * 8);
     TZ_HIP(hipMemset(expected_.get(), 0, nd * 8));
+    sent_ = DeviceBuffer(nd * 8);
+    TZ_HIP(hipMemset(sent_.get(), 0, nd * 8));
     done_ = DeviceBuffer(nd * kern::kMaxBoxes * sizeof(unsigned int));
     TZ_HIP(hipMemset(done_.get(), 0, done_.bytes()));
     err_ = DeviceBuffer(sizeof(int));
@@ -557,6 +564,10 @@ void HaloExchange::put_group(const std::vector<int> &dirs, void *stream) const {
   // block counters: one slot range per group, keyed by its first direction (groups of one
   // schedule are disjoint, so concurrently running puts never share counters)
   sig.done = done_.as<unsigned int>() + size_t(dirs.front()) * kern::kMaxBoxes;
+  // flow control: put n+1 of direction i may only overwrite the peer's ghosts / receive buffer
+  // after the peer has consumed put n (its credit, returned to my slot nd + i)
+  kern::ipc_wait(static_cast<const unsigned long long *>(flags_) + ndirs(), sent_.as<unsigned long long>(),
+                 dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/1);
   for (size_t k = 0; k < dirs.size(); ++k) {
     const int i = dirs[k];
     TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i], "direction " << i << " is not an ipc put");
@@ -592,8 +603,32 @@ void HaloExchange::put_group(const std::vector<int> &dirs, void *stream) const {
 void HaloExchange::wait_group(const std::vector<int> &dirs, void *stream) const {
   TZ_CHECK(ready() && ipcReady_, "ipc transport not set up");
   for (int i : dirs) TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i], "direction " << i << " is not an ipc put");
+  // grid mode: the ghosts are consumed once they arrived (nothing reads them inside the
+  // exchange), so the credit goes back right after the wait; buffers mode returns it after
+  // the unpack (ipc_unpack_group)
+  const std::vector<unsigned long long *> credits = credit_ptrs(dirs);
   kern::ipc_wait(static_cast<const unsigned long long *>(flags_), expected_.as<unsigned long long>(),
-                 dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream);
+                 dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/0,
+                 ipcGrid_ ? credits.data() : nullptr);
+}
+
+std::vector<unsigned long long *> HaloExchange::credit_ptrs(const std::vector<int> &dirs) const {
+  // the put that filled my slot i came from nbr(-i); its credit slot for direction i is nd + i
+  std::vector<unsigned long long *> v;
+  for (int i : dirs) {
+    const int from = nbr_[opp_[i]];
+    TZ_CHECK(peerFlags_.size() > size_t(from) && peerFlags_[size_t(from)],
+             "rank " << from << " is not IPC-mapped");
+    v.push_back(static_cast<unsigned long long *>(peerFlags_[size_t(from)]) + ndirs() + i);
+  }
+  return v;
+}
+
+void HaloExchange::ipc_unpack_group(const std::vector<int> &dirs, void *stream) const {
+  TZ_CHECK(ready() && ipcReady_ && !ipcGrid_, "ipc buffers mode not set up");
+  unpack_group(dirs, stream);
+  const std::vector<unsigned long long *> credits = credit_ptrs(dirs);
+  kern::ipc_signal(credits.data(), int(credits.size()), stream);
 }
 
 int HaloExchange::ipc_errors() {
@@ -888,7 +923,7 @@ void HaloExchange::add_ipc_part(Graph &g, const std::vector<int> &remote) {
     g.then_finish(w);
   } else {
     // "buffers" mode: my receive buffers are complete after the wait; unpack them
-    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, remote, "remote");
+    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::UnpackRelease, remote, "remote");
     g.then(w, u);
     g.then_finish(u);
   }

@@ -191,6 +191,9 @@ public:
   void put_group(const std::vector<int> &dirs, void *stream) const;
   /// ipc transport: wait until the ghosts filled by the neighbours' puts of `dirs` arrived
   void wait_group(const std::vector<int> &dirs, void *stream) const;
+  /// ipc "buffers" mode: unpack the receive buffers filled for `dirs`, then return the
+  /// senders' credits (their next put may overwrite the buffers)
+  void ipc_unpack_group(const std::vector<int> &dirs, void *stream) const;
   /// ipc transport: number of arrival waits that timed out (0 = healthy); resets the flag
   int ipc_errors();
   /// ipc transport: "grid" (puts land directly in the peer's ghost cells) or "buffers" (puts
@@ -225,6 +228,8 @@ private:
   // ipc transport state
   void *flags_ = nullptr;            // arrival counter per direction (uncached, IPC-exported)
   DeviceBuffer expected_, done_, err_;
+  DeviceBuffer sent_; // per direction: puts issued so far (credit wait bookkeeping)
+  std::vector<unsigned long long *> credit_ptrs(const std::vector<int> &dirs) const;
   bool ipcGrid_ = true;
   std::vector<void *> peerGrid_, peerFlags_; // per rank (nullptr: not a neighbour / self)
   std::vector<void *> peerRecv_;             // per direction: the receiver's buffer ("buffers")
