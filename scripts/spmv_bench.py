@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Isolated CSR SpMV kernel timings (MI355X): every lanes-per-row variant and the CSR-stream
-kernel on the SpMV workload's local block (m=150,000, nnz=10 m by default).
+"""Isolated CSR SpMV kernel timings (MI355X): every lanes-per-row variant, the CSR-stream
+kernel and the rocSPARSE CSR algorithms (library comparison) on the SpMV workload's local block
+(m=150,000, nnz=10 m by default).
 
   python scripts/spmv_bench.py [--m 150000] [--reps 200]
 """
@@ -31,10 +32,20 @@ def main():
     nbytes = rp_t.numel() * 4 + ci_t.numel() * 8 + a.m * 8
     st = torch.cuda.current_stream().cuda_stream
     K = tz._tz.kernels
-    for lanes in (4, 8, 16, 32, -1):
-        def fn():
-            K.csr_spmv(a.m, rp_t.data_ptr(), ci_t.data_ptr(), v_t.data_ptr(), x.data_ptr(),
-                       y.data_ptr(), lanes, False, st)
+    variants = [(f"lanes{w}", w) for w in (4, 8, 16, 32)] + [("stream", -1)]
+    variants += [(f"rocsparse_{alg}", alg) for alg in ("adaptive", "lrb", "rowsplit")]
+    yref = None
+    for name, v in variants:
+        if isinstance(v, int):
+            def fn(lanes=v):
+                K.csr_spmv(a.m, rp_t.data_ptr(), ci_t.data_ptr(), v_t.data_ptr(), x.data_ptr(),
+                           y.data_ptr(), lanes, False, st)
+        else:
+            lib = K.RocsparseCsr(a.m, a.m, ci_t.numel(), rp_t.data_ptr(), ci_t.data_ptr(),
+                                 v_t.data_ptr(), x.data_ptr(), y.data_ptr(), v)
+
+            def fn(lib=lib):
+                lib.run(st)
         for _ in range(5):
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -44,8 +55,12 @@ def main():
         e1.record()
         e1.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
-        print(json.dumps({"lanes": lanes, "us": round(us, 2), "nnz": ci_t.numel(),
-                          "GBps": round(nbytes / us / 1e3, 1)}), flush=True)
+        if yref is None:
+            yref = y.clone()
+        err = float((y - yref).abs().max() / yref.abs().max().clamp_min(1e-30))
+        print(json.dumps({"variant": name, "us": round(us, 2), "nnz": ci_t.numel(),
+                          "GBps": round(nbytes / us / 1e3, 1), "rel_err_vs_lanes4": err}),
+              flush=True)
 
 
 if __name__ == "__main__":

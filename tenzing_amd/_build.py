@@ -26,7 +26,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("TZ_OFFLOAD_ARCH", "gfx950")
 
 CORE = ["json", "numeric", "ops", "graph", "state", "serdes", "ctrl", "benchmark", "solve"]
-HIP_HOST = ["hip_runtime", "rccl_comm"]
+HIP_HOST = ["hip_runtime", "rccl_comm", "rocsparse_spmv"]
 WORKLOADS = ["halo", "spmv", "workloads_common"]
 KERNELS = ["halo_kernels", "spmv_kernels"]
 
@@ -61,7 +61,7 @@ def _ninja_file(debug: bool) -> str:
         f"hipflags = {common} {hipdefs}",
         f"devflags = {common} --offload-arch={ARCH} -munsafe-fp-atomics -ffp-contract=fast",
         f"pyflags = -I{pybind11.get_include()} -I{py_inc}",
-        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lpthread",
+        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lrocsparse -lrocprofiler-sdk-roctx -lpthread",
         "rule cxx",
         "  command = $cxx $cflags $extra -MMD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",

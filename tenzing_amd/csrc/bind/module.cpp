@@ -9,6 +9,7 @@
 #include "core/solve.hpp"
 #include "hip/hip_runtime.hpp"
 #include "hip/rccl_comm.hpp"
+#include "hip/rocsparse_spmv.hpp"
 #include "kernels/kernels.hpp"
 #include "workloads/workloads.hpp"
 
@@ -637,6 +638,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("compound", &SpmvArgs::compound)
       .def_readwrite("kernel_choice", &SpmvArgs::kernel_choice)
       .def_readwrite("form", &SpmvArgs::form)
+      .def_readwrite("library", &SpmvArgs::library)
       .def_readwrite("prefix", &SpmvArgs::prefix)
       .def("json", [](const SpmvArgs &a) { return a.json().dump(); });
   py::class_<DistSpmv, std::shared_ptr<DistSpmv>>(m, "DistSpmv")
@@ -677,6 +679,19 @@ PYBIND11_MODULE(_tz, m) {
                    reinterpret_cast<float *>(y), lanes, acc, P(s));
   }, py::arg("n_rows"), py::arg("row_ptr"), py::arg("col_ind"), py::arg("val"), py::arg("x"), py::arg("y"),
      py::arg("lanes") = 0, py::arg("accumulate") = false, py::arg("stream") = 0);
+  py::class_<RocsparseCsr, std::shared_ptr<RocsparseCsr>>(
+      k, "RocsparseCsr", "rocSPARSE CSR SpMV (library comparison variant): y = A x on raw pointers")
+      .def(py::init([](int64_t m, int64_t n, int64_t nnz, uintptr_t rp, uintptr_t ci, uintptr_t v,
+                       uintptr_t x, uintptr_t y, const std::string &alg) {
+             return std::make_shared<RocsparseCsr>(
+                 m, n, nnz, reinterpret_cast<const int32_t *>(rp), reinterpret_cast<const int32_t *>(ci),
+                 reinterpret_cast<const float *>(v), reinterpret_cast<const float *>(x),
+                 reinterpret_cast<float *>(y), alg.c_str());
+           }),
+           py::arg("m"), py::arg("n"), py::arg("nnz"), py::arg("row_ptr"), py::arg("col_ind"),
+           py::arg("val"), py::arg("x"), py::arg("y"), py::arg("alg") = "adaptive")
+      .def("run", [](const RocsparseCsr &r, uintptr_t s, bool acc) { r.run(P(s), acc); },
+           py::arg("stream") = 0, py::arg("accumulate") = false);
   k.def("gather_f32", [](int n, uintptr_t src, uintptr_t idx, uintptr_t dst, uintptr_t s) {
     kern::gather_f32(n, reinterpret_cast<const float *>(src), reinterpret_cast<const int32_t *>(idx),
                      reinterpret_cast<float *>(dst), P(s));

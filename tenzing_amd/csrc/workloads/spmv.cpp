@@ -3,6 +3,7 @@
 #include "core/util.hpp"
 #include "hip/hip_runtime.hpp"
 #include "hip/rccl_comm.hpp"
+#include "hip/rocsparse_spmv.hpp"
 
 #include <hip/hip_runtime_api.h>
 
@@ -23,6 +24,7 @@ Json SpmvArgs::json() const {
   j["compound"] = compound;
   j["kernel_choice"] = kernel_choice;
   j["form"] = form;
+  j["library"] = library;
   return j;
 }
 
@@ -257,6 +259,15 @@ void DistSpmv::setup(Ctrl *ctrl) {
     TZ_HIP(hipGetDevice(&dev));
     comm_ = std::make_shared<RcclComm>(*ctrl, dev);
   }
+  if (a_.kernel_choice && !a_.library.empty() && local_.nnz() > 0) {
+    auto mk = [&](DeviceBuffer &y) {
+      return std::make_shared<RocsparseCsr>(nl, nl, local_.nnz(), dLocalRow_.as<int32_t>(),
+                                            dLocalCol_.as<int32_t>(), dLocalVal_.as<float>(),
+                                            dX_.as<float>(), y.as<float>(), a_.library.c_str());
+    };
+    rsYl_ = mk(dYl_);
+    rsY_ = mk(dY_);
+  }
   TZ_HIP(hipDeviceSynchronize());
 }
 
@@ -299,6 +310,16 @@ void DistSpmv::exchange(void *stream) const {
 }
 
 void DistSpmv::spmv_local(int lanes, void *stream, bool intoY) const {
+  if (lanes == kLibrary) {
+    const auto &rs = intoY ? rsY_ : rsYl_;
+    if (rs) {
+      rs->run(stream);
+      return;
+    }
+    // no library state only for an empty local block: any kernel writes the zeros
+    TZ_CHECK(local_.nnz() == 0, "rocSPARSE SpMV variant not set up");
+    lanes = 0;
+  }
   kern::csr_spmv(int(local_rows()), dLocalRow_.as<int32_t>(), dLocalCol_.as<int32_t>(),
                  dLocalVal_.as<float>(), dX_.as<float>(), (intoY ? dY_ : dYl_).as<float>(),
                  lanes > 0 ? lanes : lanes_, false, stream);
@@ -329,6 +350,8 @@ std::shared_ptr<Graph> DistSpmv::form_graph(bool accum, const std::string &p) {
     for (int w : {4, 8, 16})
       ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w, accum));
     ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_stream", -1, accum));
+    if (!a_.library.empty())
+      ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_rocsparse_" + a_.library, kLibrary, accum));
     yl = std::make_shared<StaticChoiceOp>(p + "yl", ch);
   } else {
     yl = std::make_shared<SpmvLocal>(self, p + "yl", 0, accum);

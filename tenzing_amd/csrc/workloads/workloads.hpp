@@ -34,6 +34,7 @@
 namespace tz {
 
 class RcclComm;
+class RocsparseCsr;
 
 /// hipMalloc'd memory (RAII)
 class DeviceBuffer {
@@ -265,6 +266,9 @@ struct SpmvArgs {
   int device = -1;
   bool compound = true;     // wrap in an expandable CompoundOp (reference SpMV CompoundOp)
   bool kernel_choice = true; // local SpMV as a ChoiceOp over lanes-per-row variants
+  // rocSPARSE CSR algorithm added to that ChoiceOp as a library comparison variant (the
+  // reference's cuSPARSE SpMV); "" leaves the library out
+  std::string library = "adaptive";
   // "split": y = A_l x + A_r x_r through two partial vectors and a VectorAdd (reference
   // structure); "accum": y = A_l x, then y += A_r x_r (no partials, no add; the remote SpMV
   // waits for the local one); "choice": a ChoiceOp over both forms
@@ -297,6 +301,8 @@ public:
   // op bodies
   void scatter(void *stream) const;
   void exchange(void *stream) const;
+  /// `lanes` value selecting the rocSPARSE variant of the local product
+  static constexpr int kLibrary = -2;
   /// local block product into the partial y_l (or straight into y when `into_y`)
   void spmv_local(int lanes, void *stream, bool into_y = false) const;
   /// remote block product into the partial y_r (or y += ... when `accumulate`); no launch
@@ -318,6 +324,7 @@ private:
   DeviceBuffer dLocalRow_, dLocalCol_, dLocalVal_, dRemoteRow_, dRemoteCol_, dRemoteVal_;
   DeviceBuffer dX_, dXr_, dSendIdx_, dSend_, dYl_, dYr_, dY_;
   std::shared_ptr<RcclComm> comm_;
+  std::shared_ptr<RocsparseCsr> rsYl_, rsY_; // library SpMV into y_l / into y
   std::shared_ptr<const Graph> inner_;
   std::shared_ptr<Graph> form_graph(bool accum, const std::string &p);
 };

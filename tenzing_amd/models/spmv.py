@@ -20,6 +20,7 @@ class SpmvConfig:
     compound: bool = True       # expandable CompoundOp (reference SpMV CompoundOp)
     kernel_choice: bool = True  # local SpMV kernel variants as a ChoiceOp
     form: str = "choice"        # split (y = yl + yr, reference) | accum (y = yl; y += yr) | choice
+    library: str = "adaptive"   # rocSPARSE CSR algorithm added to the kernel ChoiceOp ("" = none)
     prefix: str = ""
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.SpmvArgs":
@@ -27,6 +28,7 @@ class SpmvConfig:
         a.m, a.bw, a.nnz, a.seed = self.m, self.bw, self.nnz, self.seed
         a.compound, a.kernel_choice, a.prefix = self.compound, self.kernel_choice, self.prefix
         a.form = self.form
+        a.library = self.library
         a.rank, a.size, a.device = rank, size, device
         return a
 

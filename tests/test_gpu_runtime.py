@@ -152,6 +152,34 @@ def test_spmv_workload_correct(tz, gpu, form):
             assert sp.check() < 1e-4
 
 
+@pytest.mark.parametrize("form", ["split", "accum"])
+def test_spmv_every_local_kernel_variant(tz, gpu, form):
+    """each alternative of the local-product ChoiceOp (wave64 kernels and the rocSPARSE
+    library variant) computes the right y, eagerly and captured into a hipGraph"""
+    from tenzing_amd.models import SpmvConfig, build_spmv
+
+    sp, g = build_spmv(SpmvConfig(m=30000, form=form), tz.SelfCtrl(), device=0)
+    by_variant = {}
+    for seed in range(400):
+        seq = tz.random_rollout(tz.State(g, tz.Platform(2)), seed)
+        names = [o.name for o in seq.ops()]
+        v = [n for n in names if n.startswith("yl_")]
+        assert len(v) == 1, names
+        by_variant.setdefault(v[0], seq)
+    assert any("rocsparse" in k for k in by_variant), sorted(by_variant)
+    assert len(by_variant) == 5, sorted(by_variant)
+    rt = tz.HipRuntime(device=0, n_streams=2)
+    for m in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+        rt.set_mode(m)
+        for name, seq in sorted(by_variant.items()):
+            sp.reset_y()
+            rt.prepare(seq)
+            assert rt.effective_mode == m, name
+            rt.run(2)
+            rt.device_sync()
+            assert sp.check() < 1e-4, (name, m)
+
+
 def test_mcts_halo_on_gpu(tz, gpu):
     halo, g = _small_halo(tz, neighbors=6, n=64)
     rt = tz.HipRuntime(device=0, n_streams=2, watchdog_s=60.0)
