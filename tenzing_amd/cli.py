@@ -96,6 +96,7 @@ def cmd_search(a) -> int:
         o = tz.DfsOpts()
         o.max_seqs = a.max_seqs
         o.bench = bo
+        o.trap_signals = True  # SIGINT/SIGTERM: print the partial results CSV, exit 1
         res = tz.dfs_explore(g, plat, bench, ctrl, o)
     else:
         o = tz.MctsOpts()
@@ -106,6 +107,7 @@ def cmd_search(a) -> int:
         o.expand_rollout = not a.no_expand_rollout
         o.dump_tree = a.dump_tree
         o.bench = bo
+        o.trap_signals = True
         if a.checkpoint:
             o.checkpoint_path = a.checkpoint
             o.checkpoint_every = 10

@@ -1,8 +1,10 @@
 """CLI drivers (Python and native) without hardware."""
 import json
 import os
+import signal
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -52,3 +54,43 @@ def test_env_report():
     out = _py("env")
     j = json.loads(out)
     assert "tenzing_amd" in j and "rccl" in j
+
+
+def test_native_cli_sigint_dumps_partial_csv():
+    """reference trap.cpp:26-30 / mcts.hpp:175-178: SIGINT during a search prints the results
+    gathered so far as CSV and exits 1"""
+    exe = os.path.join(ROOT, "tenzing_amd", "bin", "tz-search")
+    p = subprocess.Popen([exe, "--sim", "--workload", "halo", "--neighbors", "26", "--streams", "4",
+                          "--iters", "100000000", "--bench-iters", "2"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    time.sleep(4.0)
+    p.send_signal(signal.SIGINT)
+    out, err = p.communicate(timeout=60)
+    assert p.returncode == 1, err[-2000:]
+    lines = out.strip().splitlines()
+    assert json.loads(lines[0])["mcts__Opts"]["nIters"] == 100000000
+    rows = lines[1:]
+    assert len(rows) >= 1
+    for r in rows:
+        f = r.split("|")
+        assert int(f[0]) >= 0 and float(f[2]) > 0
+        json.loads(f[7])  # first op of the schedule
+
+
+def test_cpulist_parsing_and_binding(monkeypatch):
+    """GPU-local CPU binding (the reference's dead NUMA binding, numa.cpp:13): sysfs cpulist
+    parsing, and binding restricted to the CPUs this process may use"""
+    from tenzing_amd.utils import env
+
+    assert env.parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert env.parse_cpulist("") == []
+    allowed = sorted(os.sched_getaffinity(0))
+    monkeypatch.setattr(env, "local_cpus", lambda dev: [allowed[0], 10 ** 6])
+    try:
+        assert env.bind_local_cpus(0) == [allowed[0]]
+        assert os.sched_getaffinity(0) == {allowed[0]}
+    finally:
+        os.sched_setaffinity(0, allowed)
+    monkeypatch.setattr(env, "local_cpus", lambda dev: [])
+    assert env.bind_local_cpus(0) == []
+    assert sorted(os.sched_getaffinity(0)) == allowed
