@@ -125,13 +125,19 @@ def test_halo_rccl_self_exchange(tz, gpu):
     halo, g = _small_halo(tz, neighbors=6, transport="rccl")
     assert halo.uses_rccl()
     for m in (tz.ExecMode.Eager, tz.ExecMode.Graph):
-        rt = tz.HipRuntime(device=0, n_streams=2, mode=m)
-        seq = tz.random_rollout(tz.State(g, tz.Platform(2)), 4)
-        halo.init_grid()
-        rt.prepare(seq)
-        rt.run(1)
-        rt.device_sync()
-        assert halo.check_grid() == 0
+        rt = tz.HipRuntime(device=0, n_streams=2, mode=m, graph_unroll=3)
+        for seed in (4, 5):
+            seq = tz.random_rollout(tz.State(g, tz.Platform(2)), seed)
+            halo.init_grid()
+            rt.prepare(seq)
+            # RCCL send/recv must capture into the schedule's hipGraph (no silent eager fallback)
+            assert rt.effective_mode == m
+            rt.run(1)
+            rt.device_sync()
+            assert halo.check_grid() == 0
+            rt.run(7)  # unrolled graph launches + remainder
+            rt.device_sync()
+            assert halo.check_grid() == 0
 
 
 @pytest.mark.parametrize("form", ["split", "accum", "choice"])
