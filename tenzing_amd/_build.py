@@ -113,6 +113,66 @@ def _ninja_file(debug: bool) -> str:
     return "\n".join(lines) + "\n"
 
 
+SANITIZERS = {
+    # host-only: the core (graph, synchronizer, solvers, control plane) and its unit suite. GPU
+    # code is not instrumented (no GPU sanitizers on this pool)
+    "asan": "-fsanitize=address,undefined -fno-sanitize-recover=undefined",
+    "tsan": "-fsanitize=thread",
+}
+
+
+def _sanitizer_ninja(kind: str) -> str:
+    flags = SANITIZERS[kind]
+    out = BUILD / kind
+    cxx = f"{ROCM}/lib/llvm/bin/clang++"
+    common = (f"-std=c++17 -O1 -g -fno-omit-frame-pointer {flags} -Wall -Wno-unused-parameter "
+              f"-DTZ_GIT_HASH=\\\"{_git_hash()}\\\" -I{CSRC}")
+    lines = [
+        "ninja_required_version = 1.5",
+        f"cxx = {cxx}",
+        f"cflags = {common}",
+        "rule cxx",
+        "  command = $cxx $cflags -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX[" + kind + "] $out",
+        "rule link",
+        f"  command = $cxx {flags} -o $out $in -lpthread",
+        "  description = LINK $out",
+    ]
+    objs = []
+    for n in CORE:
+        o = f"{out}/core/{n}.o"
+        lines.append(f"build {o}: cxx {CSRC}/core/{n}.cpp")
+        objs.append(o)
+    o = f"{out}/tools/tz_unit.o"
+    lines.append(f"build {o}: cxx {CSRC}/tools/tz_unit.cpp")
+    objs.append(o)
+    lines.append(f"build {out}/tz-unit: link {' '.join(objs)}")
+    lines.append(f"default {out}/tz-unit")
+    return "\n".join(lines) + "\n"
+
+
+def build_sanitized(kind: str, jobs: int | None = None) -> Path:
+    """Host-only sanitizer build of the native unit suite (``asan``: AddressSanitizer +
+    UndefinedBehaviorSanitizer, ``tsan``: ThreadSanitizer). Returns the tz-unit path."""
+    if kind not in SANITIZERS:
+        raise ValueError(f"sanitizer must be one of {sorted(SANITIZERS)}")
+    out = BUILD / kind
+    out.mkdir(parents=True, exist_ok=True)
+    nf = out / "build.ninja"
+    content = _sanitizer_ninja(kind)
+    if not nf.exists() or nf.read_text() != content:
+        nf.write_text(content)
+    ninja = shutil.which("ninja") or "ninja"
+    r = subprocess.run([ninja, "-C", str(out), f"-j{jobs or min(16, os.cpu_count() or 4)}"],
+                       text=True, capture_output=True)
+    if r.returncode != 0:
+        sys.stderr.write((r.stdout or "") + (r.stderr or ""))
+        raise RuntimeError(f"tenzing_amd {kind} build failed")
+    return out / "tz-unit"
+
+
 def build(jobs: int | None = None, debug: bool = False, verbose: bool = False) -> Path:
     """Compile everything (idempotent, incremental). Returns the extension path."""
     BUILD.mkdir(parents=True, exist_ok=True)
@@ -140,5 +200,7 @@ if __name__ == "__main__":
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--sanitize", choices=sorted(SANITIZERS),
+                    help="build the host-only unit suite under a sanitizer instead")
     a = ap.parse_args()
-    print(build(a.j, a.debug, a.verbose))
+    print(build_sanitized(a.sanitize, a.j) if a.sanitize else build(a.j, a.debug, a.verbose))

@@ -5,13 +5,16 @@
 // plus synchronizer race-freedom, redundant-sync removal, serdes round trips and solvers.
 // Run: tenzing_amd/bin/tz-unit [filter]
 #include "core/benchmark.hpp"
+#include "core/ctrl.hpp"
 #include "core/solve.hpp"
 
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <functional>
+#include <future>
 #include <iostream>
+#include <thread>
 #include <random>
 #include <set>
 #include <string>
@@ -419,6 +422,77 @@ TEST(mcts_checkpoint_resume) {
   SearchResult r2 = mcts_explore(*g, Platform::make_n_streams(2), sb, ctrl, o2);
   CHECK(r2.sims.size() >= r1.sims.size());
   std::remove(o.checkpoint_path.c_str());
+}
+
+TEST(tcp_ctrl_ranks_as_threads) {
+  // the control plane (reference MPI_Bcast / MPI_Barrier / MPI_Allreduce call sites) with 4
+  // ranks as threads of one process, then a collective MCTS search over it: rank 0 owns the
+  // tree, every rank runs every candidate. Under the TSan build this is the data-race check of
+  // the control plane and of the solver's collective protocol.
+  constexpr int N = 4;
+  std::promise<int> portP;
+  std::shared_future<int> port = portP.get_future().share();
+  struct Out {
+    std::string bc;
+    double mx = 0, sm = 0;
+    std::vector<std::string> ag;
+    size_t sims = 0;
+    double best = 0;
+    std::string err;
+  };
+  std::vector<Out> out(N);
+  auto body = [&](int r) {
+    try {
+      TcpCtrl c(r, N);
+      if (r == 0) portP.set_value(c.listen(0, "127.0.0.1"));
+      c.connect("127.0.0.1", port.get(), 30.0);
+      c.barrier();
+      std::string s = r == 2 ? "from-two" : "";
+      c.bcast(s, 2);
+      out[r].bc = s;
+      double v[2] = {double(r), double(10 * r)};
+      c.allreduce_max(v, 2);
+      out[r].mx = v[0] + v[1];
+      double w = 1.0 + r;
+      c.allreduce_sum(&w, 1);
+      out[r].sm = w;
+      out[r].ag = c.allgather("r" + std::to_string(r));
+      auto g = diamond(10, 100, 100, 10);
+      SimParams p;
+      p.launch_us = 1;
+      SimBenchmarker sb(2, p);
+      MctsOpts o;
+      o.n_iters = 12;
+      o.seed = 3;
+      o.bench.n_iters = 2;
+      SearchResult res = mcts_explore(*g, Platform::make_n_streams(2), sb, c, o);
+      out[r].sims = res.sims.size();
+      if (r == 0 && res.best() >= 0) out[r].best = res.sims[res.best()].res.pct10;
+      c.barrier();
+    } catch (const std::exception &e) {
+      out[r].err = e.what();
+      if (r == 0) {
+        try {
+          portP.set_value(-1);
+        } catch (...) {
+        }
+      }
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int r = 0; r < N; ++r) ts.emplace_back(body, r);
+  for (auto &t : ts) t.join();
+  for (int r = 0; r < N; ++r) {
+    if (!out[r].err.empty()) std::fprintf(stderr, "  rank %d: %s\n", r, out[r].err.c_str());
+    CHECK(out[r].err.empty());
+    CHECK(out[r].bc == "from-two");
+    CHECK(out[r].mx == double(N - 1) + double(10 * (N - 1)));
+    CHECK(out[r].sm == double(N * (N + 1) / 2));
+    CHECK(out[r].ag.size() == size_t(N));
+    for (int q = 0; q < N && q < int(out[r].ag.size()); ++q) CHECK(out[r].ag[q] == "r" + std::to_string(q));
+    CHECK(out[r].sims == (r == 0 ? size_t(12) : size_t(0)));
+  }
+  CHECK(out[0].best > 0);
 }
 
 TEST(runs_test_behaviour) {

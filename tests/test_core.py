@@ -35,6 +35,21 @@ def test_native_unit_suite():
     assert "0 failures" in r.stderr
 
 
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_native_unit_suite_under_sanitizers(kind):
+    """the host core (graph, synchronizer, solvers, TCP control plane with ranks as
+    threads) under AddressSanitizer + UBSan and under ThreadSanitizer. Any report fails."""
+    from tenzing_amd import _build
+
+    exe = _build.build_sanitized(kind)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "0 failures" in r.stderr
+    assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
+
+
 def test_noop_graph(tz):
     g = tz.Graph()
     op1 = tz.NoOp("op1")
