@@ -76,7 +76,10 @@ def cmd_search(a) -> int:
     if a.dump_graph and ctrl.rank == 0:
         with open(a.dump_graph, "w") as f:
             f.write(g.dump_graphviz(a.workload))
-    plat = tz.Platform(a.streams)
+    distinct = a.cu_partition or bool(a.stream_priorities)
+    # CU-masked or prioritized streams are distinguishable resources: binding an op to stream 0
+    # or 1 is then a real choice, so the symmetric-stream pruning is off
+    plat = tz.Platform(a.streams, symmetric_streams=not distinct)
     bo = tz.BenchOpts(n_iters=a.bench_iters, max_retries=a.max_retries, target_secs=a.target_secs)
     rt = None
     if a.replay:
@@ -88,7 +91,9 @@ def cmd_search(a) -> int:
         bench = tz.SimBenchmarker(a.streams)
     else:
         mode = tz.ExecMode.Graph if a.mode == "graph" else tz.ExecMode.Eager
-        rt = tz.HipRuntime(device=device, n_streams=a.streams, mode=mode, watchdog_s=a.watchdog,
+        prio = [int(x) for x in a.stream_priorities.split(",")] if a.stream_priorities else []
+        rt = tz.HipRuntime(device=device, n_streams=a.streams, priorities=prio,
+                           cu_partition=a.cu_partition, mode=mode, watchdog_s=a.watchdog,
                            graph_unroll=a.graph_unroll)
         bench = tz.EmpiricalBenchmarker(rt, ctrl)
     t0 = time.time()
@@ -169,6 +174,10 @@ def main(argv=None) -> int:
     s.add_argument("--mode", default="eager", choices=["eager", "graph"])
     s.add_argument("--graph-unroll", type=int, default=1,
                    help="graph mode: iterations per hipGraph launch while benchmarking")
+    s.add_argument("--cu-partition", action="store_true",
+                   help="give each stream a disjoint, XCD-balanced CU mask")
+    s.add_argument("--stream-priorities", default="",
+                   help="comma-separated HIP stream priorities, one per stream (e.g. -1,0)")
     s.add_argument("--sim", action="store_true", help="discrete-event cost model, no GPU")
     s.add_argument("--replay", default="", help="results CSV to replay instead of running")
     s.add_argument("--seed", type=int, default=0)

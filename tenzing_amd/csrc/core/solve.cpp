@@ -3,6 +3,9 @@
 #include <algorithm>
 #include <cmath>
 #include <csignal>
+#include <cstdio>
+#include <cstring>
+#include <unistd.h>
 #include <fstream>
 #include <iostream>
 #include <limits>
@@ -508,8 +511,18 @@ SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &ben
         stop = 3;
         result.stop_reason = "time_budget";
       }
+      if (opts.trap_signals && signal_pending()) {
+        stop = 4;
+        result.stop_reason = "signal";
+      }
     }
     stop = ctrl.bcast_int(stop, 0);
+    if (stop == 4) {
+      // trapped signal on rank 0: every rank leaves together, rank 0 dumps the partial results
+      ctrl.barrier();
+      if (root) handle_pending_signal();
+      std::exit(1);
+    }
     if (stop) break;
 
     std::string msg;
@@ -688,7 +701,13 @@ SearchResult dfs_explore(const Graph &g, const Platform &plat, Benchmarker &benc
   if (root && opts.trap_signals) register_handler(dump);
   for (size_t i = 0;; ++i) {
     int64_t stop = root ? int64_t(i >= seqs.size()) : 0;
+    if (root && opts.trap_signals && signal_pending()) stop = 4;
     stop = ctrl.bcast_int(stop, 0);
+    if (stop == 4) {
+      ctrl.barrier();
+      if (root) handle_pending_signal();
+      std::exit(1);
+    }
     if (stop) break;
     std::string msg;
     if (root) msg = seqs[i].json(true).dump();
@@ -716,24 +735,50 @@ SearchResult dfs_explore(const Graph &g, const Platform &plat, Benchmarker &benc
 
 namespace {
 std::function<void(int)> g_handler;
+volatile std::sig_atomic_t g_pending = 0;
+struct sigaction g_old[3];
+const int kTrapped[3] = {SIGINT, SIGTERM, SIGABRT};
+bool g_installed = false;
+
 void trap_fn(int sig) {
-  if (g_handler) g_handler(sig);
-  std::_Exit(1);
+  // async-signal-safe: only flag the signal (the search loop dumps between candidates); a
+  // second signal while the first is pending ends the process at once
+  if (g_pending) {
+    static const char msg[] = "[tz] second signal: exiting without dump\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    std::_Exit(1);
+  }
+  g_pending = sig;
 }
 } // namespace
 
 void register_handler(std::function<void(int)> fn) {
   g_handler = std::move(fn);
-  std::signal(SIGINT, trap_fn);
-  std::signal(SIGTERM, trap_fn);
-  std::signal(SIGABRT, trap_fn);
+  g_pending = 0;
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.sa_handler = trap_fn;
+  sigemptyset(&sa.sa_mask);
+  for (int i = 0; i < 3; ++i) sigaction(kTrapped[i], &sa, &g_old[i]);
+  g_installed = true;
 }
 
 void unregister_handler() {
+  // restore whatever was installed before (e.g. Python's own SIGINT handler)
+  if (g_installed)
+    for (int i = 0; i < 3; ++i) sigaction(kTrapped[i], &g_old[i], nullptr);
+  g_installed = false;
   g_handler = nullptr;
-  std::signal(SIGINT, SIG_DFL);
-  std::signal(SIGTERM, SIG_DFL);
-  std::signal(SIGABRT, SIG_DFL);
+}
+
+int signal_pending() { return int(g_pending); }
+
+void handle_pending_signal() {
+  const int sig = int(g_pending);
+  if (g_handler) g_handler(sig);
+  std::cout.flush();
+  std::fflush(stdout);
+  std::exit(1);
 }
 
 std::string version_string() {

@@ -135,8 +135,15 @@ SearchResult dfs_explore(const Graph &g, const Platform &plat, Benchmarker &benc
 // ------------------------------------------------------------------------ misc
 
 /// install SIGINT/SIGTERM/SIGABRT handler that calls fn then exits (reference trap.cpp:11-35)
+/// Signal trap (reference src/trap.cpp:11-35): SIGINT/SIGTERM/SIGABRT only set a flag (the
+/// handler is async-signal-safe); the solvers poll it between candidates, stop collectively,
+/// call `fn` on rank 0 (dump the partial CSV) and exit(1). A second signal exits at once.
 void register_handler(std::function<void(int)> fn);
 void unregister_handler();
+/// the pending trapped signal (0 = none)
+int signal_pending();
+/// rank 0 after a collective signal stop: run the registered handler, then exit(1)
+[[noreturn]] void handle_pending_signal();
 
 /// {"major","minor","patch","hash","args"} (reference reproduce.cpp:22-37)
 Json reproduce_json(const std::vector<std::string> &args);

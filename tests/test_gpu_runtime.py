@@ -120,6 +120,25 @@ def test_graph_mode_iteration_count(tz, gpu, unroll):
         assert torch.all(y == 7.0), y[:, 0]
 
 
+@pytest.mark.parametrize("kind", ["cu_partition", "priorities"])
+def test_distinct_streams_halo_correct(tz, gpu, kind):
+    """CU-masked (disjoint, XCD-balanced) or prioritized streams as distinct resources: the
+    search platform keeps stream bindings apart and every schedule still exchanges correctly"""
+    halo, g = _small_halo(tz, neighbors=26, fuse="groups", order="qxyz", n=48)
+    kw = {"cu_partition": True} if kind == "cu_partition" else {"priorities": [-1, 0, 0]}
+    for m in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+        rt = tz.HipRuntime(device=0, n_streams=3, mode=m, **kw)
+        plat = tz.Platform(3, symmetric_streams=False)
+        for seed in range(3):
+            seq = tz.random_rollout(tz.State(g, plat), seed)
+            halo.init_grid()
+            rt.prepare(seq)
+            assert rt.effective_mode == m
+            rt.run(2)
+            rt.device_sync()
+            assert halo.check_grid() == 0
+
+
 def test_halo_rccl_self_exchange(tz, gpu):
     """RCCL transport on a 1-rank communicator (self send/recv in a group)."""
     halo, g = _small_halo(tz, neighbors=6, transport="rccl")

@@ -156,3 +156,38 @@ def test_halo_schedule_bcast_8ranks(tmp_path):
         assert len(r["nbrs"]) == 26
     coords = {tuple(r["coords"]) for r in rs}
     assert len(coords) == 8
+
+
+def test_sigint_on_rank0_stops_every_rank(tmp_path):
+    """reference trap.cpp / mcts.hpp:175-178 on several ranks: a signal to the search master
+    stops the search collectively (stop flag broadcast); rank 0 prints the partial results CSV,
+    every rank exits 1, none hangs in a collective"""
+    import signal
+    import subprocess
+    import time
+
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "tenzing_amd", "search", "--workload", "halo", "--sim",
+             "--neighbors", "26", "--streams", "2", "--iters", "100000000", "--bench-iters", "2"],
+            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    try:
+        time.sleep(12.0)
+        assert all(p.poll() is None for p in procs)
+        procs[0].send_signal(signal.SIGINT)
+        outs = [p.communicate(timeout=60) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert [p.returncode for p in procs] == [1, 1], [o[1][-1500:] for o in outs]
+    # (the launcher's rendezvous may print its own "[Gloo] ..." lines first)
+    lines = [x for x in outs[0][0].strip().splitlines() if not x.startswith("[Gloo]")]
+    assert json.loads(lines[0])["mcts__Opts"]["nIters"] == 100000000, outs[0][0][:500]
+    assert len(lines) >= 2 and all(len(x.split("|")) > 7 for x in lines[1:])
+    # only the search master prints results
+    assert [x for x in outs[1][0].strip().splitlines() if not x.startswith("[Gloo]")] == []
