@@ -413,7 +413,32 @@ void HaloExchange::setup(Ctrl *ctrl) {
     const int n = a_.comms > 0 ? std::min(a_.comms, ndirs()) : ndirs();
     int dev = 0;
     TZ_HIP(hipGetDevice(&dev));
-    comms_ = make_rccl_comms(*ctrl, dev, n);
+    // collective agreement like IPC: if any rank cannot create its communicators (e.g. several
+    // ranks on one GPU: RCCL refuses duplicate devices), nobody uses RCCL. With "auto" the IPC
+    // puts remain; a forced "rccl" transport is an error.
+    std::string why;
+    try {
+      comms_ = make_rccl_comms(*ctrl, dev, n);
+    } catch (const std::exception &e) {
+      why = e.what();
+      comms_.clear();
+    }
+    double failed = why.empty() ? 0.0 : 1.0;
+    ctrl->allreduce_max(&failed, 1);
+    if (failed != 0.0) {
+      comms_.clear();
+      TZ_LOG(Warn, "RCCL transport unavailable" << (why.empty() ? " on another rank" : ": " + why));
+      TZ_CHECK(a_.transport == "auto" && useIpc_ && ipcReady_,
+               "RCCL transport unavailable and no IPC fallback: " << why);
+      useRccl_ = false;
+      for (int i = 0; i < ndirs(); ++i) {
+        if (pipe_[i]) {
+          pipe_[i] = false;
+          send_[i] = DeviceBuffer();
+          if (ipcGrid_) recv_[i] = DeviceBuffer();
+        }
+      }
+    }
   }
   init_grid();
   if (useIpc_ && ipcReady_) {

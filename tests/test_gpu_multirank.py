@@ -61,3 +61,22 @@ def test_ipc_halo_loopback(gpu, world, mode):
             assert run["bad1"] == 0 and run["bad2"] == 0 and run["err"] == 0, run
             # 2 ranks: grid 1x1x2 (x, y self-neighbours move directly); 4 ranks: 1x2x2
             assert run["transport"] == "direct+ipc"
+
+
+def test_bench_two_ranks_loopback(gpu, tmp_path):
+    """the driver's multi-GPU bench flow (torchrun, one process per rank, collective search,
+    best-schedule broadcast, device-side verification, eager + hipGraph timing, max over ranks)
+    with both ranks on this one GPU. RCCL refuses two ranks on one device, so this also checks
+    the collective fallback to the IPC transport."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+           "--cells", "64", "--mcts-iters", "6", "--bench-iters", "3", "--deadline-s", "240"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    j = json.loads(line)
+    assert j["n_gpus"] == 2 and j["steps"] == 6 and j["verified_bad_cells"] == 0
+    assert j["transport"] == "direct+ipc" and j["config"]["rank_grid"] == [1, 1, 2]
+    assert j["value"] > 0 and j["higher_is_better"] is False
