@@ -323,6 +323,8 @@ public:
   virtual void device_sync() = 0;
   /// native handle (hipStream_t) of a logical stream, or nullptr when simulated
   virtual void *native_stream(int stream) { (void)stream; return nullptr; }
+  /// logical index of a native stream handle (-1 if it is not one of this executor's)
+  virtual int stream_index(const void *native) const { (void)native; return -1; }
 };
 
 } // namespace tz

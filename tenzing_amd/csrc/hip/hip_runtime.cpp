@@ -128,6 +128,12 @@ void *HipRuntime::native_stream(int stream) {
   return streams_[stream];
 }
 
+int HipRuntime::stream_index(const void *native) const {
+  for (size_t i = 0; i < streams_.size(); ++i)
+    if (streams_[i] == native) return int(i);
+  return -1;
+}
+
 void HipRuntime::launch(const GpuOp &op, int stream) { op.launch(native_stream(stream), *this); }
 
 void HipRuntime::event_record(int e, int stream) {

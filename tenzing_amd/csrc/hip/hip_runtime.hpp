@@ -60,6 +60,7 @@ public:
   void stream_wait(int waiter, int waitee) override;
   void device_sync() override;
   void *native_stream(int stream) override;
+  int stream_index(const void *native) const override;
 
   // ExecutorRunner
   void prepare(const Sequence &seq) override;

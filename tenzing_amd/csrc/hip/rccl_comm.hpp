@@ -6,8 +6,10 @@
 // not a host round trip) and RCCL kernels can be captured into hipGraphs. Because RCCL
 // point-to-point has no tags and a pending send occupies its stream until the peer posts the
 // matching receive, every exchange is issued as one ncclGroupStart/End group (deadlock-free on
-// periodic rings), and the reference's per-direction MPI tags become one communicator per
-// direction: transfers of different directions use different xGMI links and can overlap.
+// periodic rings). The reference's MPI tags are not needed: a transfer uses the communicator of
+// the logical stream it runs on (a few communicators per exchange), every rank runs the same
+// schedule, so each communicator sees the same order of groups on every rank, and transfers on
+// different streams (different communicators) can overlap.
 // Communicator unique ids are distributed over the host control plane (Ctrl).
 #pragma once
 

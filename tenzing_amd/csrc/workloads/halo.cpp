@@ -81,7 +81,7 @@ public:
   double cost_us() const override {
     return h_->uses_rccl() ? 8.0 + bytes() / 1.0e5 : 3.0 + bytes() / 2.5e6;
   }
-  void launch(void *s, Executor &) const override { h_->shift(i_, s); }
+  void launch(void *s, Executor &ex) const override { h_->shift(i_, s, ex.stream_index(s)); }
 
 private:
   std::shared_ptr<const HaloExchange> h_;
@@ -161,9 +161,9 @@ public:
     if (st_ == Shift) return h_->uses_rccl() ? 10.0 + bytes() / 3.0e5 : 3.0 + bytes() / 2.5e6;
     return copy_cost_us(bytes());
   }
-  void launch(void *s, Executor &) const override {
+  void launch(void *s, Executor &ex) const override {
     if (st_ == Pack) h_->pack_group(dirs_, s);
-    else if (st_ == Shift) h_->shift_group(dirs_, s);
+    else if (st_ == Shift) h_->shift_group(dirs_, s, ex.stream_index(s));
     else if (st_ == Unpack) h_->unpack_group(dirs_, s);
     else if (st_ == Direct) h_->direct_group(dirs_, s);
     else if (st_ == Put) h_->put_group(dirs_, s);
@@ -410,7 +410,7 @@ void HaloExchange::setup(Ctrl *ctrl) {
   if (useRccl_) {
     TZ_CHECK(ctrl && ctrl->size() == a_.size, "RCCL transport needs a control plane of size "
                                                   << a_.size);
-    const int n = a_.comms > 0 ? std::min(a_.comms, ndirs()) : ndirs();
+    const int n = a_.comms > 0 ? a_.comms : kDefaultComms;
     int dev = 0;
     TZ_HIP(hipGetDevice(&dev));
     // collective agreement like IPC: if any rank cannot create its communicators (e.g. several
@@ -701,13 +701,22 @@ void HaloExchange::unpack(int i, void *stream) const {
   kern::box_copy(grid(), unpack_box(i), true, stream);
 }
 
-void HaloExchange::shift(int i, void *stream) const {
+const RcclComm &HaloExchange::comm_for(int streamIdx, int dir) const {
+  TZ_CHECK(!comms_.empty(), "no RCCL communicators");
+  // every rank runs the same schedule, so an op lands on the same logical stream, hence the
+  // same communicator, on every rank, and each communicator sees its operations in the same
+  // order everywhere (RCCL's matching rule)
+  const int k = streamIdx >= 0 ? streamIdx : dir;
+  return *comms_[size_t(k) % comms_.size()];
+}
+
+void HaloExchange::shift(int i, void *stream, int streamIdx) const {
   check_pipelined(i);
   // send my slab facing d to nbr(d); receive nbr(-d)'s slab facing d into my ghost on side -d
   const int o = opp_[i];
   const size_t n = box_elems(i);
   if (useRccl_) {
-    const RcclComm &c = *comms_[size_t(i) % comms_.size()];
+    const RcclComm &c = comm_for(streamIdx, i);
     c.sendrecv(send_[i].get(), n, nbr_[i], recv_[o].get(), n, nbr_[o], 1, stream);
   } else {
     // self neighbour: device copy kernel (captures as a kernel node, unlike hipMemcpyAsync)
@@ -755,7 +764,7 @@ void HaloExchange::unpack_group(const std::vector<int> &dirs, void *stream) cons
                         true, stream);
 }
 
-void HaloExchange::shift_group(const std::vector<int> &dirs, void *stream) const {
+void HaloExchange::shift_group(const std::vector<int> &dirs, void *stream, int streamIdx) const {
   if (dirs.empty()) return;
   for (int i : dirs) check_pipelined(i);
   if (useRccl_) {
@@ -765,9 +774,7 @@ void HaloExchange::shift_group(const std::vector<int> &dirs, void *stream) const
       const size_t n = box_elems(i);
       xs.push_back({send_[i].get(), n, nbr_[i], recv_[o].get(), n, nbr_[o]});
     }
-    // one communicator per group (the group's first direction's), so concurrently scheduled
-    // groups never share a communicator
-    comms_[size_t(dirs.front()) % comms_.size()]->exchange(xs, 1, stream);
+    comm_for(streamIdx, dirs.front()).exchange(xs, 1, stream);
   } else {
     std::vector<kern::CopyDesc> cs;
     for (int i : dirs) cs.push_back({recv_[opp_[i]].get(), send_[i].get(), box_elems(i) * sizeof(double)});

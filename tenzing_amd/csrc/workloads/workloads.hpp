@@ -109,7 +109,10 @@ struct HaloArgs {
   // "none": per-direction ops; "groups": fused per group; "pack": fused pack+unpack with
   // per-direction transfers; "all": one op per stage
   std::string fuse = "choice";
-  int comms = 0;                  // RCCL communicators (0 = one per direction)
+  // RCCL communicators (0 = kDefaultComms). A transfer uses the communicator of the logical
+  // stream it runs on, so transfers on different streams never share one (RCCL serializes
+  // operations of one communicator) and a whole exchange needs only a few communicators
+  int comms = 0;
   int rank = 0, size = 1;
   int px = 0, py = 0, pz = 0;     // rank grid (0 = from prime factors, reference style)
   int pitch_pad = 0;              // extra row-pitch elements (multiple of 16: keeps alignment)
@@ -157,14 +160,15 @@ public:
   // op bodies
   void pack(int i, void *stream) const;
   void unpack(int i, void *stream) const;
-  void shift(int i, void *stream) const;
+  /// `streamIdx`: the executor's logical stream (selects the RCCL communicator; -1: by direction)
+  void shift(int i, void *stream, int streamIdx = -1) const;
   void pack_all(void *stream) const;
   void unpack_all(void *stream) const;
   void shift_all(void *stream) const;
   /// one launch / one RCCL group for a set of directions (unpack: their opposite ghosts)
   void pack_group(const std::vector<int> &dirs, void *stream) const;
   void unpack_group(const std::vector<int> &dirs, void *stream) const;
-  void shift_group(const std::vector<int> &dirs, void *stream) const;
+  void shift_group(const std::vector<int> &dirs, void *stream, int streamIdx = -1) const;
   std::vector<int> all_dirs() const;
   /// directions that go through pack -> transfer -> unpack (not direct)
   std::vector<int> pipelined_dirs() const;
@@ -231,6 +235,8 @@ private:
   DeviceBuffer expected_, done_, err_;
   DeviceBuffer sent_; // per direction: puts issued so far (credit wait bookkeeping)
   std::vector<unsigned long long *> credit_ptrs(const std::vector<int> &dirs) const;
+  const RcclComm &comm_for(int streamIdx, int dir) const;
+  static constexpr int kDefaultComms = 8;
   bool ipcGrid_ = true;
   std::vector<void *> peerGrid_, peerFlags_; // per rank (nullptr: not a neighbour / self)
   std::vector<void *> peerRecv_;             // per direction: the receiver's buffer ("buffers")
