@@ -396,7 +396,10 @@ PYBIND11_MODULE(_tz, m) {
       .def("run", &ExecutorRunner::run, py::call_guard<py::gil_scoped_release>());
   py::class_<HostExecutor, ExecutorRunner>(m, "HostExecutor", py::multiple_inheritance()).def(py::init<int>());
   py::class_<EmpiricalBenchmarker, Benchmarker>(m, "EmpiricalBenchmarker")
-      .def(py::init<ExecutorRunner &, Ctrl &>(), py::keep_alive<1, 2>(), py::keep_alive<1, 3>());
+      .def(py::init<ExecutorRunner &, Ctrl &>(), py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("benchmark_many", &EmpiricalBenchmarker::benchmark_many, py::arg("seqs"), py::arg("opts"),
+           py::arg("seed") = 0, py::call_guard<py::gil_scoped_release>(),
+           "interleaved measurement of several schedules (random order per iteration)");
 
   // ------------------------------------------------------------------ control plane
   py::class_<Ctrl, std::shared_ptr<Ctrl>>(m, "Ctrl")

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 
@@ -64,8 +65,23 @@ EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, d
   }
 }
 
+void EmpiricalBenchmarker::collective_prepare(const std::function<void()> &fn) {
+  // preparation (event provisioning, hipGraph compilation) is local and may fail on one rank
+  // only; every rank must then leave together instead of entering mismatched collectives
+  std::string err;
+  try {
+    fn();
+  } catch (const std::exception &e) {
+    err = e.what();
+  }
+  double bad = err.empty() ? 0.0 : 1.0;
+  if (ctrl_.size() > 1) ctrl_.allreduce_max(&bad, 1);
+  if (bad != 0.0)
+    TZ_THROW("schedule preparation failed" << (err.empty() ? " on another rank" : ": " + err));
+}
+
 BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts &opts) {
-  runner_.prepare(seq);
+  collective_prepare([&] { runner_.prepare(seq); });
   std::vector<double> times;
   int retries = 0;
   int64_t hint = 1;
@@ -90,6 +106,45 @@ BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts
   r.samples_per_measurement = hint;
   r.retries = retries;
   return r;
+}
+
+std::vector<BenchResult> EmpiricalBenchmarker::benchmark_many(const std::vector<Sequence> &seqs,
+                                                              const BenchOpts &opts, uint64_t seed) {
+  const size_t k = seqs.size();
+  std::vector<BenchResult> out(k);
+  if (k == 0) return out;
+  collective_prepare([&] { runner_.prepare_many(seqs); });
+  // warm each schedule up and size its batch once
+  std::vector<int64_t> hint(k, 1);
+  for (size_t i = 0; i < k; ++i) {
+    runner_.select(i);
+    hint[i] = measure(1, opts.target_secs).n;
+  }
+  std::vector<std::vector<double>> times(k);
+  std::mt19937_64 rng(seed + 0x5EEDull);
+  std::vector<int> perm(k);
+  for (int64_t it = 0; it < std::max<int64_t>(1, opts.n_iters); ++it) {
+    std::string msg;
+    if (ctrl_.rank() == 0) {
+      for (size_t i = 0; i < k; ++i) perm[i] = int(i);
+      std::shuffle(perm.begin(), perm.end(), rng);
+      msg.assign(reinterpret_cast<const char *>(perm.data()), k * sizeof(int));
+    }
+    ctrl_.bcast(msg, 0);
+    TZ_CHECK(msg.size() == k * sizeof(int), "permutation broadcast truncated");
+    std::memcpy(perm.data(), msg.data(), msg.size());
+    for (int i : perm) {
+      runner_.select(size_t(i));
+      Measurement m = measure(hint[size_t(i)], opts.target_secs);
+      hint[size_t(i)] = std::max(hint[size_t(i)], m.n);
+      times[size_t(i)].push_back(m.time);
+    }
+  }
+  for (size_t i = 0; i < k; ++i) {
+    out[i] = BenchResult::from_times(times[i]);
+    out[i].samples_per_measurement = hint[i];
+  }
+  return out;
 }
 
 void HostExecutor::run(int64_t n) {

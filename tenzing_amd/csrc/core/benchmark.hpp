@@ -13,6 +13,7 @@
 #include "serdes.hpp"
 #include "state.hpp"
 
+#include <functional>
 #include <map>
 #include <random>
 #include <string>
@@ -52,12 +53,25 @@ public:
   virtual void prepare(const Sequence &seq) = 0;
   /// run the prepared sequence `n` times back to back (host returns when all work is done)
   virtual void run(int64_t n) = 0;
+  /// provision several sequences at once; select(k) makes the k-th the one run() executes
+  /// (interleaved benchmarking). Default: re-prepare on every select.
+  virtual void prepare_many(const std::vector<Sequence> &seqs) { many_ = seqs; }
+  virtual void select(size_t k) { prepare(many_.at(k)); }
+
+private:
+  std::vector<Sequence> many_;
 };
 
 class EmpiricalBenchmarker : public Benchmarker {
 public:
   EmpiricalBenchmarker(ExecutorRunner &runner, Ctrl &ctrl) : runner_(runner), ctrl_(ctrl) {}
   BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) override;
+  /// Several schedules measured interleaved (reference src/benchmarker.cpp:21-76): every
+  /// iteration runs each schedule once (one batched measurement) in a random order chosen by
+  /// rank 0 and broadcast, so slow drift (clocks, thermals, other tenants) spreads evenly over
+  /// the schedules instead of biasing whichever ran last. Times are max over ranks.
+  std::vector<BenchResult> benchmark_many(const std::vector<Sequence> &seqs, const BenchOpts &opts,
+                                          uint64_t seed = 0);
 
 private:
   struct Measurement {
@@ -65,6 +79,7 @@ private:
     double time;
   };
   Measurement measure(int64_t nHint, double targetSecs);
+  void collective_prepare(const std::function<void()> &fn);
   ExecutorRunner &runner_;
   Ctrl &ctrl_;
 };

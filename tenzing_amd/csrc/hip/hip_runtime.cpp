@@ -178,6 +178,17 @@ void HipRuntime::stream_wait(int waiter, int waitee) {
 void HipRuntime::device_sync() { TZ_HIP(hipDeviceSynchronize()); }
 
 void HipRuntime::destroy_graph() {
+  if (!slots_.empty()) {
+    // the current graphs are borrowed from a slot
+    for (Slot &s : slots_) {
+      if (s.exec) hipGraphExecDestroy(static_cast<hipGraphExec_t>(s.exec));
+      if (s.execU) hipGraphExecDestroy(static_cast<hipGraphExec_t>(s.execU));
+    }
+    slots_.clear();
+    graphExec_ = graphExecU_ = nullptr;
+    graphNodes_ = graphEdges_ = 0;
+    return;
+  }
   if (graphExec_) {
     hipGraphExecDestroy(static_cast<hipGraphExec_t>(graphExec_));
     graphExec_ = nullptr;
@@ -313,6 +324,46 @@ void HipRuntime::prepare(const Sequence &seq) {
     graphExec_ = build_graph(1, graphNodes_, graphEdges_);
     if (unroll_ > 1) graphExecU_ = build_graph(unroll_, n, e);
   }
+}
+
+void HipRuntime::prepare_many(const std::vector<Sequence> &seqs) {
+  destroy_graph();
+  std::vector<Slot> slots;
+  try {
+    for (const Sequence &s : seqs) {
+      prepare(s); // compiles into graphExec_ / graphExecU_ (owned here until moved)
+      Slot sl;
+      sl.seq = s;
+      sl.exec = graphExec_;
+      sl.execU = graphExecU_;
+      sl.nodes = graphNodes_;
+      sl.edges = graphEdges_;
+      graphExec_ = graphExecU_ = nullptr;
+      slots.push_back(std::move(sl));
+    }
+  } catch (...) {
+    for (Slot &s : slots) {
+      if (s.exec) hipGraphExecDestroy(static_cast<hipGraphExec_t>(s.exec));
+      if (s.execU) hipGraphExecDestroy(static_cast<hipGraphExec_t>(s.execU));
+    }
+    throw;
+  }
+  slots_ = std::move(slots);
+  int events = 1;
+  for (const Slot &s : slots_) events = std::max(events, s.seq.num_events());
+  event(events - 1);
+  if (!slots_.empty()) select(0);
+}
+
+void HipRuntime::select(size_t k) {
+  TZ_CHECK(k < slots_.size(), "slot " << k << " out of range (" << slots_.size() << ")");
+  const Slot &s = slots_[k];
+  seq_ = s.seq;
+  graphExec_ = s.exec;
+  graphExecU_ = s.execU;
+  graphNodes_ = s.nodes;
+  graphEdges_ = s.edges;
+  internalUsed_ = 0;
 }
 
 void HipRuntime::run(int64_t n) {

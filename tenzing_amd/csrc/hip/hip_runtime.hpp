@@ -65,6 +65,9 @@ public:
   // ExecutorRunner
   void prepare(const Sequence &seq) override;
   void run(int64_t n) override;
+  /// graph mode: every sequence is compiled once and kept; select() switches without rebuilding
+  void prepare_many(const std::vector<Sequence> &seqs) override;
+  void select(size_t k) override;
 
   void set_mode(ExecMode m);
   ExecMode mode() const { return mode_; }
@@ -104,6 +107,12 @@ private:
   int unroll_ = 1;
   bool spinSync_ = true;
   size_t graphNodes_ = 0, graphEdges_ = 0;
+  struct Slot {
+    Sequence seq;
+    void *exec = nullptr, *execU = nullptr;
+    size_t nodes = 0, edges = 0;
+  };
+  std::vector<Slot> slots_; // prepare_many: own the compiled graphs (graphExec_ borrows)
 
   double watchdogS_ = 0;
   std::atomic<double> deadline_{0};

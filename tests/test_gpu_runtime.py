@@ -139,6 +139,24 @@ def test_distinct_streams_halo_correct(tz, gpu, kind):
             assert halo.check_grid() == 0
 
 
+def test_benchmark_many_graph_slots(tz, gpu):
+    """interleaved benchmarking keeps one compiled hipGraph per schedule (switching slots does
+    not rebuild), and the runtime returns to single-schedule use afterwards"""
+    halo, g = _small_halo(tz, neighbors=26, fuse="choice", order="qxyz", n=64)
+    seqs = [tz.random_rollout(tz.State(g, tz.Platform(3)), s) for s in range(4)]
+    rt = tz.HipRuntime(device=0, n_streams=3, mode=tz.ExecMode.Graph, graph_unroll=4)
+    bench = tz.EmpiricalBenchmarker(rt, tz.SelfCtrl())
+    res = bench.benchmark_many(seqs, tz.BenchOpts(n_iters=5, max_retries=1, target_secs=0.001))
+    assert len(res) == 4 and all(0 < r.pct10 < 5e-3 for r in res)
+    assert rt.effective_mode == tz.ExecMode.Graph
+    for seq in seqs:
+        halo.init_grid()
+        rt.prepare(seq)
+        rt.run(3)
+        rt.device_sync()
+        assert halo.check_grid() == 0
+
+
 def test_halo_rccl_self_exchange(tz, gpu):
     """RCCL transport on a 1-rank communicator (self send/recv in a group)."""
     halo, g = _small_halo(tz, neighbors=6, transport="rccl")

@@ -101,6 +101,26 @@ def test_host_ops_empirical(tz):
         assert 350e-6 < s.res.pct50 < 5e-3
 
 
+def test_benchmark_many_interleaved(tz):
+    """reference src/benchmarker.cpp:21-76: several schedules measured in a random order per
+    iteration; each keeps its own batch size and distribution"""
+    seqs = []
+    for us in (400.0, 100.0, 200.0):
+        g = tz.Graph()
+        op = tz.SleepOp(f"s{int(us)}", us)
+        g.start_then(op)
+        g.then_finish(op)
+        seqs.append(tz.random_rollout(tz.State(g, tz.Platform(1)), 0))
+    bench = tz.EmpiricalBenchmarker(tz.HostExecutor(1), tz.SelfCtrl())
+    res = bench.benchmark_many(seqs, tz.BenchOpts(n_iters=6, max_retries=1, target_secs=0.003),
+                               seed=1)
+    assert len(res) == 3
+    p50 = [r.pct50 for r in res]
+    assert p50[1] < p50[2] < p50[0]
+    assert 380e-6 < p50[0] < 2e-3 and 90e-6 < p50[1] < 1e-3
+    assert all(r.samples_per_measurement >= 1 for r in res)
+
+
 def test_pycpuop_callback(tz):
     calls = []
     g = tz.Graph()
