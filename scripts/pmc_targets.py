@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Fixed set of kernel launches for rocprofv3 counter collection (--pmc): the halo direct move
-(all 26 directions), fused pack / unpack, and the SpMV kernels, each a few times.
+(all 26 directions), fused pack / unpack, the SpMV kernels and rocSPARSE's CSR SpMV, each a
+few times.
 
   rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --output-format csv -d out -- python3 scripts/pmc_targets.py
 """
@@ -34,10 +35,13 @@ def main():
     v_t = torch.tensor(val, dtype=torch.float32, device="cuda")
     x = torch.randn(m, device="cuda")
     y = torch.zeros(m, device="cuda")
+    lib = tz._tz.kernels.RocsparseCsr(m, m, ci_t.numel(), rp_t.data_ptr(), ci_t.data_ptr(),
+                                      v_t.data_ptr(), x.data_ptr(), y.data_ptr(), "adaptive")
     for _ in range(3):
         for lanes in (8, -1):
             tz._tz.kernels.csr_spmv(m, rp_t.data_ptr(), ci_t.data_ptr(), v_t.data_ptr(),
                                     x.data_ptr(), y.data_ptr(), lanes, False, st)
+        lib.run(st)  # rocSPARSE (library comparison)
     torch.cuda.synchronize()
 
 
