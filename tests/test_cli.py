@@ -94,3 +94,11 @@ def test_cpulist_parsing_and_binding(monkeypatch):
     monkeypatch.setattr(env, "local_cpus", lambda dev: [])
     assert env.bind_local_cpus(0) == []
     assert sorted(os.sched_getaffinity(0)) == allowed
+
+
+def test_example_sim_design_rules(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "sim_design_rules.py"),
+                        "--out", str(tmp_path / "ex_")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "24 schedules" in r.stdout and "b and c same stream" in r.stdout
+    assert (tmp_path / "ex_rules.txt").exists()

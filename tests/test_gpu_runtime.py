@@ -296,3 +296,22 @@ def test_native_cli_halo_and_spmv_on_gpu(tz, gpu, tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads(r.stderr.strip().splitlines()[-1])["candidates"] == 12
+
+
+def test_example_torch_overlap(gpu):
+    """examples/torch_overlap.py: MCTS over torch ops (hipBLASLt GEMM, DMA copy, reductions)
+    finds the two-stream overlap"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "examples", "torch_overlap.py"),
+                        "--iters", "16"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["candidates"] == 16
+    # overlapping the copy chain with the GEMM chain beats running them back to back
+    assert j["best_ms"] < 0.9 * j["worst_ms"], j
+    bs = j["best_streams"]
+    assert bs["gemm"] != bs["h2d"], j
