@@ -25,7 +25,7 @@ def _build_workload(a, ctrl, device, setup):
 
     hc = HaloConfig(n=a.halo_n, nq=a.nq, ghost=a.ghost, neighbors=a.neighbors, order=a.order,
                     fuse=a.fuse, transport=a.transport)
-    sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form)
+    sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport)
     if a.workload == "halo":
         h, g = build_halo(hc, ctrl, device, setup)
         return g, {"halo": h}
@@ -199,6 +199,7 @@ def main(argv=None) -> int:
     s.add_argument("--transport", default="auto")
     s.add_argument("--spmv-m", type=int, default=150_000)
     s.add_argument("--spmv-form", default="choice", choices=["choice", "split", "accum"])
+    s.add_argument("--spmv-transport", default="auto", choices=["auto", "rccl", "ipc"])
     s.set_defaults(fn=cmd_search)
     r = sub.add_parser("rules")
     r.add_argument("results")

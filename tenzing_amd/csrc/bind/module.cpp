@@ -642,6 +642,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("kernel_choice", &SpmvArgs::kernel_choice)
       .def_readwrite("form", &SpmvArgs::form)
       .def_readwrite("library", &SpmvArgs::library)
+      .def_readwrite("transport", &SpmvArgs::transport)
       .def_readwrite("prefix", &SpmvArgs::prefix)
       .def("json", [](const SpmvArgs &a) { return a.json().dump(); });
   py::class_<DistSpmv, std::shared_ptr<DistSpmv>>(m, "DistSpmv")
@@ -653,6 +654,10 @@ PYBIND11_MODULE(_tz, m) {
       .def("remote_cols", &DistSpmv::remote_cols)
       .def("send_elems", &DistSpmv::send_elems)
       .def("num_peers", &DistSpmv::num_peers)
+      .def("transport", &DistSpmv::transport)
+      .def("uses_ipc", &DistSpmv::uses_ipc)
+      .def("uses_rccl", &DistSpmv::uses_rccl)
+      .def("ipc_errors", &DistSpmv::ipc_errors, py::call_guard<py::gil_scoped_release>())
       .def("setup", [](DistSpmv &s, Ctrl *c) { s.setup(c); }, py::arg("ctrl") = nullptr,
            py::call_guard<py::gil_scoped_release>())
       .def("ready", &DistSpmv::ready)

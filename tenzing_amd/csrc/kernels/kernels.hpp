@@ -96,6 +96,17 @@ void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const flo
               const float *x, float *y, int lanesPerRow, bool accumulate, void *stream);
 /// dst[i] = src[idx[i]]
 void gather_f32(int n, const float *src, const int32_t *idx, float *dst, void *stream);
+/// one peer's part of an IPC put of the SpMV x halo: dst[i] = src[idx[off + i]], i < n, then
+/// *flag += 1 (system scope) once the whole segment is visible
+struct PutSeg {
+  float *dst = nullptr;
+  int32_t off = 0, n = 0;
+  unsigned long long *flag = nullptr;
+};
+constexpr int kMaxPutPeers = 64;
+/// all peers' segments in one launch; `done` holds one zeroed completion counter per segment
+void gather_put_signal(const float *src, const int32_t *idx, const PutSeg *segs, int nseg,
+                       unsigned int *done, void *stream);
 /// y = a + b (f32, vectorized)
 void vector_add_f32(int n, const float *a, const float *b, float *y, void *stream);
 /// y += alpha * x (f64)

@@ -107,6 +107,37 @@ __global__ __launch_bounds__(kThreads) void gather_k(int n, const float *__restr
     dst[i] = src[idx[i]];
 }
 
+struct DevPutBatch {
+  const float *src;
+  const int32_t *idx;
+  unsigned int *done;
+  int32_t nseg;
+  uint32_t block_start[kMaxPutPeers + 1];
+  PutSeg seg[kMaxPutPeers];
+};
+
+// IPC put of the SpMV x halo: each segment gathers x[idx[off + i]] straight into a peer's
+// (IPC-mapped) remote-x buffer; the segment's last block publishes it with one system-scope
+// increment of the peer's arrival counter (same protocol as the halo puts)
+__global__ __launch_bounds__(kThreads) void gather_put_k(DevPutBatch b) {
+  int s = 0;
+  while (s + 1 < b.nseg && blockIdx.x >= b.block_start[s + 1]) ++s;
+  const PutSeg &g = b.seg[s];
+  const uint32_t nb = b.block_start[s + 1] - b.block_start[s];
+  const uint32_t tid = (blockIdx.x - b.block_start[s]) * kThreads + threadIdx.x;
+  for (uint32_t i = tid; i < uint32_t(g.n); i += nb * kThreads) g.dst[i] = b.src[b.idx[g.off + i]];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int prev = atomicAdd(&b.done[s], 1u);
+    if (prev == nb - 1) {
+      b.done[s] = 0; // ready for the next launch (kernel boundary orders it)
+      __threadfence_system();
+      __hip_atomic_fetch_add(g.flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void vector_add_k(int n, const float *__restrict__ a,
                                                          const float *__restrict__ b,
                                                          float *__restrict__ y) {
@@ -238,6 +269,30 @@ void gather_f32(int n, const float *src, const int32_t *idx, float *dst, void *s
   if (n <= 0) return;
   hipLaunchKernelGGL(gather_k, dim3(grid_for(n)), dim3(kThreads), 0,
                      static_cast<hipStream_t>(stream), n, src, idx, dst);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+void gather_put_signal(const float *src, const int32_t *idx, const PutSeg *segs, int nseg,
+                       unsigned int *done, void *stream) {
+  if (nseg <= 0) return;
+  if (nseg > kMaxPutPeers) throw std::runtime_error("gather_put_signal: too many peers");
+  if (!src || !idx || !done) throw std::runtime_error("gather_put_signal: null pointer");
+  DevPutBatch b{};
+  b.src = src;
+  b.idx = idx;
+  b.done = done;
+  b.nseg = nseg;
+  uint32_t total = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (!segs[i].dst || !segs[i].flag || segs[i].n <= 0 || segs[i].off < 0)
+      throw std::runtime_error("gather_put_signal: bad segment");
+    b.seg[i] = segs[i];
+    b.block_start[i] = total;
+    // enough blocks to stream the segment, few enough that the completion count stays cheap
+    total += uint32_t(std::min<int64_t>(64, (int64_t(segs[i].n) + 4 * kThreads - 1) / (4 * kThreads)));
+  }
+  b.block_start[nseg] = total;
+  hipLaunchKernelGGL(gather_put_k, dim3(total), dim3(kThreads), 0, static_cast<hipStream_t>(stream), b);
   TZ_HIP_LAUNCH_CHECK();
 }
 

@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <random>
 
 namespace tz {
@@ -25,6 +27,7 @@ Json SpmvArgs::json() const {
   j["kernel_choice"] = kernel_choice;
   j["form"] = form;
   j["library"] = library;
+  j["transport"] = transport;
   return j;
 }
 
@@ -137,6 +140,53 @@ private:
   std::string name_;
 };
 
+/// ipc transport: gather my x entries straight into the peers' remote-x buffers (+ signals)
+class SpmvPut : public GpuOp {
+public:
+  SpmvPut(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "SpmvPut"; }
+  double cost_us() const override { return s_->num_peers() ? 6.0 + 4.0 * double(s_->send_elems()) / 5.0e4 : 0.5; }
+  void launch(void *st, Executor &) const override { s_->put(st); }
+
+private:
+  std::shared_ptr<const DistSpmv> s_;
+  std::string name_;
+};
+
+/// ipc transport: device-side wait for the peers' puts into my remote-x buffer
+class SpmvWait : public GpuOp {
+public:
+  SpmvWait(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "SpmvWait"; }
+  double cost_us() const override { return 3.0; }
+  void launch(void *st, Executor &) const override { s_->wait_puts(st); }
+
+private:
+  std::shared_ptr<const DistSpmv> s_;
+  std::string name_;
+};
+
+/// ipc transport: remote product, then the senders' credits go back
+class SpmvRemoteRelease : public GpuOp {
+public:
+  SpmvRemoteRelease(std::shared_ptr<const DistSpmv> s, std::string name, bool accumulate)
+      : s_(std::move(s)), name_(std::move(name)), acc_(accumulate) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "SpmvRemote"; }
+  double cost_us() const override { return s_->remote_nnz() ? 6.0 + 12.0 * double(s_->remote_nnz()) / 3.0e6 : 2.5; }
+  void launch(void *st, Executor &) const override {
+    s_->spmv_remote(st, acc_);
+    s_->release(st);
+  }
+
+private:
+  std::shared_ptr<const DistSpmv> s_;
+  std::string name_;
+  bool acc_;
+};
+
 class SpmvAdd : public GpuOp {
 public:
   SpmvAdd(std::shared_ptr<const DistSpmv> s, std::string name) : s_(std::move(s)), name_(std::move(name)) {}
@@ -219,11 +269,26 @@ DistSpmv::DistSpmv(SpmvArgs a) : a_(std::move(a)) {
   }
   xLocal_.resize(size_t(nl));
   for (int64_t i = 0; i < nl; ++i) xLocal_[size_t(i)] = x_value(r0_ + i);
+  TZ_CHECK(a_.transport == "auto" || a_.transport == "rccl" || a_.transport == "ipc",
+           "SpMV transport must be auto, rccl or ipc (got " << a_.transport << ")");
+  useRccl_ = a_.size > 1 && a_.transport != "ipc";
+  useIpc_ = a_.size > 1 && a_.transport != "rccl";
   const double avg = nl ? double(local_.nnz() + remote_.nnz()) / double(nl) : 1;
   lanes_ = avg > 24 ? 16 : (avg > 6 ? 8 : 4);
 }
 
-DistSpmv::~DistSpmv() = default;
+DistSpmv::~DistSpmv() {
+  for (void *p : opened_) (void)hipIpcCloseMemHandle(p);
+  if (flags_) (void)hipFree(flags_);
+}
+
+std::string DistSpmv::transport() const {
+  if (a_.size == 1) return "none";
+  std::string t;
+  if (useRccl_) t = "rccl";
+  if (useIpc_ && (ipcReady_ || !ready())) t += t.empty() ? "ipc" : "+ipc";
+  return t.empty() ? "none" : t;
+}
 
 int DistSpmv::num_peers() const {
   int n = 0;
@@ -248,16 +313,51 @@ void DistSpmv::setup(Ctrl *ctrl) {
   up(dSendIdx_, sendIdx_.data(), sendIdx_.size() * 4);
   const size_t nl = size_t(local_rows());
   dSend_ = DeviceBuffer(std::max<size_t>(sendIdx_.size() * 4, 16));
-  dXr_ = DeviceBuffer(std::max<size_t>(remoteCols_.size() * 4, 16));
+  // (at least 64 KB: an IPC-exported buffer of its own rather than a sub-allocation)
+  dXr_ = DeviceBuffer(std::max<size_t>(remoteCols_.size() * 4, 65536));
   dYl_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));
   dYr_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));
   dY_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));
   TZ_HIP(hipMemset(dYr_.get(), 0, dYr_.bytes()));
   if (a_.size > 1) {
     TZ_CHECK(ctrl && ctrl->size() == a_.size, "SpMV needs a control plane of size " << a_.size);
-    int dev = 0;
-    TZ_HIP(hipGetDevice(&dev));
-    comm_ = std::make_shared<RcclComm>(*ctrl, dev);
+    // IPC first (collective agreement, preflight), then RCCL with the same collective fallback
+    // as the halo: several ranks on one GPU (loopback) have no RCCL
+    if (useIpc_) {
+      const std::string why = setup_ipc(ctrl);
+      double failed = why.empty() ? 0.0 : 1.0;
+      ctrl->allreduce_max(&failed, 1);
+      ipcReady_ = failed == 0.0;
+      if (!ipcReady_) {
+        TZ_LOG(Warn, "SpMV ipc transport unavailable" << (why.empty() ? " on another rank" : ": " + why));
+        TZ_CHECK(a_.transport != "ipc", "SpMV ipc transport requested but unavailable: " << why);
+      }
+    }
+    if (useIpc_ && ipcReady_) {
+      TZ_HIP(hipDeviceSynchronize());
+      ctrl->barrier();
+      ipc_preflight(ctrl);
+    }
+    if (useRccl_) {
+      int dev = 0;
+      TZ_HIP(hipGetDevice(&dev));
+      std::string why;
+      try {
+        comm_ = std::make_shared<RcclComm>(*ctrl, dev);
+      } catch (const std::exception &e) {
+        why = e.what();
+        comm_.reset();
+      }
+      double failed = why.empty() ? 0.0 : 1.0;
+      ctrl->allreduce_max(&failed, 1);
+      if (failed != 0.0) {
+        comm_.reset();
+        TZ_LOG(Warn, "SpMV RCCL transport unavailable" << (why.empty() ? " on another rank" : ": " + why));
+        TZ_CHECK(a_.transport == "auto" && useIpc_ && ipcReady_,
+                 "SpMV RCCL transport unavailable and no IPC fallback: " << why);
+        useRccl_ = false;
+      }
+    }
   }
   if (a_.kernel_choice && !a_.library.empty() && local_.nnz() > 0) {
     auto mk = [&](DeviceBuffer &y) {
@@ -334,6 +434,202 @@ void DistSpmv::spmv_remote(void *stream, bool accumulate) const {
                  lanes_, accumulate, stream);
 }
 
+// ------------------------------------------------------------------ ipc transport
+
+std::string DistSpmv::setup_ipc(Ctrl *ctrl) {
+  // Collective like the halo's: every rank makes the same control-plane calls whatever fails
+  // locally. Exported per rank: [flags][remote-x buffer][my recvOff_ per rank (i32)].
+  const size_t H = sizeof(hipIpcMemHandle_t);
+  const size_t P = size_t(a_.size);
+  std::string mine, err;
+  if (const char *v = std::getenv("TZ_IPC_TIMEOUT")) ipcTimeoutS_ = std::atof(v);
+  try {
+    TZ_HIP(hipExtMallocWithFlags(&flags_, std::max<size_t>(2 * P * 8, 64), hipDeviceMallocUncached));
+    TZ_HIP(hipMemset(flags_, 0, 2 * P * 8));
+    expected_ = DeviceBuffer(P * 8);
+    sent_ = DeviceBuffer(P * 8);
+    done_ = DeviceBuffer(size_t(kern::kMaxPutPeers) * sizeof(unsigned int));
+    err_ = DeviceBuffer(sizeof(int));
+    TZ_HIP(hipMemset(expected_.get(), 0, P * 8));
+    TZ_HIP(hipMemset(sent_.get(), 0, P * 8));
+    TZ_HIP(hipMemset(done_.get(), 0, done_.bytes()));
+    TZ_HIP(hipMemset(err_.get(), 0, sizeof(int)));
+    TZ_HIP(hipDeviceSynchronize());
+    hipIpcMemHandle_t h;
+    TZ_HIP(hipIpcGetMemHandle(&h, flags_));
+    mine.append(reinterpret_cast<const char *>(&h), H);
+    TZ_HIP(hipIpcGetMemHandle(&h, dXr_.get()));
+    mine.append(reinterpret_cast<const char *>(&h), H);
+    mine.append(reinterpret_cast<const char *>(recvOff_.data()), P * sizeof(int32_t));
+  } catch (const std::exception &e) {
+    err = std::string("export: ") + e.what();
+    mine.clear();
+  }
+  const std::vector<std::string> all = ctrl->allgather(mine);
+  if (!err.empty()) return err;
+  try {
+    TZ_CHECK(all.size() == P, "allgather returned " << all.size() << " entries");
+    peerXr_.assign(P, nullptr);
+    peerFlags_.assign(P, nullptr);
+    peerRecvOff_.assign(P, 0);
+    for (int q = 0; q < a_.size; ++q) {
+      if (q == a_.rank || (sendCount_[q] == 0 && recvCount_[q] == 0)) continue;
+      const std::string &blob = all[size_t(q)];
+      TZ_CHECK(blob.size() == 2 * H + P * sizeof(int32_t), "rank " << q << " exported no IPC handles");
+      auto open = [&](size_t k) {
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, blob.data() + k * H, H);
+        void *ptr = nullptr;
+        TZ_HIP(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
+        opened_.push_back(ptr);
+        return ptr;
+      };
+      peerFlags_[size_t(q)] = open(0);
+      if (sendCount_[q] > 0) {
+        peerXr_[size_t(q)] = open(1);
+        std::memcpy(&peerRecvOff_[size_t(q)], blob.data() + 2 * H + size_t(a_.rank) * sizeof(int32_t),
+                    sizeof(int32_t));
+      }
+    }
+  } catch (const std::exception &e) {
+    return std::string("map: ") + e.what();
+  }
+  return "";
+}
+
+void DistSpmv::ipc_preflight(Ctrl *ctrl) {
+  // one complete put -> wait -> release round whose arrivals are checked value by value; any
+  // failure turns IPC off for every rank
+  double bad = 0;
+  std::string why;
+  const double keep = ipcTimeoutS_;
+  ipcTimeoutS_ = std::min(ipcTimeoutS_, 3.0);
+  try {
+    put(nullptr);
+    wait_puts(nullptr);
+    TZ_HIP(hipDeviceSynchronize());
+  } catch (const std::exception &e) {
+    bad = 1;
+    why = std::string("preflight: ") + e.what();
+  }
+  ctrl->barrier(); // outside the try: every rank reaches it
+  if (bad == 0) {
+    try {
+      const int e = ipc_errors();
+      std::vector<float> xr(remoteCols_.size());
+      if (!xr.empty()) dXr_.download(xr.data(), xr.size() * 4);
+      size_t wrong = 0;
+      for (size_t i = 0; i < xr.size(); ++i) wrong += xr[i] != x_value(remoteCols_[i]);
+      if (e || wrong) {
+        bad = 1;
+        why = "preflight: " + std::to_string(e) + " wait timeout(s), " + std::to_string(wrong) +
+              " wrong remote x entries";
+      }
+      release(nullptr);
+      TZ_HIP(hipDeviceSynchronize());
+    } catch (const std::exception &ex) {
+      bad = 1;
+      why = std::string("preflight check: ") + ex.what();
+    }
+  }
+  ipcTimeoutS_ = keep;
+  ctrl->allreduce_max(&bad, 1);
+  if (bad != 0) {
+    ipcReady_ = false;
+    TZ_LOG(Warn, "SpMV ipc transport disabled: " << (why.empty() ? "failed on another rank" : why));
+    TZ_CHECK(a_.transport != "ipc", "SpMV ipc transport requested but " << why);
+  }
+  ctrl->barrier();
+}
+
+void DistSpmv::put(void *stream) const {
+  TZ_CHECK(ready() && useIpc_, "SpMV ipc transport not set up");
+  std::vector<int> to;
+  std::vector<kern::PutSeg> segs;
+  for (int q = 0; q < a_.size; ++q) {
+    if (q == a_.rank || sendCount_[q] == 0) continue;
+    TZ_CHECK(peerXr_[size_t(q)] && peerFlags_[size_t(q)], "rank " << q << " is not IPC-mapped");
+    kern::PutSeg sg;
+    sg.dst = static_cast<float *>(peerXr_[size_t(q)]) + peerRecvOff_[size_t(q)];
+    sg.off = sendOff_[q];
+    sg.n = sendCount_[q];
+    // the receiver counts my arrivals in its slot `my rank`
+    sg.flag = static_cast<unsigned long long *>(peerFlags_[size_t(q)]) + a_.rank;
+    segs.push_back(sg);
+    to.push_back(q);
+  }
+  if (segs.empty()) return;
+  // flow control: my put n+1 may overwrite q's remote-x entries only after q's remote product
+  // of put n returned the credit (to my slot size + q)
+  kern::ipc_wait(static_cast<const unsigned long long *>(flags_) + a_.size, sent_.as<unsigned long long>(),
+                 to.data(), int(to.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/1);
+  kern::gather_put_signal(dX_.as<float>(), dSendIdx_.as<int32_t>(), segs.data(), int(segs.size()),
+                          done_.as<unsigned int>(), stream);
+}
+
+void DistSpmv::wait_puts(void *stream) const {
+  TZ_CHECK(ready() && useIpc_, "SpMV ipc transport not set up");
+  std::vector<int> from;
+  for (int q = 0; q < a_.size; ++q)
+    if (q != a_.rank && recvCount_[q] > 0) from.push_back(q);
+  kern::ipc_wait(static_cast<const unsigned long long *>(flags_), expected_.as<unsigned long long>(),
+                 from.data(), int(from.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/0);
+}
+
+void DistSpmv::release(void *stream) const {
+  TZ_CHECK(ready() && useIpc_, "SpMV ipc transport not set up");
+  std::vector<unsigned long long *> credits;
+  for (int q = 0; q < a_.size; ++q)
+    if (q != a_.rank && recvCount_[q] > 0)
+      credits.push_back(static_cast<unsigned long long *>(peerFlags_[size_t(q)]) + a_.size + a_.rank);
+  kern::ipc_signal(credits.data(), int(credits.size()), stream);
+}
+
+int DistSpmv::ipc_errors() {
+  if (!useIpc_ || !err_.get()) return 0;
+  int e = 0;
+  TZ_HIP(hipDeviceSynchronize());
+  err_.download(&e, sizeof(e));
+  TZ_HIP(hipMemset(err_.get(), 0, sizeof(int)));
+  return e;
+}
+
+std::shared_ptr<Graph> DistSpmv::form_graph_ipc(bool accum, const std::string &p) {
+  // the reference's Scatter -> PostSend / PostRecv -> WaitRecv becomes put (gather straight
+  // into the peers' memory) -> wait; the remote product hands the buffer back (credit)
+  auto self = std::const_pointer_cast<const DistSpmv>(shared_from_this());
+  auto g = std::make_shared<Graph>();
+  OpPtr yl;
+  if (a_.kernel_choice) {
+    std::vector<OpPtr> ch;
+    for (int w : {4, 8, 16})
+      ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w, accum));
+    ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_stream", -1, accum));
+    if (!a_.library.empty())
+      ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_rocsparse_" + a_.library, kLibrary, accum));
+    yl = std::make_shared<StaticChoiceOp>(p + "yl", ch);
+  } else {
+    yl = std::make_shared<SpmvLocal>(self, p + "yl", 0, accum);
+  }
+  auto put = std::make_shared<SpmvPut>(self, p + "put");
+  auto wait = std::make_shared<SpmvWait>(self, p + "wait");
+  auto yr = std::make_shared<SpmvRemoteRelease>(self, p + "yr", accum);
+  g->start_then(yl);
+  g->start_then(put);
+  g->then(put, wait);
+  g->then(wait, yr);
+  if (accum) {
+    g->then(yl, yr);
+    g->then_finish(yr);
+  } else {
+    auto y = std::make_shared<SpmvAdd>(self, p + "y");
+    g->then(yl, y);
+    g->then(yr, y);
+    g->then_finish(y);
+  }
+  return g;
+}
+
 void DistSpmv::add(void *stream) const {
   kern::vector_add_f32(int(local_rows()), dYl_.as<float>(), dYr_.as<float>(), dY_.as<float>(), stream);
 }
@@ -382,20 +678,37 @@ std::shared_ptr<const Graph> DistSpmv::op_graph() {
   const std::string &f = a_.form;
   TZ_CHECK(f == "split" || f == "accum" || f == "choice",
            "SpMV form must be split, accum or choice (got " << f << ")");
-  if (f != "choice") {
-    inner_ = form_graph(f == "accum", p);
-    return inner_;
+  // one transport's graph: a single form, or both forms as a ChoiceOp (accum-form op names
+  // carry an extra "a_" so every op name stays unique in the expanded graph)
+  auto forms = [&](bool ipc, const std::string &q) -> std::shared_ptr<Graph> {
+    auto one = [&](bool accum, const std::string &r) {
+      return ipc ? form_graph_ipc(accum, r) : form_graph(accum, r);
+    };
+    if (f != "choice") return one(f == "accum", q);
+    std::vector<OpPtr> alts = {std::make_shared<StaticCompoundOp>(q + "split", one(false, q)),
+                               std::make_shared<StaticCompoundOp>(q + "accum", one(true, q + "a_"))};
+    auto g = std::make_shared<Graph>();
+    auto c = std::make_shared<StaticChoiceOp>(q + "form", alts);
+    g->start_then(c);
+    g->then_finish(c);
+    return g;
+  };
+  // graph-only builds (no setup) assume IPC can be mapped
+  const bool ipc = useIpc_ && (ipcReady_ || !ready());
+  const bool rccl = useRccl_ || a_.size == 1;
+  TZ_CHECK(ipc || rccl, "SpMV has no transport for its x halo");
+  if (ipc && rccl) {
+    // the transport is a search decision too; IPC variants' op names carry "i_"
+    std::vector<OpPtr> alts = {std::make_shared<StaticCompoundOp>(p + "via_rccl", forms(false, p)),
+                               std::make_shared<StaticCompoundOp>(p + "via_ipc", forms(true, p + "i_"))};
+    auto g = std::make_shared<Graph>();
+    auto c = std::make_shared<StaticChoiceOp>(p + "xfer", alts);
+    g->start_then(c);
+    g->then_finish(c);
+    inner_ = g;
+  } else {
+    inner_ = forms(ipc, ipc ? p + "i_" : p);
   }
-  // both forms as alternatives; accum-form op names carry an extra "a_" so every op name
-  // stays unique in the expanded graph
-  std::vector<OpPtr> forms = {
-      std::make_shared<StaticCompoundOp>(p + "split", form_graph(false, p)),
-      std::make_shared<StaticCompoundOp>(p + "accum", form_graph(true, p + "a_"))};
-  auto g = std::make_shared<Graph>();
-  auto c = std::make_shared<StaticChoiceOp>(p + "form", forms);
-  g->start_then(c);
-  g->then_finish(c);
-  inner_ = g;
   return inner_;
 }
 

@@ -279,6 +279,11 @@ struct SpmvArgs {
   // structure); "accum": y = A_l x, then y += A_r x_r (no partials, no add; the remote SpMV
   // waits for the local one); "choice": a ChoiceOp over both forms
   std::string form = "choice";
+  // x-halo transport between ranks: "rccl" (gather -> grouped RCCL exchange), "ipc" (the gather
+  // kernel stores straight into the peers' IPC-mapped remote-x buffers + device-side arrival
+  // wait; also the loopback backend for several ranks on one GPU), "auto" (both as a ChoiceOp
+  // when both can be set up, else whichever can)
+  std::string transport = "auto";
   std::string prefix = "";  // op-name prefix (to combine several workloads in one graph)
   Json json() const;
 };
@@ -315,6 +320,20 @@ public:
   /// when the remote block is empty
   void spmv_remote(void *stream, bool accumulate = false) const;
   void add(void *stream) const;
+  // ipc transport
+  /// credit wait, then one launch that gathers my x entries straight into every peer's remote-x
+  /// buffer and signals their arrival counters
+  void put(void *stream) const;
+  /// wait until every peer's put of this iteration arrived in my remote-x buffer
+  void wait_puts(void *stream) const;
+  /// return the senders' credits (their next put may overwrite my remote-x buffer)
+  void release(void *stream) const;
+  bool uses_rccl() const { return useRccl_; }
+  bool uses_ipc() const { return useIpc_ && ipcReady_; }
+  /// "rccl", "ipc", "rccl+ipc" (search chooses) or "none" (one rank)
+  std::string transport() const;
+  /// number of arrival/credit waits that timed out (0 = healthy); resets the flag
+  int ipc_errors();
 
 private:
   SpmvArgs a_;
@@ -331,6 +350,15 @@ private:
   DeviceBuffer dX_, dXr_, dSendIdx_, dSend_, dYl_, dYr_, dY_;
   std::shared_ptr<RcclComm> comm_;
   std::shared_ptr<RocsparseCsr> rsYl_, rsY_; // library SpMV into y_l / into y
+  std::shared_ptr<Graph> form_graph_ipc(bool accumulate, const std::string &prefix);
+  std::string setup_ipc(Ctrl *ctrl);
+  void ipc_preflight(Ctrl *ctrl);
+  bool useRccl_ = false, useIpc_ = false, ipcReady_ = false;
+  void *flags_ = nullptr; // [arrivals from rank q | credits from rank q] (uncached, exported)
+  DeviceBuffer expected_, sent_, done_, err_;
+  std::vector<void *> peerXr_, peerFlags_, opened_;
+  std::vector<int32_t> peerRecvOff_; // where my segment starts in peer q's remote-x buffer
+  double ipcTimeoutS_ = 10.0;
   std::shared_ptr<const Graph> inner_;
   std::shared_ptr<Graph> form_graph(bool accum, const std::string &p);
 };

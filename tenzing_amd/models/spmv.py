@@ -21,6 +21,7 @@ class SpmvConfig:
     kernel_choice: bool = True  # local SpMV kernel variants as a ChoiceOp
     form: str = "choice"        # split (y = yl + yr, reference) | accum (y = yl; y += yr) | choice
     library: str = "adaptive"   # rocSPARSE CSR algorithm added to the kernel ChoiceOp ("" = none)
+    transport: str = "auto"     # x halo between ranks: rccl | ipc | auto (ChoiceOp over both)
     prefix: str = ""
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.SpmvArgs":
@@ -29,6 +30,7 @@ class SpmvConfig:
         a.compound, a.kernel_choice, a.prefix = self.compound, self.kernel_choice, self.prefix
         a.form = self.form
         a.library = self.library
+        a.transport = self.transport
         a.rank, a.size, a.device = rank, size, device
         return a
 

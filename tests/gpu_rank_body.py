@@ -74,6 +74,53 @@ def main():
             out.setdefault("mcts_err", []).append(halo.ipc_errors())
             del rt, halo
         out["runs"] = res
+    elif case in ("spmv", "fused"):
+        from tenzing_amd.models import SpmvConfig, build_fused, build_spmv
+
+        m = int(os.environ.get("TZ_TEST_M", "30000"))
+        if case == "spmv":
+            sp, g = build_spmv(SpmvConfig(m=m), ctrl, dev)
+            halo = None
+        else:
+            halo, sp, g = build_fused(HaloConfig(n=32, neighbors=26, order="qxyz", fuse="choice"),
+                                      SpmvConfig(m=m), ctrl, dev)
+        out["transport"] = sp.transport()
+        rt = tz.HipRuntime(device=dev, n_streams=3, watchdog_s=60.0)
+        res = []
+        for mode in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+            rt.set_mode(mode)
+            rt.set_graph_unroll(3 if mode == tz.ExecMode.Graph else 1)
+            for seed in range(4):
+                msg = ""
+                if ctrl.rank == 0:
+                    msg = tz.random_rollout(tz.State(g, tz.Platform(3)), seed).json(True)
+                seq = tz.OpIndex(g).sequence_from_json(ctrl.bcast(msg, 0).decode())
+                names = [o.name for o in seq.ops()]
+                sp.reset_y()
+                if halo is not None:
+                    halo.init_grid()
+                ctrl.barrier()
+                rt.prepare(seq)
+                rt.run(1)
+                rt.device_sync()
+                ctrl.barrier()
+                err1 = sp.check()
+                bad = halo.check_grid() if halo is not None else 0
+                ctrl.barrier()
+                rt.run(5)  # y = A x is idempotent: repeated iterations keep it right
+                rt.device_sync()
+                ctrl.barrier()
+                res.append(dict(mode=str(mode), seed=seed, err1=err1, err2=sp.check(), bad=int(bad),
+                                ipc=any(n.startswith(("i_", "spmv_i_")) for n in names),
+                                ipc_err=sp.ipc_errors()))
+        bench = tz.EmpiricalBenchmarker(rt, ctrl)
+        o = tz.MctsOpts()
+        o.n_iters = 6
+        o.bench = tz.BenchOpts(n_iters=3, max_retries=1, target_secs=0.001)
+        rt.set_mode(tz.ExecMode.Eager)
+        r = tz.mcts_explore(g, tz.Platform(3), bench, ctrl, o)
+        out["mcts"] = len(r.sims)
+        out["runs"] = res
     print("RESULT " + json.dumps(out), flush=True)
 
 

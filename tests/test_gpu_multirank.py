@@ -80,3 +80,17 @@ def test_bench_two_ranks_loopback(gpu, tmp_path):
     assert j["n_gpus"] == 2 and j["steps"] == 6 and j["verified_bad_cells"] == 0
     assert j["transport"] == "direct+ipc" and j["config"]["rank_grid"] == [1, 1, 2]
     assert j["value"] > 0 and j["higher_is_better"] is False
+
+
+@pytest.mark.parametrize("world,case", [(2, "spmv"), (4, "spmv"), (2, "fused")])
+def test_spmv_ipc_loopback(gpu, world, case):
+    """distributed SpMV (and SpMV + halo in one graph, BASELINE config 5) on several ranks of
+    one GPU: RCCL refuses the shared device, so the x halo goes through IPC puts; every rank's
+    y is checked against the host reference after every schedule"""
+    res = _launch(case, world)
+    for r in res:
+        assert r["size"] == world and r["transport"] == "ipc"
+        assert r["mcts"] == (6 if r["rank"] == 0 else 0)
+        for run in r["runs"]:
+            assert run["err1"] < 1e-4 and run["err2"] < 1e-4, run
+            assert run["bad"] == 0 and run["ipc_err"] == 0 and run["ipc"], run
