@@ -59,6 +59,10 @@ def main() -> int:
                     choices=["auto", "direct", "copy", "rccl", "ipc"],
                     help="auto: direct (pack-free) moves for self-neighbours, RCCL between "
                          "ranks; ipc: pack-free puts into IPC-mapped peer grids")
+    ap.add_argument("--rank-grid", default="",
+                    help="PXxPYxPZ rank grid (default: the reference rule, prime factors to the "
+                         "smallest dimension: 8 -> 2x2x2). Per-rank work is fixed either way; "
+                         "slabs (1x1xN) send 2 instead of 6 faces per rank")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=40)
@@ -92,8 +96,13 @@ def main() -> int:
         print(f"bench.py: warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
     t_setup = time.time()
+    grid = tuple(int(v) for v in args.rank_grid.lower().split("x")) if args.rank_grid else ()
+    if grid and (len(grid) != 3 or grid[0] * grid[1] * grid[2] != world):
+        print(f"bench.py: --rank-grid {args.rank_grid} does not factor {world} ranks",
+              file=sys.stderr)
+        return 2
     cfg = HaloConfig(n=args.n, neighbors=args.neighbors, fuse=args.fuse, order=args.order,
-                     transport=args.transport)
+                     transport=args.transport, rank_grid=grid)
     halo, graph = build_halo(cfg, ctrl, device)
     mode = tz.ExecMode.Graph if args.search_mode == "graph" else tz.ExecMode.Eager
     rt = tz.HipRuntime(device=device, n_streams=args.streams, mode=mode, watchdog_s=120.0,

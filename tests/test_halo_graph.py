@@ -116,3 +116,18 @@ def test_ipc_transport_graph(tz, fuse, size, mode, monkeypatch):
             assert [names[k] for k in unpacks] == ["he_unpack_remote"] and unpacks[0] > w
         if fuse == "none":
             assert len(puts) == n_ipc
+
+
+@pytest.mark.parametrize("grid", [(1, 1, 8), (8, 1, 1), (2, 4, 1)])
+def test_explicit_rank_grid_neighbours_are_symmetric(tz, grid):
+    """an explicit rank grid (e.g. slabs) instead of the reference's prime-factor rule: every
+    rank's neighbour in direction d sees this rank as its neighbour in direction -d"""
+    from tenzing_amd.models import HaloConfig
+
+    hs = [tz._tz.HaloExchange(HaloConfig(n=16, neighbors=26, rank_grid=grid).args(r, 8, -1))
+          for r in range(8)]
+    for r, h in enumerate(hs):
+        assert list(h.rank_grid()) == list(grid)
+        for i in range(h.ndirs()):
+            q = h.neighbor(i)
+            assert hs[q].neighbor(h.opposite(i)) == r
