@@ -78,6 +78,9 @@ def _ninja_file(debug: bool) -> str:
         "rule link_exe",
         "  command = $hipcc -o $out $in $ldflags",
         "  description = LINK $out",
+        "rule ar",
+        "  command = rm -f $out && ar rcs $out $in",
+        "  description = AR $out",
     ]
     objs_core, objs_rt = [], []
     for n in CORE:
@@ -109,7 +112,17 @@ def _ninja_file(debug: bool) -> str:
         lines.append(f"  extra = {hipdefs}")
         exe = PKG / "bin" / tool.replace("_", "-")
         lines.append(f"build {exe}: link_exe {allobjs} {o}")
-    lines.append(f"default {ext_path()} {PKG / 'bin' / 'tz-search'} {PKG / 'bin' / 'tz-unit'}")
+    # the engine as a C++ library (reference: the static `tenzing` library that drivers link),
+    # plus a user-side example that defines its own kernel op against it
+    lib = BUILD / "libtenzing_amd.a"
+    lines.append(f"build {lib}: ar {allobjs}")
+    ex_src = ROOT / "examples" / "cpp" / "custom_kernel_op.hip"
+    ex_obj = f"{BUILD}/examples/custom_kernel_op.o"
+    ex_exe = PKG / "bin" / "tz-example-custom-op"
+    lines.append(f"build {ex_obj}: hipdev {ex_src}")
+    lines.append(f"build {ex_exe}: link_exe {ex_obj} {lib}")
+    lines.append(f"default {ext_path()} {PKG / 'bin' / 'tz-search'} {PKG / 'bin' / 'tz-unit'} "
+                 f"{lib} {ex_exe}")
     return "\n".join(lines) + "\n"
 
 

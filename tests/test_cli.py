@@ -102,3 +102,13 @@ def test_example_sim_design_rules(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert "24 schedules" in r.stdout and "b and c same stream" in r.stdout
     assert (tmp_path / "ex_rules.txt").exists()
+
+
+def test_cpp_library_example_sim():
+    """examples/cpp/custom_kernel_op.hip: a user-defined kernel op searched through the C++
+    library (built against build/libtenzing_amd.a), hardware-free"""
+    exe = os.path.join(ROOT, "tenzing_amd", "bin", "tz-example-custom-op")
+    r = subprocess.run([exe, "--sim"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["candidates"] == 24 and j["best_us"] < j["worst_us"]

@@ -315,3 +315,18 @@ def test_example_torch_overlap(gpu):
     assert j["best_ms"] < 0.9 * j["worst_ms"], j
     bs = j["best_streams"]
     assert bs["gemm"] != bs["h2d"], j
+
+
+def test_cpp_library_example_on_gpu(tz, gpu):
+    """the C++ library example on the device: its own HIP kernel op, MCTS over 2 streams, the
+    winning schedule's results checked by the program (exit 1 on a wrong element)"""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tenzing_amd", "bin", "tz-example-custom-op")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    # the two chains overlap on two streams
+    assert j["best_us"] < 0.8 * j["worst_us"], j
