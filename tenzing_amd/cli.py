@@ -62,6 +62,10 @@ def cmd_search(a) -> int:
     from tenzing_amd.parallel import init_ctrl, select_device
 
     ctrl = init_ctrl()
+    if ctrl.rank == 0:
+        # version + command line, like the reference's reproduce::dump_with_cli (stderr keeps
+        # stdout for results)
+        print(tz._tz.reproduce_json(sys.argv), file=sys.stderr, flush=True)
     if a.workload == "noop":
         a.host = True  # no GPU op in the graph: time it on the host executor
     hw = not (a.sim or a.replay or a.host)
