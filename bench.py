@@ -213,7 +213,8 @@ def main() -> int:
     ms = t / args.steps * 1e3
 
     names = [o.name for o in best.ops()]
-    via = [t for t, key in (("direct", "he_direct_"), ("rccl", "he_shift_"), ("ipc", "he_put_"))
+    via = [t for t, key in (("direct", "he_direct_"), ("rccl", "he_shift_"), ("ipc", "he_put_"),
+                            ("sdma", "he_copyput_"))
            if any(n.startswith(key) for n in names)]
     if rank == 0:
         bytes_total = halo.exchange_bytes() * world

@@ -139,17 +139,19 @@ private:
 class HaloStageGroup : public GpuOp {
 public:
   // UnpackRelease: unpack IPC receive buffers, then hand them back to the senders (credits)
-  enum Stage { Pack, Shift, Unpack, Direct, Put, UnpackRelease };
+  // CopyPut: pack locally, copy-engine (SDMA) copy into the peer's receive buffer, signal
+  enum Stage { Pack, Shift, Unpack, Direct, Put, UnpackRelease, CopyPut };
   HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag)
       : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
   std::string name() const override {
     static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_", "he_put_",
-                                "he_unpack_"};
+                                "he_unpack_", "he_copyput_"};
     return pre[st_] + tag_;
   }
   std::string kind() const override {
     static const char *k[] = {"HaloPackGroup", "HaloShiftGroup", "HaloUnpackGroup",
-                              "HaloDirectGroup", "HaloPutGroup", "HaloUnpackGroup"};
+                              "HaloDirectGroup", "HaloPutGroup", "HaloUnpackGroup",
+                              "HaloCopyPutGroup"};
     return k[st_];
   }
   double bytes() const override {
@@ -167,6 +169,7 @@ public:
     else if (st_ == Unpack) h_->unpack_group(dirs_, s);
     else if (st_ == Direct) h_->direct_group(dirs_, s);
     else if (st_ == Put) h_->put_group(dirs_, s);
+    else if (st_ == CopyPut) h_->copy_put_group(dirs_, s);
     else h_->ipc_unpack_group(dirs_, s);
   }
 
@@ -279,6 +282,9 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   }
   ipcGrid_ = gridElems_ * sizeof(double) < (size_t(2) << 30);
   if (const char *v = std::getenv("TZ_IPC_GRID")) ipcGrid_ = std::atoi(v) != 0;
+  // copy-engine puts (buffers mode only): on unless TZ_IPC_COPY=0
+  useCopy_ = useIpc_;
+  if (const char *v = std::getenv("TZ_IPC_COPY")) useCopy_ = useCopy_ && std::atoi(v) != 0;
 }
 
 HaloExchange::~HaloExchange() {
@@ -388,7 +394,7 @@ void HaloExchange::setup(Ctrl *ctrl) {
   recv_.resize(ndirs());
   for (int i = 0; i < ndirs(); ++i) {
     if (direct_[i]) continue;
-    if (pipe_[i]) send_[i] = DeviceBuffer(box_elems(i) * sizeof(double));
+    if (pipe_[i] || (ipc_[i] && useCopy_ && !ipcGrid_)) send_[i] = DeviceBuffer(box_elems(i) * sizeof(double));
     // ipc "buffers" mode needs the receive buffer too (the peer packs straight into it)
     if (pipe_[i] || (ipc_[i] && !ipcGrid_))
       recv_[i] = DeviceBuffer(box_elems(opp_[i]) * sizeof(double));
@@ -434,7 +440,8 @@ void HaloExchange::setup(Ctrl *ctrl) {
       for (int i = 0; i < ndirs(); ++i) {
         if (pipe_[i]) {
           pipe_[i] = false;
-          send_[i] = DeviceBuffer();
+          // (copy-engine puts pack into send_; buffers-mode puts land in recv_)
+          if (!(ipc_[i] && useCopy_ && !ipcGrid_)) send_[i] = DeviceBuffer();
           if (ipcGrid_) recv_[i] = DeviceBuffer();
         }
       }
@@ -623,6 +630,33 @@ void HaloExchange::put_group(const std::vector<int> &dirs, void *stream) const {
   }
   if (ipcGrid_) kern::box_move_many_signal(ms.data(), int(ms.size()), sig, stream);
   else kern::box_pack_many_signal(grid(), bs.data(), int(bs.size()), sig, stream);
+}
+
+void HaloExchange::copy_put_group(const std::vector<int> &dirs, void *stream) const {
+  // The copy-engine put: pack into my local send buffers (one launch), then one device-to-device
+  // copy per direction into the receiver's IPC-mapped buffer. Across GPUs HIP runs these on the
+  // SDMA engines, so the xGMI transfer itself takes no CUs (they stay free for concurrent local
+  // work); then one small kernel publishes the arrivals. Same credit protocol as put_group.
+  TZ_CHECK(ready() && ipcReady_ && useCopy_ && !ipcGrid_, "ipc copy-engine puts not set up");
+  TZ_CHECK(!dirs.empty() && dirs.size() <= size_t(kern::kMaxBoxes), "bad copy-put group");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::vector<kern::BoxDesc> bs;
+  std::vector<unsigned long long *> arrive;
+  for (int i : dirs) {
+    TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i] && send_[i].get() && peerRecv_[size_t(i)],
+             "direction " << i << " is not a copy-engine put");
+    kern::BoxDesc b = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
+    b.buf = send_[i].as<double>();
+    bs.push_back(b);
+    arrive.push_back(static_cast<unsigned long long *>(peerFlags_[size_t(nbr_[i])]) + i);
+  }
+  kern::ipc_wait(static_cast<const unsigned long long *>(flags_) + ndirs(), sent_.as<unsigned long long>(),
+                 dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/1);
+  kern::box_copy_many(grid(), bs.data(), int(bs.size()), false, stream);
+  for (int i : dirs)
+    TZ_HIP(hipMemcpyAsync(peerRecv_[size_t(i)], send_[i].get(), box_elems(i) * sizeof(double),
+                          hipMemcpyDeviceToDevice, s));
+  kern::ipc_signal(arrive.data(), int(arrive.size()), stream);
 }
 
 void HaloExchange::wait_group(const std::vector<int> &dirs, void *stream) const {
@@ -820,12 +854,15 @@ void HaloExchange::pack_all(void *stream) const { pack_group(pipelined_dirs(), s
 void HaloExchange::unpack_all(void *stream) const { unpack_group(pipelined_dirs(), stream); }
 void HaloExchange::shift_all(void *stream) const { shift_group(pipelined_dirs(), stream); }
 
-void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, bool viaIpc) {
+void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, int via) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   for (int i : dirs) {
-    if (direct_[i] || viaIpc) {
-      OpPtr d = direct_[i] ? OpPtr(std::make_shared<HaloDirect>(self, i))
-                           : OpPtr(std::make_shared<HaloPut>(self, i));
+    if (direct_[i] || via != kViaPipe) {
+      OpPtr d;
+      if (direct_[i]) d = std::make_shared<HaloDirect>(self, i);
+      else if (via == kViaPut) d = std::make_shared<HaloPut>(self, i);
+      else d = std::make_shared<HaloStageGroup>(self, HaloStageGroup::CopyPut, std::vector<int>{i},
+                                                dirs_[i].name());
       g.start_then(d);
       g.then_finish(d);
       continue;
@@ -841,7 +878,7 @@ void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, bool viaIp
 }
 
 void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag,
-                             bool viaIpc) {
+                             int via) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   std::vector<int> local, remote;
   for (int i : dirs) (direct_[i] ? local : remote).push_back(i);
@@ -852,8 +889,9 @@ void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::
     g.then_finish(d);
   }
   if (remote.empty()) return;
-  if (viaIpc) {
-    auto d = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Put, remote, tag);
+  if (via != kViaPipe) {
+    auto d = std::make_shared<HaloStageGroup>(
+        self, via == kViaPut ? HaloStageGroup::Put : HaloStageGroup::CopyPut, remote, tag);
     g.start_then(d);
     g.then_finish(d);
     return;
@@ -867,11 +905,11 @@ void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::
   g.then_finish(u);
 }
 
-void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, bool viaIpc,
+void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via,
                                  const std::string &pre) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   const std::string &f = a_.fuse;
-  const bool singleStage = direct_[dirs.front()] || viaIpc;
+  const bool singleStage = direct_[dirs.front()] || via != kViaPipe;
   auto subset = [&](const std::vector<int> &v) {
     std::vector<int> r;
     for (int i : v)
@@ -879,10 +917,10 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, bool vi
     return r;
   };
   if (f == "none") {
-    add_chains(g, dirs, viaIpc);
+    add_chains(g, dirs, via);
   } else if (f == "all" || (f == "pack" && singleStage)) {
     // (direct moves and puts have no pack stage: "pack" degenerates to one fused op)
-    add_fused(g, dirs, "all", viaIpc);
+    add_fused(g, dirs, "all", via);
   } else if (f == "pack") {
     // fused pack / unpack kernels, per-direction transfers
     auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, "all");
@@ -904,16 +942,16 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, bool vi
              {"faces", subset(group_dirs(1))}, {"small", subset(group_dirs(0))}})
       if (!gr.second.empty()) groups.push_back(gr);
     if (f == "groups") {
-      for (auto &gr : groups) add_fused(g, gr.second, gr.first, viaIpc);
+      for (auto &gr : groups) add_fused(g, gr.second, gr.first, via);
       return;
     }
     // per group: split chains vs one fused chain
     auto grouped = std::make_shared<Graph>();
     for (auto &gr : groups) {
       auto split = std::make_shared<Graph>();
-      add_chains(*split, gr.second, viaIpc);
+      add_chains(*split, gr.second, via);
       auto fused = std::make_shared<Graph>();
-      add_fused(*fused, gr.second, gr.first, viaIpc);
+      add_fused(*fused, gr.second, gr.first, via);
       std::vector<OpPtr> alts = {
           std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_split", split),
           std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_fused", fused)};
@@ -930,7 +968,7 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, bool vi
     // two groups: additionally one chain for every direction (a single launch per stage
     // avoids the two groups' kernels competing for CUs)
     auto all = std::make_shared<Graph>();
-    add_fused(*all, dirs, "all", viaIpc);
+    add_fused(*all, dirs, "all", via);
     std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped),
                               std::make_shared<StaticCompoundOp>(pre + "he_allfused", all)};
     auto choice = std::make_shared<StaticChoiceOp>(pre + "he_exchange", top);
@@ -941,21 +979,23 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, bool vi
   }
 }
 
-void HaloExchange::add_ipc_part(Graph &g, const std::vector<int> &remote) {
-  // puts never wait for anything remote, so each rank's puts all complete; the arrival wait
-  // runs after them (one spinning kernel per rank, never ahead of its own puts)
+void HaloExchange::add_ipc_part(Graph &g, const std::vector<int> &remote, int via) {
+  // puts wait only for the credit of the previous iteration, so each rank's puts all complete;
+  // the arrival wait runs after them (one spinning kernel per rank, never ahead of its own
+  // puts). The copy-engine variant's op names carry "cp_" (unique in the expanded graph).
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  const std::string v = via == kViaCopy ? "cp_" : "";
   auto puts = std::make_shared<Graph>();
-  add_structure(*puts, remote, true, "ipc_");
-  auto c = std::make_shared<StaticCompoundOp>("he_puts", puts);
-  auto w = std::make_shared<HaloWait>(self, remote, "remote");
+  add_structure(*puts, remote, via, via == kViaCopy ? "cp_" : "ipc_");
+  auto c = std::make_shared<StaticCompoundOp>("he_" + v + "puts", puts);
+  auto w = std::make_shared<HaloWait>(self, remote, v + "remote");
   g.start_then(c);
   g.then(c, w);
   if (ipcGrid_) {
     g.then_finish(w);
   } else {
     // "buffers" mode: my receive buffers are complete after the wait; unpack them
-    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::UnpackRelease, remote, "remote");
+    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::UnpackRelease, remote, v + "remote");
     g.then(w, u);
     g.then_finish(u);
   }
@@ -969,31 +1009,43 @@ void HaloExchange::add_to_graph(Graph &g) {
   std::vector<int> local, remote;
   for (int i = 0; i < ndirs(); ++i) (direct_[i] ? local : remote).push_back(i);
   if (remote.empty()) {
-    add_structure(g, all_dirs(), false, "");
+    add_structure(g, all_dirs(), kViaPipe, "");
     return;
   }
   if (!local.empty()) {
-    if (a_.fuse == "none") add_chains(g, local, false);
-    else add_fused(g, local, "self", false);
+    if (a_.fuse == "none") add_chains(g, local, kViaPipe);
+    else add_fused(g, local, "self", kViaPipe);
   }
   // graph-only builds (no setup) assume IPC can be mapped
   const bool ipc = useIpc_ && (ipcReady_ || !ready());
   const bool pipe = useRccl_ || a_.transport == "copy";
   TZ_CHECK(ipc || pipe, "no transport available for the remote directions");
-  if (ipc && pipe) {
-    auto viaRccl = std::make_shared<Graph>();
-    add_structure(*viaRccl, remote, false, "");
-    auto viaIpc = std::make_shared<Graph>();
-    add_ipc_part(*viaIpc, remote);
-    std::vector<OpPtr> alts = {std::make_shared<StaticCompoundOp>("he_via_rccl", viaRccl),
-                               std::make_shared<StaticCompoundOp>("he_via_ipc", viaIpc)};
+  // the copy-engine variant needs receive buffers ("buffers" mode)
+  const bool copy = ipc && useCopy_ && !ipcGrid_;
+  std::vector<OpPtr> alts;
+  if (pipe) {
+    auto gr = std::make_shared<Graph>();
+    add_structure(*gr, remote, kViaPipe, "");
+    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_rccl", gr));
+  }
+  if (ipc) {
+    auto gr = std::make_shared<Graph>();
+    add_ipc_part(*gr, remote, kViaPut);
+    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_ipc", gr));
+  }
+  if (copy) {
+    auto gr = std::make_shared<Graph>();
+    add_ipc_part(*gr, remote, kViaCopy);
+    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_sdma", gr));
+  }
+  if (alts.size() > 1) {
     auto c = std::make_shared<StaticChoiceOp>("he_remote", alts);
     g.start_then(c);
     g.then_finish(c);
   } else if (ipc) {
-    add_ipc_part(g, remote);
+    add_ipc_part(g, remote, kViaPut);
   } else {
-    add_structure(g, remote, false, "");
+    add_structure(g, remote, kViaPipe, "");
   }
 }
 

@@ -194,6 +194,9 @@ public:
   /// ipc transport: put my slabs facing `dirs` into the neighbours' ghost regions and signal
   /// their arrival counters (one launch)
   void put_group(const std::vector<int> &dirs, void *stream) const;
+  /// ipc transport, copy-engine variant ("buffers" mode): pack locally, hipMemcpyAsync (SDMA
+  /// across GPUs) into the neighbours' receive buffers, then signal their arrival counters
+  void copy_put_group(const std::vector<int> &dirs, void *stream) const;
   /// ipc transport: wait until the ghosts filled by the neighbours' puts of `dirs` arrived
   void wait_group(const std::vector<int> &dirs, void *stream) const;
   /// ipc "buffers" mode: unpack the receive buffers filled for `dirs`, then return the
@@ -212,12 +215,14 @@ public:
   void direct(int i, void *stream) const { direct_group({i}, stream); }
 
 private:
-  // graph builders; remote directions use IPC puts when `viaIpc`, else pack/transfer/unpack
-  void add_chains(Graph &g, const std::vector<int> &dirs, bool viaIpc);
-  void add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag, bool viaIpc);
-  void add_structure(Graph &g, const std::vector<int> &dirs, bool viaIpc,
+  // graph builders; remote directions go through `via`: pack/transfer/unpack (kViaPipe), IPC
+  // puts (kViaPut) or copy-engine puts (kViaCopy)
+  static constexpr int kViaPipe = 0, kViaPut = 1, kViaCopy = 2;
+  void add_chains(Graph &g, const std::vector<int> &dirs, int via);
+  void add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag, int via);
+  void add_structure(Graph &g, const std::vector<int> &dirs, int via,
                      const std::string &pre); // fuse mode over `dirs`
-  void add_ipc_part(Graph &g, const std::vector<int> &remote);
+  void add_ipc_part(Graph &g, const std::vector<int> &remote, int via);
   void check_pipelined(int i) const;
   std::string setup_ipc(Ctrl *ctrl); // "" on success, else why IPC cannot be used
   void ipc_preflight(Ctrl *ctrl);    // one verified exchange; disables IPC collectively on failure
@@ -230,6 +235,7 @@ private:
   bool useRccl_ = false, useDirect_ = false, useIpc_ = false;
   std::vector<bool> direct_, ipc_, pipe_; // per direction: self move / IPC put / pack-transfer-unpack
   bool ipcReady_ = false;
+  bool useCopy_ = false; // copy-engine puts offered (buffers mode)
   // ipc transport state
   void *flags_ = nullptr;            // arrival counter per direction (uncached, IPC-exported)
   DeviceBuffer expected_, done_, err_;

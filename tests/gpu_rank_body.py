@@ -60,7 +60,9 @@ def main():
                     bad2 = halo.check_grid()
                     res.append(dict(fuse=fuse, mode=str(mode), seed=seed, bad1=int(bad1),
                                     bad2=int(bad2), err=halo.ipc_errors(),
-                                    transport=halo.transport(), ipc_mode=halo.ipc_mode()))
+                                    transport=halo.transport(), ipc_mode=halo.ipc_mode(),
+                                    copyput=any(o.name.startswith("he_copyput_")
+                                                for o in seq.ops())))
             if os.environ.get("TZ_TEST_NO_MCTS"):
                 continue
             # a short collective search over ipc schedules

@@ -61,6 +61,9 @@ def test_ipc_halo_loopback(gpu, world, mode):
             assert run["bad1"] == 0 and run["bad2"] == 0 and run["err"] == 0, run
             # 2 ranks: grid 1x1x2 (x, y self-neighbours move directly); 4 ranks: 1x2x2
             assert run["transport"] == "direct+ipc"
+        # buffers mode also offers copy-engine (SDMA) puts: some schedules must have used them
+        used = any(run["copyput"] for run in r["runs"])
+        assert used == (mode == "buffers"), [run["copyput"] for run in r["runs"]]
 
 
 def test_bench_two_ranks_loopback(gpu, tmp_path):

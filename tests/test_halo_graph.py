@@ -102,20 +102,26 @@ def test_ipc_transport_graph(tz, fuse, size, mode, monkeypatch):
     n_ipc = sum(h.is_ipc(i) for i in range(h.ndirs()))
     assert n_ipc == 26 - sum(h.is_direct(i) for i in range(h.ndirs()))
     assert h.transport() == ("ipc" if size == 8 else "direct+ipc")
-    for seed in range(3):
+    seen = set()
+    for seed in range(12):
         names = _names(tz, g, seed)
-        assert names[-1] == "he_wait_remote" or "he_wait_remote" in names
-        w = names.index("he_wait_remote")
-        puts = [k for k, n in enumerate(names) if n.startswith("he_put_")]
+        # buffers mode also offers copy-engine puts (pack locally, SDMA copy, signal): a
+        # ChoiceOp between the two, whose op names differ ("cp_")
+        v = "cp_" if "he_wait_cp_remote" in names else ""
+        seen.add(v)
+        w = names.index(f"he_wait_{v}remote")
+        puts = [k for k, n in enumerate(names) if n.startswith("he_copyput_" if v else "he_put_")]
         assert puts and max(puts) < w
         assert not any(n.startswith(("he_pack_", "he_shift_")) for n in names)
+        assert not any(n.startswith("he_put_" if v else "he_copyput_") for n in names)
         unpacks = [k for k, n in enumerate(names) if n.startswith("he_unpack_")]
         if mode == "grid":
             assert not unpacks
         else:
-            assert [names[k] for k in unpacks] == ["he_unpack_remote"] and unpacks[0] > w
+            assert [names[k] for k in unpacks] == [f"he_unpack_{v}remote"] and unpacks[0] > w
         if fuse == "none":
             assert len(puts) == n_ipc
+    assert seen == ({""} if mode == "grid" else {"", "cp_"})
 
 
 @pytest.mark.parametrize("grid", [(1, 1, 8), (8, 1, 1), (2, 4, 1)])
