@@ -7,8 +7,9 @@ halo-exchange 8 ranks". Per rank: 512^3 cells x 3 quantities (f64), ghost 3, 26 
 4 HIP streams, one process per GPU, RCCL over xGMI between ranks (weak scaling: per-GPU work is
 fixed as N grows). Synthetic grid data.
 
-Flow: (1) MCTS (FastMin) explores stream assignment x issue order x sync placement, every
-candidate benchmarked on all ranks (max over ranks); (2) the best schedule is verified for
+Flow: (1) MCTS (FastMin) explores stream assignment x issue order x sync placement x op
+implementation, every candidate compiled to a hipGraph and benchmarked on all ranks (max over
+ranks), then the 4 best are re-measured interleaved; (2) the best schedule is verified for
 correctness (every ghost cell checked on the device); (3) it is replayed W warm-up + K timed
 iterations in eager mode and as a captured hipGraph, bracketed by barrier + device sync, max over
 ranks; the faster mode is reported. `value` = ms per halo-exchange iteration (lower is better);
@@ -70,7 +71,10 @@ def main() -> int:
     ap.add_argument("--bench-iters", type=int, default=20)
     ap.add_argument("--target-secs", type=float, default=0.004)
     ap.add_argument("--strategy", default="FastMin")
-    ap.add_argument("--search-mode", default="eager", choices=["eager", "graph"])
+    ap.add_argument("--search-mode", default="graph", choices=["eager", "graph"],
+                    help="benchmark candidates eagerly or compiled to hipGraphs (default: graph, "
+                         "the way the final number is measured; eager rankings can mislead, "
+                         "profiles/r1_bench_loopback/)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--graph-unroll", type=int, default=10,
                     help="iterations per hipGraph launch when timing the graph-compiled schedule")
@@ -117,7 +121,19 @@ def main() -> int:
     opts.seed = args.seed
     opts.bench = tz.BenchOpts(n_iters=args.bench_iters, max_retries=3, target_secs=args.target_secs)
     platform = tz.Platform(n_streams=args.streams)
-    res = tz.mcts_explore(graph, platform, bench, ctrl, opts)
+    try:
+        res = tz.mcts_explore(graph, platform, bench, ctrl, opts)
+    except Exception as e:  # noqa: BLE001
+        # a candidate that cannot be compiled to a hipGraph fails on every rank together
+        # (collective preparation), so every rank can fall back to eager candidates together
+        if mode != tz.ExecMode.Graph:
+            raise
+        print(f"bench.py: rank {rank}: graph-mode search failed ({e}); searching eagerly",
+              file=sys.stderr)
+        mode = tz.ExecMode.Eager
+        rt.set_mode(mode)
+        rt.set_graph_unroll(1)
+        res = tz.mcts_explore(graph, platform, bench, ctrl, opts)
     search_wall = res.wall_s
 
     # the K best distinct candidates (by the search's pct10) -> every rank
@@ -165,7 +181,7 @@ def main() -> int:
                       [p * 1e3 for p in payload["pct10"]], "chosen": k,
                       "wall_s": time.time() - t_rr}
         rt.set_mode(mode)
-        rt.set_graph_unroll(args.graph_unroll if args.search_mode == "graph" else 1)
+        rt.set_graph_unroll(args.graph_unroll if mode == tz.ExecMode.Graph else 1)
 
     # correctness of the winning schedule: one exchange from a fresh grid, every cell checked
     rt.set_mode(tz.ExecMode.Eager)
@@ -248,6 +264,7 @@ def main() -> int:
             "search_wall_s": search_wall,
             "mcts_candidates": payload["n_sims"],
             "mcts_tree_nodes": payload["tree"],
+            "search_mode": "hipgraph" if mode == tz.ExecMode.Graph else "eager",
             "search_best_pct10_ms": best_pct10 * 1e3,
             "rerank": rerank,
             "eager_ms_per_step": t_eager / args.steps * 1e3,
