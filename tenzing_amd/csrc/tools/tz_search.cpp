@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
@@ -51,7 +52,9 @@ void usage() {
          "  [--target-secs S] [--mode eager|graph] [--sim] [--seed N] [--no-expand-rollout]\n"
          "  [--halo-n N] [--nq N] [--ghost N] [--neighbors 6|26] [--order xyzq|qxyz]\n"
          "  [--fuse none|pack|all|groups|choice] [--graph-unroll K]\n"
-         "  [--transport auto|rccl|ipc|copy|direct] [--spmv-m N] [--spmv-form choice|split|accum] [--max-seqs N] [--rdzv-file PATH]\n"
+         "  [--transport auto|rccl|ipc|copy|direct] [--rank-grid PXxPYxPZ] [--spmv-m N]\n"
+         "  [--spmv-form choice|split|accum] [--spmv-transport auto|rccl|ipc]\n"
+         "  [--spmv-library adaptive|lrb|rowsplit|''] [--cu-partition] [--max-seqs N] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--watchdog S]\n";
 }
@@ -125,6 +128,11 @@ int main(int argc, char **argv) {
       TZ_CHECK(h.order == "xyzq" || h.order == "qxyz", "--order must be xyzq or qxyz");
       h.rank = rank;
       h.size = size;
+      const std::string rg = a.get("rank-grid", "");
+      if (!rg.empty()) {
+        TZ_CHECK(std::sscanf(rg.c_str(), "%dx%dx%d", &h.px, &h.py, &h.pz) == 3,
+                 "--rank-grid must look like 2x2x2");
+      }
       halo = std::make_shared<HaloExchange>(h);
       if (!sim) halo->setup(ctrl.get());
       halo->add_to_graph(*g);
@@ -136,6 +144,8 @@ int main(int argc, char **argv) {
       s.size = size;
       s.prefix = workload == "halo+spmv" ? "spmv_" : "";
       s.form = a.get("spmv-form", "choice");
+      s.transport = a.get("spmv-transport", "auto");
+      s.library = a.get("spmv-library", "adaptive");
       spmv = std::make_shared<DistSpmv>(s);
       if (!sim) spmv->setup(ctrl.get());
       spmv->add_to_graph(*g);
@@ -157,6 +167,8 @@ int main(int argc, char **argv) {
     }
 
     Platform plat = Platform::make_n_streams(streams);
+    // CU-partitioned streams are distinguishable resources: no symmetric-stream pruning
+    if (a.flag("cu-partition")) plat.symmetric_streams = false;
     std::unique_ptr<HipRuntime> rt;
     std::unique_ptr<Benchmarker> bench;
     if (sim) {
@@ -167,6 +179,7 @@ int main(int argc, char **argv) {
       ro.mode = a.get("mode", "eager") == "graph" ? ExecMode::Graph : ExecMode::Eager;
       ro.watchdog_s = a.num("watchdog", 60);
       ro.graph_unroll = int(a.num("graph-unroll", 1));
+      ro.cu_partition = a.flag("cu-partition");
       rt = std::make_unique<HipRuntime>(ro);
       bench = std::make_unique<EmpiricalBenchmarker>(*rt, *ctrl);
     }
