@@ -121,15 +121,13 @@ def main() -> int:
     opts.seed = args.seed
     opts.bench = tz.BenchOpts(n_iters=args.bench_iters, max_retries=3, target_secs=args.target_secs)
     platform = tz.Platform(n_streams=args.streams)
-    try:
-        res = tz.mcts_explore(graph, platform, bench, ctrl, opts)
-    except Exception as e:  # noqa: BLE001
-        # a candidate that cannot be compiled to a hipGraph fails on every rank together
-        # (collective preparation), so every rank can fall back to eager candidates together
-        if mode != tz.ExecMode.Graph:
-            raise
-        print(f"bench.py: rank {rank}: graph-mode search failed ({e}); searching eagerly",
-              file=sys.stderr)
+    # candidates that cannot be compiled to a hipGraph are skipped by the search (every rank
+    # agrees: preparation is collective); if none could be measured, search eagerly instead
+    res = tz.mcts_explore(graph, platform, bench, ctrl, opts)
+    measured = float(len(res.sims)) if rank == 0 else 1.0
+    if mode == tz.ExecMode.Graph and ctrl.allreduce_max([0.0 if measured else 1.0])[0] > 0:
+        print(f"bench.py: rank {rank}: no candidate could run as a hipGraph "
+              f"({res.failed} skipped); searching eagerly", file=sys.stderr)
         mode = tz.ExecMode.Eager
         rt.set_mode(mode)
         rt.set_graph_unroll(1)
@@ -150,7 +148,8 @@ def main() -> int:
                 break
         payload = json.dumps({"seqs": [res.sims[i].seq.json() for i in top],
                               "pct10": [res.sims[i].res.pct10 for i in top],
-                              "n_sims": len(res.sims), "tree": res.tree_size})
+                              "n_sims": len(res.sims), "tree": res.tree_size,
+                              "failed": res.failed})
         if args.csv:
             with open(args.csv, "w") as f:
                 f.write(res.dump_csv())
@@ -263,6 +262,7 @@ def main() -> int:
             },
             "search_wall_s": search_wall,
             "mcts_candidates": payload["n_sims"],
+            "mcts_skipped": payload["failed"],
             "mcts_tree_nodes": payload["tree"],
             "search_mode": "hipgraph" if mode == tz.ExecMode.Graph else "eager",
             "search_best_pct10_ms": best_pct10 * 1e3,

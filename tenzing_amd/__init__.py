@@ -76,6 +76,7 @@ from ._tz import (  # noqa: E402,F401
     OpBase,
     OpIndex,
     Platform,
+    PyBenchmarker,
     PyCpuOp,
     PyGpuOp,
     RcclComm,

@@ -77,6 +77,25 @@ private:
   bool capturable_;
 };
 
+/// a benchmarker written in Python: fn(sequence, bench_opts) -> BenchResult (an analytical
+/// model, a remote service, a replay of some other log...). An exception raised by fn counts as
+/// a failed candidate (skipped by the solvers unless `skip_failed` is off).
+class PyBenchmarker : public Benchmarker {
+public:
+  explicit PyBenchmarker(py::function fn) : fn_(std::move(fn)) {}
+  ~PyBenchmarker() override {
+    py::gil_scoped_acquire g;
+    fn_ = py::function();
+  }
+  BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) override {
+    py::gil_scoped_acquire g;
+    return fn_(seq, opts).cast<BenchResult>();
+  }
+
+private:
+  py::function fn_;
+};
+
 py::dict counters_dict(const Counters &c) {
   py::dict d;
   for (const auto &kv : c.seconds) d[py::str(kv.first)] = kv.second;
@@ -388,6 +407,8 @@ PYBIND11_MODULE(_tz, m) {
         for (auto &s : e.trace()) l.append(py::make_tuple(s.name, s.stream, s.start, s.end));
         return l;
       });
+  py::class_<PyBenchmarker, Benchmarker>(m, "PyBenchmarker")
+      .def(py::init<py::function>(), py::arg("fn"));
   py::class_<CsvBenchmarker, Benchmarker>(m, "CsvBenchmarker")
       .def(py::init<const std::string &, const Graph &>())
       .def("__len__", &CsvBenchmarker::size);
@@ -461,6 +482,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("checkpoint_every", &MctsOpts::checkpoint_every)
       .def_readwrite("resume_path", &MctsOpts::resume_path)
       .def_readwrite("trap_signals", &MctsOpts::trap_signals)
+      .def_readwrite("skip_failed", &MctsOpts::skip_failed)
       .def("json", [](const MctsOpts &o) { return o.json().dump(); });
   py::class_<DfsOpts>(m, "DfsOpts")
       .def(py::init<>())
@@ -469,6 +491,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("remove_redundant_syncs", &DfsOpts::remove_redundant_syncs)
       .def_readwrite("bench", &DfsOpts::bench)
       .def_readwrite("trap_signals", &DfsOpts::trap_signals)
+      .def_readwrite("skip_failed", &DfsOpts::skip_failed)
       .def("json", [](const DfsOpts &o) { return o.json().dump(); });
   py::class_<SimResult>(m, "SimResult")
       .def_readonly("seq", &SimResult::seq)
@@ -480,6 +503,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readonly("tree_size", &SearchResult::tree_size)
       .def_readonly("tree_fully_visited", &SearchResult::tree_fully_visited)
       .def_readonly("stop_reason", &SearchResult::stop_reason)
+      .def_readonly("failed", &SearchResult::failed)
       .def("best", &SearchResult::best)
       .def("counters", [](const SearchResult &r) { return counters_dict(r.counters); })
       .def("dump_csv", [](const SearchResult &r) {

@@ -341,6 +341,20 @@ struct Tree {
     return node.children[best[u(rng)]].get();
   }
 
+  /// a candidate that could not be benchmarked: count the visit, take the path out of the
+  /// search (fully visited), feed the strategy nothing
+  void prune_failed(MctsNode *node) {
+    node->fully_visited = true;
+    for (; node; node = node->parent) {
+      ++node->n;
+      if (!node->children.empty()) {
+        bool all = true;
+        for (auto &ch : node->children) all = all && ch->fully_visited;
+        if (all) node->fully_visited = true;
+      }
+    }
+  }
+
   void backprop(MctsNode *node, const BenchResult &br) {
     for (; node; node = node->parent) {
       ++node->n;
@@ -604,9 +618,26 @@ SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &ben
     if (!root) seq = index.sequence_from_json(m.at("seq"));
 
     BenchResult br;
+    bool failed = false;
     if (!cached) {
       ScopedTimer t(C, "BENCHMARK");
-      br = bench.benchmark(seq, opts.bench);
+      if (opts.skip_failed) {
+        // preparation failures (e.g. a schedule that cannot be compiled to a hipGraph) are
+        // agreed on collectively by the benchmarker, so every rank skips the same candidate
+        try {
+          br = bench.benchmark(seq, opts.bench);
+        } catch (const std::exception &e) {
+          failed = true;
+          if (root) TZ_LOG(Warn, "mcts iter " << iter << ": candidate skipped: " << e.what());
+        }
+      } else {
+        br = bench.benchmark(seq, opts.bench);
+      }
+    }
+    if (root && failed) {
+      ++result.failed;
+      tree.prune_failed(bpStart);
+      continue;
     }
     if (root) {
       SimResult sr;
@@ -717,7 +748,17 @@ SearchResult dfs_explore(const Graph &g, const Platform &plat, Benchmarker &benc
     sr.seq = seq;
     {
       ScopedTimer t(result.counters, "BENCHMARK");
-      sr.res = bench.benchmark(seq, opts.bench);
+      try {
+        sr.res = bench.benchmark(seq, opts.bench);
+      } catch (const std::exception &e) {
+        // collective preparation failure: every rank skips this sequence
+        if (!opts.skip_failed) throw;
+        if (root) {
+          ++result.failed;
+          TZ_LOG(Warn, "dfs sequence " << i << " skipped: " << e.what());
+        }
+        continue;
+      }
     }
     if (root) {
       result.sims.push_back(sr);

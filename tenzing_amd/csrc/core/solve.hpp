@@ -40,6 +40,7 @@ struct SearchResult {
   size_t tree_size = 0;
   size_t tree_fully_visited = 0;
   std::string stop_reason;
+  size_t failed = 0; // candidates that could not be benchmarked (skipped)
 
   /// index of the best (lowest pct10) result, -1 if none
   int best() const;
@@ -91,6 +92,7 @@ struct MctsOpts {
   bool remove_redundant_syncs = true;
   bool reuse_measurements = true; // benchmark each equivalent final schedule once
   bool verify = true;           // race-check every candidate before it runs
+  bool skip_failed = true;      // a candidate whose benchmark throws is pruned, not fatal
   bool dump_tree = false;
   std::string dump_tree_prefix = "mcts_";
   std::string strategy = "FastMin";
@@ -120,6 +122,7 @@ struct DfsOpts {
   bool dedup_states = true;
   bool remove_redundant_syncs = true;
   bool trap_signals = false;
+  bool skip_failed = true; // a sequence whose benchmark throws is skipped, not fatal
   BenchOpts bench;
   Json json() const;
 };

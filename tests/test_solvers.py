@@ -159,3 +159,45 @@ def test_time_budget_stop(tz):
     o.bench = tz.BenchOpts(n_iters=2)
     r = tz.mcts_explore(g, tz.Platform(4), tz.SimBenchmarker(4), tz.SelfCtrl(), o)
     assert r.stop_reason in ("time_budget", "full_tree")
+
+
+def test_failed_candidates_are_skipped(tz):
+    """a candidate whose benchmark fails (e.g. cannot be compiled to a hipGraph) is pruned from
+    the tree instead of ending the search; DFS skips it too"""
+    g = tz.Graph()
+    k = {n: tz.SimGpuOp(n, t) for n, t in (("k1", 10), ("k2", 100), ("k3", 100), ("k4", 10))}
+    g.start_then(k["k1"])
+    g.then(k["k1"], k["k2"])
+    g.then(k["k1"], k["k3"])
+    g.then(k["k2"], k["k4"])
+    g.then(k["k3"], k["k4"])
+    g.then_finish(k["k4"])
+    sim = tz.SimBenchmarker(2)
+    calls = {"n": 0, "failed": 0}
+
+    def flaky(seq, opts):
+        calls["n"] += 1
+        # fail every schedule that runs k2 and k3 on different streams
+        streams = {o["name"]: o.get("stream") for o in json.loads(seq.json())}
+        if streams["k2"] != streams["k3"]:
+            calls["failed"] += 1
+            raise RuntimeError("cannot prepare this schedule")
+        return sim.benchmark(seq, opts)
+
+    bench = tz.PyBenchmarker(flaky)
+    o = tz.MctsOpts()
+    o.n_iters = 30
+    o.bench = tz.BenchOpts(n_iters=2)
+    r = tz.mcts_explore(g, tz.Platform(2), bench, tz.SelfCtrl(), o)
+    assert r.failed == calls["failed"] > 0
+    assert len(r.sims) + r.failed == 30 or r.stop_reason == "full_tree"
+    for s in r.sims:
+        st = {x["name"]: x.get("stream") for x in json.loads(s.seq.json())}
+        assert st["k2"] == st["k3"]
+    d = tz.DfsOpts()
+    d.bench = tz.BenchOpts(n_iters=2)
+    r2 = tz.dfs_explore(g, tz.Platform(2), bench, tz.SelfCtrl(), d)
+    assert r2.failed > 0 and len(r2.sims) > 0
+    o.skip_failed = False
+    with pytest.raises(Exception):
+        tz.mcts_explore(g, tz.Platform(2), bench, tz.SelfCtrl(), o)
