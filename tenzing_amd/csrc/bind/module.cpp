@@ -609,6 +609,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("py", &HaloArgs::py)
       .def_readwrite("pz", &HaloArgs::pz)
       .def_readwrite("pitch_pad", &HaloArgs::pitch_pad)
+      .def_readwrite("ghost_align", &HaloArgs::ghost_align)
       .def_readwrite("device", &HaloArgs::device)
       .def("json", [](const HaloArgs &a) { return a.json().dump(); });
   py::class_<HaloExchange, std::shared_ptr<HaloExchange>>(m, "HaloExchange")

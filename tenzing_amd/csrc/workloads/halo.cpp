@@ -31,6 +31,7 @@ Json HaloArgs::json() const {
   j["py"] = py;
   j["pz"] = pz;
   j["pitch_pad"] = pitch_pad;
+  j["ghost_align"] = ghost_align;
   return j;
 }
 
@@ -189,6 +190,8 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.order == "xyzq" || a_.order == "qxyz", "order must be xyzq or qxyz");
   TZ_CHECK(a_.rank >= 0 && a_.rank < a_.size, "bad rank");
   TZ_CHECK(a_.pitch_pad >= 0 && a_.pitch_pad % 16 == 0, "pitch_pad must be a multiple of 16");
+  TZ_CHECK(a_.ghost_align == 0 || a_.ghost_align == 8 || a_.ghost_align == 16,
+           "ghost_align must be 0, 8 or 16");
 
   // rank grid: prime factors (descending) multiply the currently smallest dimension, ties to
   // the later dimension (reference halo_run_strategy.hpp:80-98: 2 -> 1x1x2, 4 -> 1x2x2)
@@ -226,7 +229,10 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
 
   const int64_t X = a_.nx + 2 * a_.ghost, Y = a_.ny + 2 * a_.ghost, Z = a_.nz + 2 * a_.ghost;
   if (a_.order == "xyzq") {
-    xoff_ = (8 - a_.ghost % 8) % 8;                 // interior rows start 64-B aligned
+    // interior rows (and so the inner ends of the x ghost runs) start on a 64-B sector, or on
+    // a ghost_align boundary
+    const int64_t al = a_.ghost_align > 8 ? a_.ghost_align : 8;
+    xoff_ = (al - a_.ghost % al) % al;
     pitch_ = round_up(xoff_ + X, 16) + a_.pitch_pad; // rows are whole 128-B lines
     sy_ = pitch_;
     sz_ = pitch_ * Y;
@@ -255,6 +261,16 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
       }
     }
     xoff_ = best < 0 ? 0 : best;
+    if (a_.ghost_align > 0) {
+      // instead: the smallest padding that puts the inner ends of both x ghost runs on
+      // ghost_align boundaries (ghost-low ends, ghost-high starts there when q*n is a multiple
+      // of it); direct moves then widen the x ghost writes over the row padding to whole units
+      for (int64_t off = 0; off < 2 * a_.ghost_align; ++off)
+        if ((q * (off + g)) % a_.ghost_align == 0) {
+          xoff_ = off;
+          break;
+        }
+    }
     pitch_ = round_up(int64_t(a_.nq) * (xoff_ + X), 16) + a_.pitch_pad;
     sy_ = pitch_;
     sz_ = pitch_ * Y;
@@ -837,10 +853,37 @@ void HaloExchange::direct_group(const std::vector<int> &dirs, void *stream) cons
     m.n1 = s.n1;
     m.n2 = s.n2;
     m.n3 = s.n3;
+    if (a_.ghost_align > 0) widen_to_sectors(dirs_[opp_[i]].dx, m);
     ms.push_back(m);
   }
   for (size_t k = 0; k < ms.size(); k += kern::kMaxBoxes)
     kern::box_move_many(ms.data() + k, int(std::min<size_t>(kern::kMaxBoxes, ms.size() - k)), stream);
+}
+
+void HaloExchange::widen_to_sectors(int ghostDx, kern::MoveDesc &m) const {
+  // A move whose destination is an x ghost run (side -x: ghost-low, +x: ghost-high) writes a
+  // few elements less than whole 64-B sectors; the rest of those sectors is row padding (x < 0
+  // or x >= n + 2g), whose contents nobody reads. Widening source and destination rows over
+  // that padding turns every x-face write into full-sector writes (a partially written sector
+  // costs the memory a read-modify-write). Row strides are multiples of 16 elements, so the
+  // alignment of the first row holds for every row.
+  if (ghostDx == 0) return;
+  const int64_t rowLen = pitch_; // elements per (y[,q]) row, a multiple of 16
+  if (ghostDx < 0) {
+    const int64_t A = a_.ghost_align;
+    const int64_t x0 = m.dst_off % rowLen; // ghost-low: padding [0, x0) before it
+    const int64_t e = m.dst_off % A;
+    if (e > x0) return;
+    m.src_off -= e;
+    m.dst_off -= e;
+    m.len += int32_t(e);
+  } else {
+    const int64_t A = a_.ghost_align;
+    const int64_t end = m.dst_off % rowLen + m.len; // ghost-high: padding [end, rowLen) after
+    const int64_t e = (A - (m.dst_off + m.len) % A) % A;
+    if (end + e > rowLen) return;
+    m.len += int32_t(e);
+  }
 }
 
 std::vector<int> HaloExchange::pipelined_dirs() const {

@@ -116,6 +116,11 @@ struct HaloArgs {
   int rank = 0, size = 1;
   int px = 0, py = 0, pz = 0;     // rank grid (0 = from prime factors, reference style)
   int pitch_pad = 0;              // extra row-pitch elements (multiple of 16: keeps alignment)
+  // 8 or 16: the x padding puts the inner ends of the x ghost runs (ghost-low end, ghost-high
+  // start) on 8-element (64-B sector) / 16-element (128-B line) boundaries, and direct moves
+  // widen their x ghost writes over the neighbouring row padding to whole sectors / lines (no
+  // partially written sectors or lines on the x faces). 0: line-optimal padding, exact runs.
+  int ghost_align = 16;
   int device = -1;
   Json json() const;
 };
@@ -242,6 +247,7 @@ private:
   DeviceBuffer sent_; // per direction: puts issued so far (credit wait bookkeeping)
   std::vector<unsigned long long *> credit_ptrs(const std::vector<int> &dirs) const;
   const RcclComm &comm_for(int streamIdx, int dir) const;
+  void widen_to_sectors(int ghostDx, kern::MoveDesc &m) const;
   static constexpr int kDefaultComms = 8;
   bool ipcGrid_ = true;
   std::vector<void *> peerGrid_, peerFlags_; // per rank (nullptr: not a neighbour / self)
