@@ -8,6 +8,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 
@@ -1014,6 +1015,23 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via
     add_fused(*all, dirs, "all", via);
     std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped),
                               std::make_shared<StaticCompoundOp>(pre + "he_allfused", all)};
+    // remote directions to several peers: one chain per peer as well. Each peer is one xGMI
+    // link, so per-peer transfers on different streams use the links in parallel (copy-engine
+    // copies and RCCL groups issued on one stream would take them one at a time)
+    // Every rank must build the same graph (schedules are broadcast by op name): the split of
+    // directions by peer is the same on every rank of a periodic Cartesian grid, so groups are
+    // kept in order of their first direction and named after it, never after a rank id.
+    std::map<int, std::vector<int>> byPeer;
+    for (int i : dirs)
+      if (!direct_[i]) byPeer[nbr_[i]].push_back(i);
+    if (byPeer.size() > 1 && byPeer.size() < dirs.size()) {
+      std::vector<std::vector<int>> groupsByPeer;
+      for (const auto &kv : byPeer) groupsByPeer.push_back(kv.second);
+      std::sort(groupsByPeer.begin(), groupsByPeer.end());
+      auto peers = std::make_shared<Graph>();
+      for (const auto &grp : groupsByPeer) add_fused(*peers, grp, "p" + dirs_[grp.front()].name(), via);
+      top.push_back(std::make_shared<StaticCompoundOp>(pre + "he_bypeer", peers));
+    }
     auto choice = std::make_shared<StaticChoiceOp>(pre + "he_exchange", top);
     g.start_then(choice);
     g.then_finish(choice);

@@ -137,3 +137,25 @@ def test_explicit_rank_grid_neighbours_are_symmetric(tz, grid):
         for i in range(h.ndirs()):
             q = h.neighbor(i)
             assert hs[q].neighbor(h.opposite(i)) == r
+
+
+@pytest.mark.parametrize("size", [2, 4, 8])
+@pytest.mark.parametrize("transport", ["auto", "rccl", "ipc"])
+def test_every_rank_builds_the_same_op_names(tz, size, transport, monkeypatch):
+    """schedules are broadcast from rank 0 by op name: every rank's graph must contain the same
+    names for every alternative (per-peer groups included), in both IPC modes"""
+    from tenzing_amd.models import HaloConfig
+
+    for grid_mode in ("0", "1"):
+        monkeypatch.setenv("TZ_IPC_GRID", grid_mode)
+        graphs = []
+        for r in range(size):
+            h = tz._tz.HaloExchange(HaloConfig(n=32, neighbors=26, order="qxyz", fuse="choice",
+                                               transport=transport).args(r, size, -1))
+            g = tz.Graph()
+            h.add_to_graph(g)
+            graphs.append(g)
+        for seed in range(25):
+            js = tz.random_rollout(tz.State(graphs[0], tz.Platform(4)), seed).json(True)
+            for g in graphs[1:]:
+                tz.OpIndex(g).sequence_from_json(js)
