@@ -68,8 +68,10 @@ def main() -> int:
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=40)
     ap.add_argument("--search-budget-s", type=float, default=120.0)
-    ap.add_argument("--bench-iters", type=int, default=20)
-    ap.add_argument("--target-secs", type=float, default=0.004)
+    # per candidate: 10 measurements of >= 3 ms each. 20 x 4 ms finds the same best schedule
+    # with twice the search time (profiles/r1_search_len/bench_settings.txt)
+    ap.add_argument("--bench-iters", type=int, default=10)
+    ap.add_argument("--target-secs", type=float, default=0.003)
     ap.add_argument("--strategy", default="FastMin")
     ap.add_argument("--search-mode", default="graph", choices=["eager", "graph"],
                     help="benchmark candidates eagerly or compiled to hipGraphs (default: graph, "
