@@ -28,7 +28,7 @@ ARCH = os.environ.get("TZ_OFFLOAD_ARCH", "gfx950")
 CORE = ["json", "numeric", "ops", "graph", "state", "serdes", "ctrl", "benchmark", "solve"]
 HIP_HOST = ["hip_runtime", "rccl_comm", "rocsparse_spmv"]
 WORKLOADS = ["halo", "spmv", "workloads_common"]
-KERNELS = ["halo_kernels", "spmv_kernels"]
+KERNELS = ["halo_kernels", "spmv_kernels", "stencil_kernels"]
 
 
 def _git_hash() -> str:

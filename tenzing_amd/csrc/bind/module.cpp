@@ -725,6 +725,27 @@ PYBIND11_MODULE(_tz, m) {
            py::arg("val"), py::arg("x"), py::arg("y"), py::arg("alg") = "adaptive")
       .def("run", [](const RocsparseCsr &r, uintptr_t s, bool acc) { r.run(P(s), acc); },
            py::arg("stream") = 0, py::arg("accumulate") = false);
+  k.def("stencil7", [](uintptr_t in, uintptr_t out, int64_t base, int row, int ny, int nz,
+                       int nouter, int64_t sy, int64_t sz, int64_t so, int xs, double c0, double c1,
+                       bool lds, uintptr_t s) {
+    kern::StencilBox b;
+    b.in = reinterpret_cast<const double *>(in);
+    b.out = reinterpret_cast<double *>(out);
+    b.base = base;
+    b.row = row;
+    b.ny = ny;
+    b.nz = nz;
+    b.nouter = nouter;
+    b.sy = sy;
+    b.sz = sz;
+    b.so = so;
+    b.xs = xs;
+    b.c0 = c0;
+    b.c1 = c1;
+    kern::stencil7(b, lds, P(s));
+  }, py::arg("in_"), py::arg("out"), py::arg("base"), py::arg("row"), py::arg("ny"), py::arg("nz"),
+     py::arg("nouter"), py::arg("sy"), py::arg("sz"), py::arg("so"), py::arg("xs"),
+     py::arg("c0") = 0.4, py::arg("c1") = 0.1, py::arg("lds") = true, py::arg("stream") = 0);
   k.def("gather_f32", [](int n, uintptr_t src, uintptr_t idx, uintptr_t dst, uintptr_t s) {
     kern::gather_f32(n, reinterpret_cast<const float *>(src), reinterpret_cast<const int32_t *>(idx),
                      reinterpret_cast<float *>(dst), P(s));

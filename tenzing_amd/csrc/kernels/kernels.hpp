@@ -118,6 +118,21 @@ void empty(void *stream);
 /// spin for `ticks` of the constant-rate wall clock (synthetic device work for scheduling tests)
 void busy_wait(int64_t ticks, int blocks, void *stream);
 
+/// A box of the halo grid for the 7-point stencil (see stencil_kernels.hip). Element (i, y, z,
+/// o) of the box is at base + o*so + z*sz + y*sy + i, for i < row (a contiguous run), y < ny,
+/// z < nz, o < nouter; its x neighbours are +-xs away. The box must have a one-cell apron of
+/// valid memory (ghosts) on every side.
+struct StencilBox {
+  const double *in = nullptr;
+  double *out = nullptr;
+  int64_t base = 0, sy = 0, sz = 0, so = 0;
+  int32_t row = 0, ny = 0, nz = 0, nouter = 1, xs = 1;
+  double c0 = 0.4, c1 = 0.1;
+};
+/// out = c0 * in + c1 * (sum of the 6 face neighbours) over the box; `lds`: 2.5-D LDS-tiled
+/// kernel, else neighbours straight from global memory (both march z with a register queue)
+void stencil7(const StencilBox &b, bool lds, void *stream);
+
 /// Halo grid geometry for init / verification kernels.
 struct HaloGeom {
   int32_t order = 0; // 0 = XYZQ (x fastest, q slowest, x-padded rows), 1 = QXYZ

@@ -144,3 +144,43 @@ def test_vector_kernels(tz, gpu):
     assert torch.equal(g, a[idx.long()])
     assert torch.allclose(yd, yd0 + 2.5 * xd)
     assert torch.equal(io, 3.0 + 0.5 * torch.arange(1000, dtype=torch.float64, device="cuda"))
+
+
+@pytest.mark.parametrize("lds", [True, False])
+@pytest.mark.parametrize("order", ["qxyz", "xyzq"])
+def test_stencil7_matches_torch(tz, gpu, order, lds):
+    """7-point stencil over a box with a one-cell apron, both storage orders, box extents that
+    are not multiples of the tile (64 x 8 x 32), against a torch fp64 reference"""
+    torch = pytest.importorskip("torch")
+    nq, nx, ny, nz, pad = 3, 100, 37, 45, 5
+    c0, c1 = 0.4, 0.1
+    if order == "qxyz":
+        P = nq * (nx + 2 + 2 * pad)
+        G = torch.randn(nz + 2, ny + 2, P, dtype=torch.float64, device="cuda")
+        O = torch.zeros_like(G)
+        x0 = nq * (1 + pad)  # first box element in a row
+        row, xs, sy, sz, so, nouter = nq * nx, nq, P, P * (ny + 2), 0, 1
+        base = sz + sy + x0
+
+        def sl(t, dz, dy, dx):
+            return t[1 + dz:nz + 1 + dz, 1 + dy:ny + 1 + dy, x0 + dx:x0 + dx + row]
+    else:
+        P = nx + 2 + 2 * pad
+        G = torch.randn(nq, nz + 2, ny + 2, P, dtype=torch.float64, device="cuda")
+        O = torch.zeros_like(G)
+        x0 = 1 + pad
+        row, xs, sy, sz, nouter = nx, 1, P, P * (ny + 2), nq
+        so = sz * (nz + 2)
+        base = sz + sy + x0
+
+        def sl(t, dz, dy, dx):
+            return t[:, 1 + dz:nz + 1 + dz, 1 + dy:ny + 1 + dy, x0 + dx:x0 + dx + row]
+    tz._tz.kernels.stencil7(G.data_ptr(), O.data_ptr(), base, row, ny, nz, nouter, sy, sz, so, xs,
+                            c0, c1, lds, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = c0 * sl(G, 0, 0, 0) + c1 * (sl(G, 0, 0, -xs) + sl(G, 0, 0, xs) + sl(G, 0, -1, 0) +
+                                      sl(G, 0, 1, 0) + sl(G, -1, 0, 0) + sl(G, 1, 0, 0))
+    got = sl(O, 0, 0, 0)
+    assert torch.allclose(got, ref, rtol=1e-13, atol=1e-13), (got - ref).abs().max()
+    # nothing outside the box is written
+    assert float(O.abs().sum()) == pytest.approx(float(got.abs().sum()), rel=1e-12)
