@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""7-point stencil kernel on the halo workload's 512^3 x 3 f64 grid: LDS-tiled vs direct, both
+storage orders; effective HBM rate = (interior bytes read + written) / time.
+
+  python scripts/stencil_bench.py [--n 512] [--reps 20]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import tenzing_amd as tz  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    n, nq, g = a.n, 3, 3
+    st = torch.cuda.current_stream().cuda_stream
+    for order in ("qxyz", "xyzq"):
+        if order == "qxyz":
+            P = nq * (n + 2 * g + 16)
+            G = torch.randn(n + 2 * g, n + 2 * g, P, dtype=torch.float64, device="cuda")
+            x0 = nq * (g + 13)
+            row, xs, sy, sz, so, nouter = nq * n, nq, P, P * (n + 2 * g), 0, 1
+        else:
+            P = n + 2 * g + 16
+            G = torch.randn(nq, n + 2 * g, n + 2 * g, P, dtype=torch.float64, device="cuda")
+            x0 = g + 13
+            row, xs, sy, sz, nouter = n, 1, P, P * (n + 2 * g), nq
+            so = sz * (n + 2 * g)
+        O = torch.empty_like(G)
+        base = g * sz + g * sy + x0
+        nbytes = 2 * 8 * n ** 3 * nq
+        configs = [(True, ty, zc) for ty in (4, 8, 16) for zc in (32, 64)] + [(False, 8, 32)]
+        for lds, ty, zc in configs:
+            tz._tz.kernels.set_stencil_tuning(ty, zc)
+
+            def fn():
+                tz._tz.kernels.stencil7(G.data_ptr(), O.data_ptr(), base, row, n, n, nouter, sy, sz,
+                                        so, xs, 0.4, 0.1, lds, st)
+            for _ in range(3):
+                fn()
+            ts = []
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3)
+            us = statistics.median(ts)
+            print(json.dumps({"order": order, "lds": lds, "ty": ty, "zc": zc, "us": round(us, 1),
+                              "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
+        del G, O
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -129,6 +129,12 @@ struct StencilBox {
   int32_t row = 0, ny = 0, nz = 0, nouter = 1, xs = 1;
   double c0 = 0.4, c1 = 0.1;
 };
+/// stencil launch shape: rows per workgroup tile (4, 8, 16) and planes per z chunk (32, 64)
+struct StencilTuning {
+  int ty = 16; // 64 x 16 tiles, 64-plane chunks: 4.2 TB/s at 512^3 x 3 (scripts/stencil_bench.py)
+  int zc = 64;
+};
+StencilTuning &stencil_tuning();
 /// out = c0 * in + c1 * (sum of the 6 face neighbours) over the box; `lds`: 2.5-D LDS-tiled
 /// kernel, else neighbours straight from global memory (both march z with a register queue)
 void stencil7(const StencilBox &b, bool lds, void *stream);

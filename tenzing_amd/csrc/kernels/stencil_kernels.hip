@@ -18,6 +18,7 @@
 
 #include "kernels.hpp"
 
+#include <cstdint>
 #include <stdexcept>
 #include <string>
 
@@ -33,87 +34,183 @@ namespace {
       throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e_));     \
   } while (0)
 
-constexpr int TX = 64, TY = 8, XS_MAX = 4, ZC = 32;
-constexpr int LW = TX + 2 * XS_MAX; // LDS row width (doubles)
+constexpr int TX = 64, XS_MAX = 4;
 
 __device__ __forceinline__ double ldnt(const double *p) { return __builtin_nontemporal_load(p); }
 
-template <bool LDS>
+typedef double dbl2_t __attribute__((ext_vector_type(2)));
+
+// VX consecutive elements per thread (VX = 2: 16-B loads/stores of the z queue and the output)
+template <int VX> struct VT;
+template <> struct VT<1> {
+  using T = double;
+  __device__ static T zero() { return 0.0; }
+  __device__ static double get(const T &v, int) { return v; }
+};
+template <> struct VT<2> {
+  using T = dbl2_t;
+  __device__ static T zero() { return T{0.0, 0.0}; }
+  __device__ static double get(const T &v, int k) { return k ? v.y : v.x; }
+};
+
+template <bool LDS, int VX, int TY, int ZC>
 __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
+  using V = VT<VX>;
+  using T = typename V::T;
+  constexpr int W = TX * VX;              // elements per tile row
+  constexpr int LW = W + 2 * XS_MAX;      // LDS row width
   __shared__ double tile[TY + 2][LW];
   const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
-  const int r = blockIdx.x * TX + tx;          // element within the row
-  const int y = blockIdx.y * TY + ty;          // row
+  const int r = blockIdx.x * W + tx * VX; // first element of this thread within the row
+  const int y = blockIdx.y * TY + ty;     // row
   const int zChunks = (b.nz + ZC - 1) / ZC;
-  const int outer = blockIdx.z / zChunks;      // XYZQ: quantity
+  const int outer = blockIdx.z / zChunks; // XYZQ: quantity
   const int z0 = (blockIdx.z % zChunks) * ZC;
   const int z1 = min(z0 + ZC, b.nz);
-  const bool mine = r < b.row && y < b.ny; // an output element of the box
+  // VX = 2 launches only when row is even: a thread's two elements are both in or both out
+  const bool mine = r < b.row && y < b.ny; // output elements of the box
   // the x / y neighbours of the box's last column / row are elements just outside the box:
   // threads there still load their (real) value into the tile
   const bool live = LDS ? (r < b.row + b.xs && y <= b.ny) : mine;
   const int64_t e0 = b.base + int64_t(outer) * b.so + int64_t(y) * b.sy + r; // plane 0 offset
   const double *in = b.in;
+  auto load = [&](int64_t e) { return *reinterpret_cast<const T *>(in + e); };
 
-  // registers: z - 1 and z of this element (z + 1 is loaded inside the loop)
-  double prev = mine ? in[e0 + int64_t(z0 - 1) * b.sz] : 0.0;
-  double cur = live ? in[e0 + int64_t(z0) * b.sz] : 0.0;
+  // apron cells of the LDS tile (xs columns left/right, one row above/below): each thread owns
+  // up to two, and loads them one plane ahead like the z queue, so no load sits between a
+  // plane's barrier and its compute
+  constexpr int NAPRON = 2 * LW + 2 * TY * XS_MAX;
+  constexpr int NT = TX * TY;
+  int alr[2], alc[2], agr[2], agy[2];
+  bool aok[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int k = threadIdx.x + a * NT;
+    int lr = 0, lc = 0;
+    if (k < 2 * LW) {
+      lr = k < LW ? 0 : TY + 1;
+      lc = k % LW;
+    } else if (k < NAPRON) {
+      const int j = k - 2 * LW;
+      lr = 1 + j / (2 * XS_MAX);
+      const int c = j % (2 * XS_MAX);
+      lc = c < XS_MAX ? c : W + c; // left apron [0, XS_MAX), right [W+XS_MAX, LW)
+    }
+    alr[a] = lr;
+    alc[a] = lc;
+    agr[a] = blockIdx.x * W + lc - XS_MAX;
+    agy[a] = blockIdx.y * TY + lr - 1;
+    // apron cells outside [-xs, row + xs) x [-1, ny] feed no stored output: never loaded
+    aok[a] = LDS && k < NAPRON && agr[a] >= -b.xs && agr[a] < b.row + b.xs && agy[a] >= -1 &&
+             agy[a] <= b.ny;
+  }
+  const int64_t pbase = b.base + int64_t(outer) * b.so;
+  auto apron = [&](int a, int z) {
+    return aok[a] ? in[pbase + int64_t(z) * b.sz + int64_t(agy[a]) * b.sy + agr[a]] : 0.0;
+  };
+
+  // register queue: planes z - 1, z, z + 1 of my elements; z + 2 is prefetched one plane ahead
+  T prev = mine ? load(e0 + int64_t(z0 - 1) * b.sz) : V::zero();
+  T cur = live ? load(e0 + int64_t(z0) * b.sz) : V::zero();
+  T next = live ? load(e0 + int64_t(z0 + 1) * b.sz) : V::zero();
+  double ap0 = apron(0, z0), ap1 = apron(1, z0);
   for (int z = z0; z < z1; ++z) {
     const int64_t e = e0 + int64_t(z) * b.sz;
-    const double next = live ? ldnt(in + e + b.sz) : 0.0;
-    double xm, xp, ym, yp;
+    // z + 2 is at most plane nz (the ghost plane) of the last chunk
+    T nn = V::zero();
+    if (live && z + 2 <= b.nz) nn = __builtin_nontemporal_load(reinterpret_cast<const T *>(in + e + 2 * b.sz));
+    double xm[VX], xp[VX], ym[VX], yp[VX];
     if (LDS) {
-      // this plane: my element, plus the apron (xs columns left/right, one row above/below)
-      tile[ty + 1][tx + XS_MAX] = cur;
-      const int64_t p = b.base + int64_t(outer) * b.so + int64_t(z) * b.sz;
-      const int rx0 = blockIdx.x * TX, ry0 = blockIdx.y * TY;
-      for (int k = threadIdx.x; k < 2 * LW + 2 * TY * XS_MAX; k += TX * TY) {
-        int lr, lc; // LDS row / column
-        if (k < 2 * LW) {
-          lr = k < LW ? 0 : TY + 1;
-          lc = k % LW;
-        } else {
-          const int j = k - 2 * LW;
-          lr = 1 + j / (2 * XS_MAX);
-          const int c = j % (2 * XS_MAX);
-          lc = c < XS_MAX ? c : TX + c; // left apron [0, XS_MAX), right [TX+XS_MAX, LW)
-        }
-        const int gr = rx0 + lc - XS_MAX, gy = ry0 + lr - 1;
-        // apron cells outside [-xs, row + xs) x [-1, ny] feed no stored output: skip them
-        const bool ok = gr >= -b.xs && gr < b.row + b.xs && gy >= -1 && gy <= b.ny;
-        tile[lr][lc] = ok ? in[p + int64_t(gy) * b.sy + gr] : 0.0;
+#pragma unroll
+      for (int k = 0; k < VX; ++k) tile[ty + 1][XS_MAX + tx * VX + k] = V::get(cur, k);
+      if (aok[0]) tile[alr[0]][alc[0]] = ap0;
+      if (aok[1]) tile[alr[1]][alc[1]] = ap1;
+      // next plane's apron (plane z + 1 <= nz exists)
+      if (z + 1 < z1) {
+        ap0 = apron(0, z + 1);
+        ap1 = apron(1, z + 1);
       }
       __syncthreads();
-      xm = tile[ty + 1][tx + XS_MAX - b.xs];
-      xp = tile[ty + 1][tx + XS_MAX + b.xs];
-      ym = tile[ty][tx + XS_MAX];
-      yp = tile[ty + 2][tx + XS_MAX];
+#pragma unroll
+      for (int k = 0; k < VX; ++k) {
+        const int c = XS_MAX + tx * VX + k;
+        xm[k] = tile[ty + 1][c - b.xs];
+        xp[k] = tile[ty + 1][c + b.xs];
+        ym[k] = tile[ty][c];
+        yp[k] = tile[ty + 2][c];
+      }
     } else {
-      xm = mine ? in[e - b.xs] : 0.0;
-      xp = mine ? in[e + b.xs] : 0.0;
-      ym = mine ? in[e - b.sy] : 0.0;
-      yp = mine ? in[e + b.sy] : 0.0;
+#pragma unroll
+      for (int k = 0; k < VX; ++k) {
+        xm[k] = mine ? in[e + k - b.xs] : 0.0;
+        xp[k] = mine ? in[e + k + b.xs] : 0.0;
+        ym[k] = mine ? in[e + k - b.sy] : 0.0;
+        yp[k] = mine ? in[e + k + b.sy] : 0.0;
+      }
     }
-    if (mine)
-      __builtin_nontemporal_store(b.c0 * cur + b.c1 * (xm + xp + ym + yp + prev + next), b.out + e);
+    if (mine) {
+      T o;
+      if constexpr (VX == 1) {
+        o = b.c0 * cur + b.c1 * (xm[0] + xp[0] + ym[0] + yp[0] + prev + next);
+      } else {
+        o.x = b.c0 * cur.x + b.c1 * (xm[0] + xp[0] + ym[0] + yp[0] + prev.x + next.x);
+        o.y = b.c0 * cur.y + b.c1 * (xm[1] + xp[1] + ym[1] + yp[1] + prev.y + next.y);
+      }
+      __builtin_nontemporal_store(o, reinterpret_cast<T *>(b.out + e));
+    }
     if (LDS) __syncthreads(); // the tile is rewritten for the next plane
     prev = cur;
     cur = next;
+    next = nn;
   }
 }
 
+} // namespace
+
+StencilTuning &stencil_tuning() {
+  static StencilTuning t;
+  return t;
+}
+
+namespace {
+template <bool LDS, int VX, int TY, int ZC>
+void launch_stencil(const StencilBox &b, hipStream_t s) {
+  const int W = TX * VX;
+  const int zChunks = (b.nz + ZC - 1) / ZC;
+  const dim3 g(unsigned((b.row + W - 1) / W), unsigned((b.ny + TY - 1) / TY),
+               unsigned(zChunks * b.nouter));
+  hipLaunchKernelGGL((stencil7_k<LDS, VX, TY, ZC>), g, dim3(TX * TY), 0, s, b);
+}
+
+template <bool LDS, int VX>
+void launch_ty(const StencilBox &b, hipStream_t s) {
+  const StencilTuning &t = stencil_tuning();
+  if (t.ty == 4) {
+    if (t.zc == 64) launch_stencil<LDS, VX, 4, 64>(b, s);
+    else launch_stencil<LDS, VX, 4, 32>(b, s);
+  } else if (t.ty == 16) {
+    if (t.zc == 64) launch_stencil<LDS, VX, 16, 64>(b, s);
+    else launch_stencil<LDS, VX, 16, 32>(b, s);
+  } else {
+    if (t.zc == 64) launch_stencil<LDS, VX, 8, 64>(b, s);
+    else launch_stencil<LDS, VX, 8, 32>(b, s);
+  }
+}
 } // namespace
 
 void stencil7(const StencilBox &b, bool lds, void *stream) {
   if (b.row <= 0 || b.ny <= 0 || b.nz <= 0 || b.nouter <= 0) return;
   if (!b.in || !b.out) throw std::runtime_error("stencil7: null grid");
   if (b.xs < 1 || b.xs > XS_MAX) throw std::runtime_error("stencil7: x neighbour distance must be 1..4");
-  const int zChunks = (b.nz + ZC - 1) / ZC;
-  const dim3 g(unsigned((b.row + TX - 1) / TX), unsigned((b.ny + TY - 1) / TY),
-               unsigned(zChunks * b.nouter));
+  // two elements per thread (16-B accesses) when every row of the box starts 16-B aligned
+  const bool v2 = b.row % 2 == 0 && b.base % 2 == 0 && b.sy % 2 == 0 && b.sz % 2 == 0 &&
+                  b.so % 2 == 0 && reinterpret_cast<uintptr_t>(b.in) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(b.out) % 16 == 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (lds) hipLaunchKernelGGL(stencil7_k<true>, g, dim3(TX * TY), 0, s, b);
-  else hipLaunchKernelGGL(stencil7_k<false>, g, dim3(TX * TY), 0, s, b);
+  if (lds && v2) launch_ty<true, 2>(b, s);
+  else if (lds) launch_ty<true, 1>(b, s);
+  else if (v2) launch_ty<false, 2>(b, s);
+  else launch_ty<false, 1>(b, s);
   TZ_HIP_LAUNCH_CHECK();
 }
 
