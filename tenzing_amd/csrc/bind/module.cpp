@@ -610,6 +610,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("pz", &HaloArgs::pz)
       .def_readwrite("pitch_pad", &HaloArgs::pitch_pad)
       .def_readwrite("ghost_align", &HaloArgs::ghost_align)
+      .def_readwrite("stencil", &HaloArgs::stencil)
       .def_readwrite("device", &HaloArgs::device)
       .def("json", [](const HaloArgs &a) { return a.json().dump(); });
   py::class_<HaloExchange, std::shared_ptr<HaloExchange>>(m, "HaloExchange")
@@ -634,6 +635,9 @@ PYBIND11_MODULE(_tz, m) {
       .def("grid_ptr", [](const HaloExchange &h) { return reinterpret_cast<uintptr_t>(h.grid()); })
       .def("init_grid", [](HaloExchange &h, uintptr_t s) { h.init_grid(P(s)); }, py::arg("stream") = 0)
       .def("check_grid", [](HaloExchange &h, uintptr_t s) { return h.check_grid(P(s)); }, py::arg("stream") = 0)
+      .def("check_stencil", [](HaloExchange &h, uintptr_t s) { return h.check_stencil(P(s)); }, py::arg("stream") = 0)
+      .def("stencil", [](const HaloExchange &h, int region, uintptr_t s) { h.stencil(region, P(s)); },
+           py::arg("region"), py::arg("stream") = 0)
       .def("pack", [](const HaloExchange &h, int i, uintptr_t s) { h.pack(i, P(s)); })
       .def("unpack", [](const HaloExchange &h, int i, uintptr_t s) { h.unpack(i, P(s)); })
       .def("shift", [](const HaloExchange &h, int i, uintptr_t s) { h.shift(i, P(s)); })

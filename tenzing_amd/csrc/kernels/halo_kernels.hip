@@ -408,7 +408,46 @@ __global__ __launch_bounds__(kThreads) void halo_check_k(const double *__restric
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(count, bad);
 }
 
+// stencil mode: out must hold c0 * v + c1 * (6 face neighbours of v) of the initialized field v
+// (global coordinates, periodic), for every interior cell; counts the cells that do not
+__global__ __launch_bounds__(kThreads) void stencil_check_k(const double *__restrict__ out, HaloGeom g,
+                                                            double c0, double c1,
+                                                            unsigned long long *count) {
+  const int64_t total = int64_t(g.nx) * g.ny * g.nz * g.nq;
+  const int64_t GX = int64_t(g.nx) * g.px, GY = int64_t(g.ny) * g.py, GZ = int64_t(g.nz) * g.pz;
+  unsigned long long bad = 0;
+  for (int64_t lin = int64_t(blockIdx.x) * kThreads + threadIdx.x; lin < total;
+       lin += int64_t(gridDim.x) * kThreads) {
+    const int64_t x = lin % g.nx;
+    int64_t r = lin / g.nx;
+    const int64_t y = r % g.ny;
+    r /= g.ny;
+    const int64_t z = r % g.nz;
+    const int q = int(r / g.nz);
+    const int64_t X = x + g.g, Y = y + g.g, Z = z + g.g; // storage coordinates
+    const int64_t idx = g.order == 0 ? q * g.sq + Z * g.sz + Y * g.sy + X + g.xoff
+                                     : q + int64_t(g.nq) * (X + g.xoff) + Y * g.sy + Z * g.sz;
+    const int64_t gx = int64_t(g.cx) * g.nx + x, gy = int64_t(g.cy) * g.ny + y,
+                  gz = int64_t(g.cz) * g.nz + z;
+    auto v = [&](int64_t dx, int64_t dy, int64_t dz) {
+      return halo_value(q, wrapi(gx + dx, GX), wrapi(gy + dy, GY), wrapi(gz + dz, GZ));
+    };
+    const double want = c0 * v(0, 0, 0) + c1 * (v(-1, 0, 0) + v(1, 0, 0) + v(0, -1, 0) +
+                                                v(0, 1, 0) + v(0, 0, -1) + v(0, 0, 1));
+    bad += fabs(out[idx] - want) > 1e-12 * fabs(want) + 1e-9;
+  }
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_xor(bad, off);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(count, bad);
+}
+
 } // namespace
+
+void stencil_check(const double *out, const HaloGeom &g, unsigned long long *count, void *stream) {
+  const StencilBox defaults;
+  hipLaunchKernelGGL(stencil_check_k, dim3(4096), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     out, g, defaults.c0, defaults.c1, count);
+  TZ_HIP_LAUNCH_CHECK();
+}
 
 void halo_init(double *grid, const HaloGeom &g, void *stream) {
   hipLaunchKernelGGL(halo_init_k, dim3(4096), dim3(kThreads), 0, static_cast<hipStream_t>(stream),

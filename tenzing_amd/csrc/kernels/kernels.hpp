@@ -127,6 +127,10 @@ struct StencilBox {
   double *out = nullptr;
   int64_t base = 0, sy = 0, sz = 0, so = 0;
   int32_t row = 0, ny = 0, nz = 0, nouter = 1, xs = 1;
+  // elements at the start / end of every row that are neither stored nor read beyond: a box
+  // can keep an aligned row (16-B accesses) while excluding its first / last x cells (the
+  // ghost-free interior); the masked elements then need no apron on that side
+  int32_t m0 = 0, m1 = 0;
   double c0 = 0.4, c1 = 0.1;
 };
 /// stencil launch shape: rows per workgroup tile (4, 8, 16) and planes per z chunk (32, 64)
@@ -138,6 +142,10 @@ StencilTuning &stencil_tuning();
 /// out = c0 * in + c1 * (sum of the 6 face neighbours) over the box; `lds`: 2.5-D LDS-tiled
 /// kernel, else neighbours straight from global memory (both march z with a register queue)
 void stencil7(const StencilBox &b, bool lds, void *stream);
+/// a box one or a few cells thick (the boundary shell) goes to a one-thread-per-element kernel
+bool stencil_thin(const StencilBox &b);
+/// several thin boxes in one launch
+void stencil7_thin_many(const StencilBox *b, int n, void *stream);
 
 /// Halo grid geometry for init / verification kernels.
 struct HaloGeom {
@@ -151,6 +159,9 @@ struct HaloGeom {
 void halo_init(double *grid, const HaloGeom &g, void *stream);
 /// count elements that differ from what a completed exchange must leave; result in *count
 void halo_check(const double *grid, const HaloGeom &g, unsigned long long *count, void *stream);
+/// stencil mode: count interior cells of `out` that differ from the 7-point stencil (default
+/// coefficients) of the field halo_init writes (global coordinates, periodic)
+void stencil_check(const double *out, const HaloGeom &g, unsigned long long *count, void *stream);
 
 } // namespace kern
 } // namespace tz

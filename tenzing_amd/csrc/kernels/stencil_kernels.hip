@@ -18,6 +18,7 @@
 
 #include "kernels.hpp"
 
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -68,10 +69,14 @@ __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
   const int z0 = (blockIdx.z % zChunks) * ZC;
   const int z1 = min(z0 + ZC, b.nz);
   // VX = 2 launches only when row is even: a thread's two elements are both in or both out
-  const bool mine = r < b.row && y < b.ny; // output elements of the box
+  // output elements of the box (m0 / m1 masked at the row ends); VX = 2 pairs straddling a
+  // mask edge store element by element
+  const int rlo = b.m0, rhi = b.row - b.m1;
+  const bool mine = r + VX > rlo && r < rhi && y < b.ny;
   // the x / y neighbours of the box's last column / row are elements just outside the box:
-  // threads there still load their (real) value into the tile
-  const bool live = LDS ? (r < b.row + b.xs && y <= b.ny) : mine;
+  // threads there still load their (real) value into the tile (never past the masked ends)
+  const int llo = rlo - b.xs, lhi = rhi + b.xs;
+  const bool live = LDS ? (r + VX > llo && r < lhi && y <= b.ny) : mine;
   const int64_t e0 = b.base + int64_t(outer) * b.so + int64_t(y) * b.sy + r; // plane 0 offset
   const double *in = b.in;
   auto load = [&](int64_t e) { return *reinterpret_cast<const T *>(in + e); };
@@ -101,8 +106,7 @@ __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
     agr[a] = blockIdx.x * W + lc - XS_MAX;
     agy[a] = blockIdx.y * TY + lr - 1;
     // apron cells outside [-xs, row + xs) x [-1, ny] feed no stored output: never loaded
-    aok[a] = LDS && k < NAPRON && agr[a] >= -b.xs && agr[a] < b.row + b.xs && agy[a] >= -1 &&
-             agy[a] <= b.ny;
+    aok[a] = LDS && k < NAPRON && agr[a] >= llo && agr[a] < lhi && agy[a] >= -1 && agy[a] <= b.ny;
   }
   const int64_t pbase = b.base + int64_t(outer) * b.so;
   auto apron = [&](int a, int z) {
@@ -152,11 +156,17 @@ __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
       T o;
       if constexpr (VX == 1) {
         o = b.c0 * cur + b.c1 * (xm[0] + xp[0] + ym[0] + yp[0] + prev + next);
+        __builtin_nontemporal_store(o, b.out + e);
       } else {
         o.x = b.c0 * cur.x + b.c1 * (xm[0] + xp[0] + ym[0] + yp[0] + prev.x + next.x);
         o.y = b.c0 * cur.y + b.c1 * (xm[1] + xp[1] + ym[1] + yp[1] + prev.y + next.y);
+        if (r >= rlo && r + 1 < rhi) {
+          __builtin_nontemporal_store(o, reinterpret_cast<T *>(b.out + e));
+        } else {
+          if (r >= rlo) b.out[e] = o.x;
+          if (r + 1 >= rlo && r + 1 < rhi) b.out[e + 1] = o.y;
+        }
       }
-      __builtin_nontemporal_store(o, reinterpret_cast<T *>(b.out + e));
     }
     if (LDS) __syncthreads(); // the tile is rewritten for the next plane
     prev = cur;
@@ -165,7 +175,70 @@ __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
   }
 }
 
+// thin boxes (the one-cell boundary shell): one thread per output element, neighbours from
+// global memory (L2) — a z-march or a 64-wide tile would leave most lanes idle on a slab that
+// is one cell thick. Up to kMaxFlat boxes in one launch (blocks map to boxes through a prefix
+// table), 4 elements in flight per thread.
+constexpr int kMaxFlat = 8;
+struct FlatBatch {
+  StencilBox b[kMaxFlat];
+  uint32_t block_start[kMaxFlat + 1];
+  int32_t n;
+};
+
+__device__ __forceinline__ void flat_one(const StencilBox &b, int64_t it) {
+  const int64_t i = it % b.row;
+  if (i < b.m0 || i >= b.row - b.m1) return;
+  int64_t r = it / b.row;
+  const int64_t y = r % b.ny;
+  r /= b.ny;
+  const int64_t z = r % b.nz;
+  const int64_t o = r / b.nz;
+  const int64_t e = b.base + o * b.so + z * b.sz + y * b.sy + i;
+  const double *in = b.in;
+  b.out[e] = b.c0 * in[e] + b.c1 * (in[e - b.xs] + in[e + b.xs] + in[e - b.sy] + in[e + b.sy] +
+                                    in[e - b.sz] + in[e + b.sz]);
+}
+
+__global__ __launch_bounds__(256) void stencil7_flat_k(FlatBatch fb) {
+  int k = 0;
+  while (k + 1 < fb.n && blockIdx.x >= fb.block_start[k + 1]) ++k;
+  const StencilBox &b = fb.b[k];
+  const int64_t total = int64_t(b.row) * b.ny * b.nz * b.nouter;
+  const int64_t nth = int64_t(fb.block_start[k + 1] - fb.block_start[k]) * 256;
+  int64_t it = int64_t(blockIdx.x - fb.block_start[k]) * 256 + threadIdx.x;
+  for (; it + 3 * nth < total; it += 4 * nth) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) flat_one(b, it + u * nth);
+  }
+  for (; it < total; it += nth) flat_one(b, it);
+}
+
 } // namespace
+
+bool stencil_thin(const StencilBox &b) { return b.nz < 4 || b.ny < 4 || b.row < 32; }
+
+void stencil7_thin_many(const StencilBox *boxes, int n, void *stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int k0 = 0; k0 < n; k0 += kMaxFlat) {
+    FlatBatch fb{};
+    uint32_t total = 0;
+    for (int k = k0; k < n && fb.n < kMaxFlat; ++k) {
+      const StencilBox &b = boxes[k];
+      const int64_t items = int64_t(b.row) * b.ny * b.nz * b.nouter;
+      if (items <= 0) continue;
+      if (!b.in || !b.out) throw std::runtime_error("stencil7: null grid");
+      fb.b[fb.n] = b;
+      fb.block_start[fb.n] = total;
+      total += uint32_t(std::min<int64_t>((items + 1023) / 1024, 8192)); // 4 per thread
+      ++fb.n;
+    }
+    if (fb.n == 0) continue;
+    fb.block_start[fb.n] = total;
+    hipLaunchKernelGGL(stencil7_flat_k, dim3(total), dim3(256), 0, s, fb);
+    TZ_HIP_LAUNCH_CHECK();
+  }
+}
 
 StencilTuning &stencil_tuning() {
   static StencilTuning t;
@@ -207,6 +280,10 @@ void stencil7(const StencilBox &b, bool lds, void *stream) {
                   b.so % 2 == 0 && reinterpret_cast<uintptr_t>(b.in) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(b.out) % 16 == 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (stencil_thin(b)) {
+    stencil7_thin_many(&b, 1, stream);
+    return;
+  }
   if (lds && v2) launch_ty<true, 2>(b, s);
   else if (lds) launch_ty<true, 1>(b, s);
   else if (v2) launch_ty<false, 2>(b, s);

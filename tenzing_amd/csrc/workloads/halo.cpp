@@ -33,6 +33,7 @@ Json HaloArgs::json() const {
   j["pz"] = pz;
   j["pitch_pad"] = pitch_pad;
   j["ghost_align"] = ghost_align;
+  j["stencil"] = stencil;
   return j;
 }
 
@@ -119,6 +120,29 @@ public:
 private:
   std::shared_ptr<const HaloExchange> h_;
   int i_;
+};
+
+/// stencil over an interior region (stencil mode)
+class HaloStencil : public GpuOp {
+public:
+  HaloStencil(std::shared_ptr<const HaloExchange> h, int region) : h_(std::move(h)), region_(region) {}
+  std::string name() const override {
+    static const char *n[] = {"st_interior", "st_boundary", "st_full"};
+    return n[region_];
+  }
+  std::string kind() const override { return "Stencil7"; }
+  double bytes() const override {
+    const auto &a = h_->args();
+    const double n3 = double(a.nx) * a.ny * a.nz, in3 = double(a.nx - 2) * (a.ny - 2) * (a.nz - 2);
+    const double cells = region_ == 0 ? in3 : (region_ == 1 ? n3 - in3 : n3);
+    return 16.0 * cells * a.nq;
+  }
+  double cost_us() const override { return 3.0 + bytes() / 4.0e6; }
+  void launch(void *s, Executor &) const override { h_->stencil(region_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int region_;
 };
 
 /// ipc transport: device-side wait for the neighbours' puts into my ghosts
@@ -430,6 +454,10 @@ void HaloExchange::setup(Ctrl *ctrl) {
     }
   }
   count_ = DeviceBuffer(sizeof(unsigned long long));
+  if (a_.stencil) {
+    out_ = DeviceBuffer(gridElems_ * sizeof(double));
+    TZ_HIP(hipMemset(out_.get(), 0, out_.bytes()));
+  }
   if (useRccl_) {
     TZ_CHECK(ctrl && ctrl->size() == a_.size, "RCCL transport needs a control plane of size "
                                                   << a_.size);
@@ -1062,7 +1090,111 @@ void HaloExchange::add_ipc_part(Graph &g, const std::vector<int> &remote, int vi
   }
 }
 
+kern::StencilBox HaloExchange::stencil_box(int x0, int x1, int y0, int y1, int z0, int z1) const {
+  // cells [x0,x1) x [y0,y1) x [z0,z1) of the interior (interior coordinates)
+  kern::StencilBox b;
+  b.in = grid();
+  b.out = out_.as<double>();
+  const int64_t g = a_.ghost;
+  if (a_.order == "xyzq") {
+    b.base = (z0 + g) * sz_ + (y0 + g) * sy_ + (x0 + g) + xoff_;
+    b.row = x1 - x0;
+    b.xs = 1;
+    b.so = sq_;
+    b.nouter = a_.nq;
+  } else {
+    b.base = int64_t(a_.nq) * (x0 + g + xoff_) + (y0 + g) * sy_ + (z0 + g) * sz_;
+    b.row = a_.nq * (x1 - x0);
+    b.xs = a_.nq;
+    b.so = 0;
+    b.nouter = 1;
+  }
+  b.sy = sy_;
+  b.sz = sz_;
+  b.ny = y1 - y0;
+  b.nz = z1 - z0;
+  return b;
+}
+
+void HaloExchange::stencil(int region, void *stream) const {
+  TZ_CHECK(ready() && out_.get(), "stencil mode not set up");
+  const int X = a_.nx, Y = a_.ny, Z = a_.nz;
+  std::vector<kern::StencilBox> boxes;
+  if (region == 2) {
+    boxes.push_back(stencil_box(0, X, 0, Y, 0, Z));
+  } else if (region == 0) {
+    // full rows with the first / last x cell masked: rows stay 16-B aligned
+    if (X > 2 && Y > 2 && Z > 2) {
+      kern::StencilBox b = stencil_box(0, X, 1, Y - 1, 1, Z - 1);
+      b.m0 = b.m1 = b.xs;
+      boxes.push_back(b);
+    }
+  } else {
+    // the shell: two z planes, two y slabs between them, two x slabs inside those
+    boxes.push_back(stencil_box(0, X, 0, Y, 0, 1));
+    if (Z > 1) boxes.push_back(stencil_box(0, X, 0, Y, Z - 1, Z));
+    if (Z > 2) {
+      boxes.push_back(stencil_box(0, X, 0, 1, 1, Z - 1));
+      if (Y > 1) boxes.push_back(stencil_box(0, X, Y - 1, Y, 1, Z - 1));
+      if (Y > 2) {
+        boxes.push_back(stencil_box(0, 1, 1, Y - 1, 1, Z - 1));
+        if (X > 1) boxes.push_back(stencil_box(X - 1, X, 1, Y - 1, 1, Z - 1));
+      }
+    }
+  }
+  // thin boxes (the shell's slabs) share one launch; the rest go one by one
+  std::vector<kern::StencilBox> thin;
+  for (const auto &b : boxes) {
+    if (kern::stencil_thin(b)) thin.push_back(b);
+    else kern::stencil7(b, true, stream);
+  }
+  if (!thin.empty()) kern::stencil7_thin_many(thin.data(), int(thin.size()), stream);
+}
+
+uint64_t HaloExchange::check_stencil(void *stream) {
+  TZ_CHECK(ready() && out_.get(), "stencil mode not set up");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  TZ_HIP(hipMemsetAsync(count_.get(), 0, sizeof(unsigned long long), s));
+  kern::stencil_check(out_.as<double>(), geom(), count_.as<unsigned long long>(), stream);
+  unsigned long long n = 0;
+  TZ_HIP(hipMemcpyAsync(&n, count_.get(), sizeof(n), hipMemcpyDeviceToHost, s));
+  TZ_HIP(hipStreamSynchronize(s));
+  return n;
+}
+
 void HaloExchange::add_to_graph(Graph &g) {
+  if (!a_.stencil) {
+    add_exchange(g);
+    return;
+  }
+  // the exchange as one compound op, shared by both alternatives
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  auto ex = std::make_shared<Graph>();
+  add_exchange(*ex);
+  auto xchg = std::make_shared<StaticCompoundOp>("he_xchg", ex);
+  // split: interior (needs no ghost) runs beside the exchange, the shell after it
+  auto split = std::make_shared<Graph>();
+  auto interior = std::make_shared<HaloStencil>(self, 0);
+  auto shell = std::make_shared<HaloStencil>(self, 1);
+  split->start_then(interior);
+  split->then_finish(interior);
+  split->start_then(xchg);
+  split->then(xchg, shell);
+  split->then_finish(shell);
+  // full: the whole interior after the exchange (one launch)
+  auto full = std::make_shared<Graph>();
+  auto all = std::make_shared<HaloStencil>(self, 2);
+  full->start_then(xchg);
+  full->then(xchg, all);
+  full->then_finish(all);
+  std::vector<OpPtr> alts = {std::make_shared<StaticCompoundOp>("st_split", split),
+                             std::make_shared<StaticCompoundOp>("st_after", full)};
+  auto c = std::make_shared<StaticChoiceOp>("st_mode", alts);
+  g.start_then(c);
+  g.then_finish(c);
+}
+
+void HaloExchange::add_exchange(Graph &g) {
   // self-neighbour directions are moved directly and remote directions go through RCCL or IPC
   // puts; the local moves form their own op(s), the remote directions get the fuse structure
   // (and the search overlaps the two). With both transports available ("auto" on several

@@ -121,6 +121,10 @@ struct HaloArgs {
   // widen their x ghost writes over the neighbouring row padding to whole sectors / lines (no
   // partially written sectors or lines on the x faces). 0: line-optimal padding, exact runs.
   int ghost_align = 16;
+  // also run a 7-point stencil over the interior after the exchange (into a second grid): the
+  // search may update the ghost-free interior while ghosts are in flight and the one-cell
+  // boundary shell afterwards, or the whole domain after the exchange (a ChoiceOp)
+  bool stencil = false;
   int device = -1;
   Json json() const;
 };
@@ -153,14 +157,23 @@ public:
   /// allocate device memory and (for RCCL) communicators; collective over ctrl when size > 1
   void setup(Ctrl *ctrl);
   bool ready() const { return grid_.get() != nullptr; }
-  /// add the exchange's ops and edges to g (Start -> packs ... unpacks -> Finish)
+  /// add the exchange's ops and edges to g (Start -> packs ... unpacks -> Finish); in stencil
+  /// mode the stencil around it
   void add_to_graph(Graph &g);
+  /// the exchange alone
+  void add_exchange(Graph &g);
 
   // device data
   double *grid() const { return grid_.as<double>(); }
   void init_grid(void *stream = nullptr);
   /// number of wrong elements after an exchange (0 = all ghosts correct, interior untouched)
   uint64_t check_grid(void *stream = nullptr);
+  /// stencil mode: number of output cells that differ from the stencil of the initialized grid
+  uint64_t check_stencil(void *stream = nullptr);
+  /// stencil mode: apply the stencil to an interior region: 0 = ghost-free interior
+  /// [1, n-1)^3, 1 = the one-cell boundary shell, 2 = the whole interior
+  void stencil(int region, void *stream) const;
+  double *stencil_out() const { return out_.as<double>(); }
 
   // op bodies
   void pack(int i, void *stream) const;
@@ -258,6 +271,8 @@ private:
   std::vector<DeviceBuffer> send_, recv_;
   std::vector<std::shared_ptr<RcclComm>> comms_;
   DeviceBuffer count_;
+  DeviceBuffer out_; // stencil output grid (stencil mode)
+  kern::StencilBox stencil_box(int x0, int x1, int y0, int y1, int z0, int z1) const;
 };
 
 // ------------------------------------------------------------------ distributed SpMV

@@ -30,6 +30,7 @@ class HaloConfig:
     pitch_pad: int = 0    # extra row-pitch elements (multiple of 16)
     rank_grid: tuple = ()  # (px, py, pz); () = reference rule (prime factors, smallest dim first)
     ghost_align: int = 16  # x ghost runs aligned to 8 (sector) / 16 (line) elements, 0 = off
+    stencil: bool = False  # add a 7-point stencil (interior beside / shell after the exchange)
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":
         a = _tz.HaloArgs()
@@ -43,6 +44,7 @@ class HaloConfig:
         a.comms = self.comms
         a.pitch_pad = self.pitch_pad
         a.ghost_align = self.ghost_align
+        a.stencil = self.stencil
         if self.rank_grid:
             a.px, a.py, a.pz = (int(v) for v in self.rank_grid)
         a.rank, a.size, a.device = rank, size, device

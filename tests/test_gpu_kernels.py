@@ -146,7 +146,7 @@ def test_vector_kernels(tz, gpu):
     assert torch.equal(io, 3.0 + 0.5 * torch.arange(1000, dtype=torch.float64, device="cuda"))
 
 
-@pytest.mark.parametrize("nx", [100, 99])  # even rows: 2 elements per thread; odd: 1
+@pytest.mark.parametrize("nx", [100, 99, 1])  # even rows: 2 per thread; odd: 1; 1: thin box
 @pytest.mark.parametrize("lds", [True, False])
 @pytest.mark.parametrize("order", ["qxyz", "xyzq"])
 def test_stencil7_matches_torch(tz, gpu, order, lds, nx):

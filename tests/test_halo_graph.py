@@ -159,3 +159,25 @@ def test_every_rank_builds_the_same_op_names(tz, size, transport, monkeypatch):
             js = tz.random_rollout(tz.State(graphs[0], tz.Platform(4)), seed).json(True)
             for g in graphs[1:]:
                 tz.OpIndex(g).sequence_from_json(js)
+
+
+def test_stencil_mode_graph(tz):
+    """stencil mode: a ChoiceOp between "interior beside the exchange, shell after it" and
+    "whole stencil after the exchange"; every rollout is race-free and keeps the stencil after
+    the ghosts it reads"""
+    from tenzing_amd.models import HaloConfig, build_halo
+
+    h, g = build_halo(HaloConfig(n=32, neighbors=26, order="qxyz", fuse="choice", stencil=True),
+                      setup=False)
+    seen = set()
+    for seed in range(40):
+        seq = tz.random_rollout(tz.State(g, tz.Platform(3)), seed)
+        names = [o.name for o in seq.ops()]
+        st = [n for n in names if n.startswith("st_")]
+        seen.add(tuple(sorted(st)))
+        moves = [k for k, n in enumerate(names) if n.startswith("he_direct_")]
+        if "st_full" in names:
+            assert max(moves) < names.index("st_full")
+        else:
+            assert max(moves) < names.index("st_boundary")
+    assert seen == {("st_full",), ("st_boundary", "st_interior")}
