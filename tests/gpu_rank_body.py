@@ -29,8 +29,9 @@ def main():
         modes = os.environ.get("TZ_TEST_MODES", "eager,graph").split(",")
         for fuse in fuses:
             say("build_halo", n, fuse)
+            stencil = bool(os.environ.get("TZ_TEST_STENCIL"))
             halo, g = build_halo(HaloConfig(n=n, neighbors=26, order="qxyz", transport="ipc",
-                                            fuse=fuse), ctrl, dev)
+                                            fuse=fuse, stencil=stencil), ctrl, dev)
             say("built")
             rt = tz.HipRuntime(device=dev, n_streams=3, watchdog_s=60.0)
             for mode in [tz.ExecMode.Eager if m == "eager" else tz.ExecMode.Graph for m in modes]:
@@ -51,13 +52,13 @@ def main():
                     rt.device_sync()
                     say("synced")
                     ctrl.barrier()
-                    bad1 = halo.check_grid()
+                    bad1 = halo.check_grid() + (halo.check_stencil() if stencil else 0)
                     say("checked", bad1)
                     ctrl.barrier()
                     rt.run(7)  # repeated exchanges keep the ghosts right
                     rt.device_sync()
                     ctrl.barrier()
-                    bad2 = halo.check_grid()
+                    bad2 = halo.check_grid() + (halo.check_stencil() if stencil else 0)
                     res.append(dict(fuse=fuse, mode=str(mode), seed=seed, bad1=int(bad1),
                                     bad2=int(bad2), err=halo.ipc_errors(),
                                     transport=halo.transport(), ipc_mode=halo.ipc_mode(),

@@ -97,3 +97,12 @@ def test_spmv_ipc_loopback(gpu, world, case):
         for run in r["runs"]:
             assert run["err1"] < 1e-4 and run["err2"] < 1e-4, run
             assert run["bad"] == 0 and run["ipc_err"] == 0 and run["ipc"], run
+
+
+def test_stencil_mode_loopback(gpu):
+    """exchange + stencil on 2 ranks of one GPU (IPC): ghosts and every stencil output cell are
+    right on both ranks, whichever stencil alternative a schedule takes"""
+    res = _launch("ipc_halo", 2, extra_env={"TZ_TEST_STENCIL": "1", "TZ_TEST_FUSES": "choice"})
+    for r in res:
+        for run in r["runs"]:
+            assert run["bad1"] == 0 and run["bad2"] == 0 and run["err"] == 0, run
