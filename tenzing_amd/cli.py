@@ -24,7 +24,7 @@ def _build_workload(a, ctrl, device, setup):
     from tenzing_amd.models import HaloConfig, SpmvConfig, build_fused, build_halo, build_spmv
 
     hc = HaloConfig(n=a.halo_n, nq=a.nq, ghost=a.ghost, neighbors=a.neighbors, order=a.order,
-                    fuse=a.fuse, transport=a.transport)
+                    fuse=a.fuse, transport=a.transport, stencil=a.stencil)
     sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport)
     if a.workload == "halo":
         h, g = build_halo(hc, ctrl, device, setup)
@@ -201,6 +201,8 @@ def main(argv=None) -> int:
     s.add_argument("--order", default="xyzq")
     s.add_argument("--fuse", default="choice")
     s.add_argument("--transport", default="auto")
+    s.add_argument("--stencil", action="store_true",
+                   help="halo: add the 7-point stencil (interior beside / shell after the exchange)")
     s.add_argument("--spmv-m", type=int, default=150_000)
     s.add_argument("--spmv-form", default="choice", choices=["choice", "split", "accum"])
     s.add_argument("--spmv-transport", default="auto", choices=["auto", "rccl", "ipc"])

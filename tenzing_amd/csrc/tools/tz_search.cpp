@@ -54,7 +54,8 @@ void usage() {
          "  [--fuse none|pack|all|groups|choice] [--graph-unroll K]\n"
          "  [--transport auto|rccl|ipc|copy|direct] [--rank-grid PXxPYxPZ] [--spmv-m N]\n"
          "  [--spmv-form choice|split|accum] [--spmv-transport auto|rccl|ipc]\n"
-         "  [--spmv-library adaptive|lrb|rowsplit|''] [--cu-partition] [--max-seqs N] [--rdzv-file PATH]\n"
+         "  [--spmv-library adaptive|lrb|rowsplit|''] [--cu-partition] [--stencil] [--max-seqs N]\n"
+         "  [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--watchdog S]\n";
 }
@@ -125,6 +126,7 @@ int main(int argc, char **argv) {
       h.fuse = a.get("fuse", "none");
       h.transport = a.get("transport", "auto");
       h.order = a.get("order", "xyzq");
+      h.stencil = a.flag("stencil");
       TZ_CHECK(h.order == "xyzq" || h.order == "qxyz", "--order must be xyzq or qxyz");
       h.rank = rank;
       h.size = size;
