@@ -28,6 +28,13 @@ def main():
         hc.pack_all(st)
         hc.shift_all(st)
         hc.unpack_all(st)
+    hs, _ = build_halo(HaloConfig(n=512, neighbors=26, order="qxyz", transport="direct",
+                                  stencil=True), tz.SelfCtrl(), device=0)
+    for _ in range(3):
+        hs.stencil(2, st)  # whole interior: 2.5-D LDS-tiled 7-point stencil
+        hs.stencil(1, st)  # the one-cell shell (thin-slab kernel)
+    del hs
+    torch.cuda.synchronize()
     m = 150_000
     rp, ci, val = tz._tz.random_band_matrix(m, m, 10 * m, 1)
     rp_t = torch.tensor(rp, dtype=torch.int32, device="cuda")
