@@ -20,10 +20,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--orders", default="qxyz,xyzq")
     a = ap.parse_args()
     n, nq, g = a.n, 3, 3
     st = torch.cuda.current_stream().cuda_stream
-    for order in ("qxyz", "xyzq"):
+    for order in a.orders.split(","):
         if order == "qxyz":
             P = nq * (n + 2 * g + 16)
             G = torch.randn(n + 2 * g, n + 2 * g, P, dtype=torch.float64, device="cuda")
@@ -38,9 +39,25 @@ def main():
         O = torch.empty_like(G)
         base = g * sz + g * sy + x0
         nbytes = 2 * 8 * n ** 3 * nq
-        configs = [(True, ty, zc) for ty in (4, 8, 16) for zc in (32, 64)] + [(False, 8, 32)]
-        for lds, ty, zc in configs:
-            tz._tz.kernels.set_stencil_tuning(ty, zc)
+        configs = [(True, ty, zc, pf, db) for ty in (8, 16) for zc in (32, 64) for pf in (1, 2)
+                   for db in (True, False)]
+        configs += [(False, 8, 32, 1, False)]
+        # roof: torch's contiguous copy of the whole padded grid (read + write every element)
+        for _ in range(3):
+            O.copy_(G)
+        ts = []
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            O.copy_(G)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        us = statistics.median(ts)
+        print(json.dumps({"order": order, "copy_roof": True, "us": round(us, 1),
+                          "TBps": round(2 * 8 * G.numel() / us / 1e6, 2)}), flush=True)
+        for lds, ty, zc, pf, db in configs:
+            tz._tz.kernels.set_stencil_tuning(ty, zc, pf, db)
 
             def fn():
                 tz._tz.kernels.stencil7(G.data_ptr(), O.data_ptr(), base, row, n, n, nouter, sy, sz,
@@ -56,7 +73,7 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1e3)
             us = statistics.median(ts)
-            print(json.dumps({"order": order, "lds": lds, "ty": ty, "zc": zc, "us": round(us, 1),
+            print(json.dumps({"order": order, "lds": lds, "ty": ty, "zc": zc, "pf": pf, "db": db, "us": round(us, 1),
                               "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
         del G, O
         torch.cuda.empty_cache()

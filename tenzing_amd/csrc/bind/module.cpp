@@ -750,10 +750,12 @@ PYBIND11_MODULE(_tz, m) {
   }, py::arg("in_"), py::arg("out"), py::arg("base"), py::arg("row"), py::arg("ny"), py::arg("nz"),
      py::arg("nouter"), py::arg("sy"), py::arg("sz"), py::arg("so"), py::arg("xs"),
      py::arg("c0") = 0.4, py::arg("c1") = 0.1, py::arg("lds") = true, py::arg("stream") = 0);
-  k.def("set_stencil_tuning", [](int ty, int zc) {
+  k.def("set_stencil_tuning", [](int ty, int zc, int pf, bool db) {
     kern::stencil_tuning().ty = ty;
     kern::stencil_tuning().zc = zc;
-  }, py::arg("ty") = 8, py::arg("zc") = 32);
+    kern::stencil_tuning().pf = pf;
+    kern::stencil_tuning().db = db;
+  }, py::arg("ty") = 16, py::arg("zc") = 64, py::arg("pf") = 1, py::arg("db") = true);
   k.def("gather_f32", [](int n, uintptr_t src, uintptr_t idx, uintptr_t dst, uintptr_t s) {
     kern::gather_f32(n, reinterpret_cast<const float *>(src), reinterpret_cast<const int32_t *>(idx),
                      reinterpret_cast<float *>(dst), P(s));

@@ -137,6 +137,8 @@ struct StencilBox {
 struct StencilTuning {
   int ty = 16; // 64 x 16 tiles, 64-plane chunks: 4.2 TB/s at 512^3 x 3 (scripts/stencil_bench.py)
   int zc = 64;
+  int pf = 1;  // planes in flight beyond z + 1 (1 or 2)
+  bool db = true; // double-buffered LDS tile (one barrier per plane instead of two)
 };
 StencilTuning &stencil_tuning();
 /// out = c0 * in + c1 * (sum of the 6 face neighbours) over the box; `lds`: 2.5-D LDS-tiled

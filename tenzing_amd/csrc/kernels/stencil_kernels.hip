@@ -54,13 +54,15 @@ template <> struct VT<2> {
   __device__ static double get(const T &v, int k) { return k ? v.y : v.x; }
 };
 
-template <bool LDS, int VX, int TY, int ZC>
+// PF: planes prefetched ahead of the z + 1 plane (1: z + 2; 2: z + 2 and z + 3), i.e. the
+// loads each lane keeps in flight; the tile is double-buffered, one barrier per plane
+template <bool LDS, int VX, int TY, int ZC, int PF, bool DB>
 __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
   using V = VT<VX>;
   using T = typename V::T;
   constexpr int W = TX * VX;              // elements per tile row
   constexpr int LW = W + 2 * XS_MAX;      // LDS row width
-  __shared__ double tile[TY + 2][LW];
+  __shared__ double tiles[LDS && DB ? 2 : 1][TY + 2][LW];
   const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
   const int r = blockIdx.x * W + tx * VX; // first element of this thread within the row
   const int y = blockIdx.y * TY + ty;     // row
@@ -113,16 +115,24 @@ __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
     return aok[a] ? in[pbase + int64_t(z) * b.sz + int64_t(agy[a]) * b.sy + agr[a]] : 0.0;
   };
 
-  // register queue: planes z - 1, z, z + 1 of my elements; z + 2 is prefetched one plane ahead
+  // register queue: planes z - 1, z, z + 1 of my elements, and z + 2 .. z + 1 + PF in flight
+  // (at most plane nz, the ghost plane, of the last chunk)
+  auto loadnt = [&](int zz) {
+    return live && zz <= b.nz
+               ? __builtin_nontemporal_load(reinterpret_cast<const T *>(in + e0 + int64_t(zz) * b.sz))
+               : V::zero();
+  };
   T prev = mine ? load(e0 + int64_t(z0 - 1) * b.sz) : V::zero();
   T cur = live ? load(e0 + int64_t(z0) * b.sz) : V::zero();
   T next = live ? load(e0 + int64_t(z0 + 1) * b.sz) : V::zero();
+  T ahead[PF];
+#pragma unroll
+  for (int p = 0; p + 1 < PF; ++p) ahead[p] = loadnt(z0 + 2 + p);
   double ap0 = apron(0, z0), ap1 = apron(1, z0);
   for (int z = z0; z < z1; ++z) {
     const int64_t e = e0 + int64_t(z) * b.sz;
-    // z + 2 is at most plane nz (the ghost plane) of the last chunk
-    T nn = V::zero();
-    if (live && z + 2 <= b.nz) nn = __builtin_nontemporal_load(reinterpret_cast<const T *>(in + e + 2 * b.sz));
+    ahead[PF - 1] = loadnt(z + 1 + PF);
+    auto &tile = tiles[LDS && DB ? (z - z0) & 1 : 0];
     double xm[VX], xp[VX], ym[VX], yp[VX];
     if (LDS) {
 #pragma unroll
@@ -168,10 +178,14 @@ __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
         }
       }
     }
-    if (LDS) __syncthreads(); // the tile is rewritten for the next plane
+    // double-buffered: no second barrier (the next plane writes the other tile, and every
+    // thread has left this plane's reads behind before anyone passes the next plane's barrier)
+    if (LDS && !DB) __syncthreads();
     prev = cur;
     cur = next;
-    next = nn;
+    next = ahead[0];
+#pragma unroll
+    for (int p = 0; p + 1 < PF; ++p) ahead[p] = ahead[p + 1];
   }
 }
 
@@ -246,28 +260,38 @@ StencilTuning &stencil_tuning() {
 }
 
 namespace {
-template <bool LDS, int VX, int TY, int ZC>
-void launch_stencil(const StencilBox &b, hipStream_t s) {
+template <bool LDS, int VX, int TY, int ZC, int PF, bool DB>
+void launch_stencil_db(const StencilBox &b, hipStream_t s) {
   const int W = TX * VX;
   const int zChunks = (b.nz + ZC - 1) / ZC;
   const dim3 g(unsigned((b.row + W - 1) / W), unsigned((b.ny + TY - 1) / TY),
                unsigned(zChunks * b.nouter));
-  hipLaunchKernelGGL((stencil7_k<LDS, VX, TY, ZC>), g, dim3(TX * TY), 0, s, b);
+  hipLaunchKernelGGL((stencil7_k<LDS, VX, TY, ZC, PF, DB>), g, dim3(TX * TY), 0, s, b);
+}
+
+template <bool LDS, int VX, int TY, int ZC, int PF>
+void launch_stencil(const StencilBox &b, hipStream_t s) {
+  if (stencil_tuning().db) launch_stencil_db<LDS, VX, TY, ZC, PF, true>(b, s);
+  else launch_stencil_db<LDS, VX, TY, ZC, PF, false>(b, s);
+}
+
+template <bool LDS, int VX, int TY>
+void launch_zc(const StencilBox &b, hipStream_t s) {
+  const StencilTuning &t = stencil_tuning();
+  if (t.zc == 64) {
+    if (t.pf >= 2) launch_stencil<LDS, VX, TY, 64, 2>(b, s);
+    else launch_stencil<LDS, VX, TY, 64, 1>(b, s);
+  } else {
+    if (t.pf >= 2) launch_stencil<LDS, VX, TY, 32, 2>(b, s);
+    else launch_stencil<LDS, VX, TY, 32, 1>(b, s);
+  }
 }
 
 template <bool LDS, int VX>
 void launch_ty(const StencilBox &b, hipStream_t s) {
   const StencilTuning &t = stencil_tuning();
-  if (t.ty == 4) {
-    if (t.zc == 64) launch_stencil<LDS, VX, 4, 64>(b, s);
-    else launch_stencil<LDS, VX, 4, 32>(b, s);
-  } else if (t.ty == 16) {
-    if (t.zc == 64) launch_stencil<LDS, VX, 16, 64>(b, s);
-    else launch_stencil<LDS, VX, 16, 32>(b, s);
-  } else {
-    if (t.zc == 64) launch_stencil<LDS, VX, 8, 64>(b, s);
-    else launch_stencil<LDS, VX, 8, 32>(b, s);
-  }
+  if (t.ty == 16) launch_zc<LDS, VX, 16>(b, s);
+  else launch_zc<LDS, VX, 8>(b, s);
 }
 } // namespace
 

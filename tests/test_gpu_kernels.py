@@ -146,12 +146,20 @@ def test_vector_kernels(tz, gpu):
     assert torch.equal(io, 3.0 + 0.5 * torch.arange(1000, dtype=torch.float64, device="cuda"))
 
 
+@pytest.fixture(params=[(16, 64, 1), (8, 32, 2), (16, 32, 2)], ids=lambda t: "ty%d-zc%d-pf%d" % t)
+def stencil_tuning(tz, request):
+    """kernel tilings (rows per tile, planes per chunk, planes in flight); restores the default"""
+    tz._tz.kernels.set_stencil_tuning(*request.param)
+    yield request.param
+    tz._tz.kernels.set_stencil_tuning()
+
+
 @pytest.mark.parametrize("nx", [100, 99, 1])  # even rows: 2 per thread; odd: 1; 1: thin box
 @pytest.mark.parametrize("lds", [True, False])
 @pytest.mark.parametrize("order", ["qxyz", "xyzq"])
-def test_stencil7_matches_torch(tz, gpu, order, lds, nx):
+def test_stencil7_matches_torch(tz, gpu, order, lds, nx, stencil_tuning):
     """7-point stencil over a box with a one-cell apron, both storage orders, box extents that
-    are not multiples of the tile (64 x 8 x 32), against a torch fp64 reference"""
+    are not multiples of the tile (64 x 8 x 32 planes), against a torch fp64 reference"""
     torch = pytest.importorskip("torch")
     nq, ny, nz, pad = 3, 37, 45, 5
     c0, c1 = 0.4, 0.1
