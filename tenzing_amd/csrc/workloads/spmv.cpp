@@ -594,23 +594,26 @@ int DistSpmv::ipc_errors() {
   return e;
 }
 
+OpPtr DistSpmv::local_op(bool accum, const std::string &p) {
+  // the local product, or (kernel_choice) a ChoiceOp over the lanes-per-row kernels, the
+  // CSR-stream kernel and rocSPARSE; both transports' graphs use the same op names for it
+  auto self = std::const_pointer_cast<const DistSpmv>(shared_from_this());
+  if (!a_.kernel_choice) return std::make_shared<SpmvLocal>(self, p + "yl", 0, accum);
+  std::vector<OpPtr> ch;
+  for (int w : {4, 8, 16})
+    ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w, accum));
+  ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_stream", -1, accum));
+  if (!a_.library.empty())
+    ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_rocsparse_" + a_.library, kLibrary, accum));
+  return std::make_shared<StaticChoiceOp>(p + "yl", ch);
+}
+
 std::shared_ptr<Graph> DistSpmv::form_graph_ipc(bool accum, const std::string &p) {
   // the reference's Scatter -> PostSend / PostRecv -> WaitRecv becomes put (gather straight
   // into the peers' memory) -> wait; the remote product hands the buffer back (credit)
   auto self = std::const_pointer_cast<const DistSpmv>(shared_from_this());
   auto g = std::make_shared<Graph>();
-  OpPtr yl;
-  if (a_.kernel_choice) {
-    std::vector<OpPtr> ch;
-    for (int w : {4, 8, 16})
-      ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w, accum));
-    ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_stream", -1, accum));
-    if (!a_.library.empty())
-      ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_rocsparse_" + a_.library, kLibrary, accum));
-    yl = std::make_shared<StaticChoiceOp>(p + "yl", ch);
-  } else {
-    yl = std::make_shared<SpmvLocal>(self, p + "yl", 0, accum);
-  }
+  OpPtr yl = local_op(accum, p);
   auto put = std::make_shared<SpmvPut>(self, p + "put");
   auto wait = std::make_shared<SpmvWait>(self, p + "wait");
   auto yr = std::make_shared<SpmvRemoteRelease>(self, p + "yr", accum);
@@ -640,18 +643,7 @@ std::shared_ptr<Graph> DistSpmv::form_graph(bool accum, const std::string &p) {
   // stream-ordered RCCL exchange.
   auto self = std::const_pointer_cast<const DistSpmv>(shared_from_this());
   auto g = std::make_shared<Graph>();
-  OpPtr yl;
-  if (a_.kernel_choice) {
-    std::vector<OpPtr> ch;
-    for (int w : {4, 8, 16})
-      ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w, accum));
-    ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_stream", -1, accum));
-    if (!a_.library.empty())
-      ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_rocsparse_" + a_.library, kLibrary, accum));
-    yl = std::make_shared<StaticChoiceOp>(p + "yl", ch);
-  } else {
-    yl = std::make_shared<SpmvLocal>(self, p + "yl", 0, accum);
-  }
+  OpPtr yl = local_op(accum, p);
   auto scatter = std::make_shared<SpmvScatter>(self, p + "Pack");
   auto xchg = std::make_shared<SpmvExchange>(self, p + "exchange");
   auto yr = std::make_shared<SpmvRemote>(self, p + "yr", accum);

@@ -388,6 +388,7 @@ private:
   double ipcTimeoutS_ = 10.0;
   std::shared_ptr<const Graph> inner_;
   std::shared_ptr<Graph> form_graph(bool accum, const std::string &p);
+  OpPtr local_op(bool accum, const std::string &p);
 };
 
 } // namespace tz
