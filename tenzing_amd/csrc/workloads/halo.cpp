@@ -1,18 +1,10 @@
-#include "workloads.hpp"
-
-#include "core/numeric.hpp"
-#include "core/util.hpp"
-#include "hip/hip_runtime.hpp"
-#include "hip/rccl_comm.hpp"
-
-#include <hip/hip_runtime_api.h>
-
-#include <algorithm>
-#include <map>
-#include <cstdlib>
-#include <cstring>
+// Halo workload: arguments, rank grid and grid layout, setup, and the pack / unpack / RCCL
+// shift / direct-move operations (reference src/halo_exchange/ops_halo_exchange.cu).
+// IPC / SDMA transport: halo_ipc.cpp; op graph: halo_graph.cpp; stencil: halo_stencil.cpp.
+#include "halo_internal.hpp"
 
 namespace tz {
+
 
 Json HaloArgs::json() const {
   Json j;
@@ -41,172 +33,6 @@ std::string HaloExchange::Dir::name() const {
   return "dx" + std::to_string(dx) + "_dy" + std::to_string(dy) + "_dz" + std::to_string(dz);
 }
 
-namespace {
-
-// byte-cost model for the simulator: ~5 TB/s effective HBM stream + launch latency
-double copy_cost_us(double bytes) { return 3.0 + bytes / 5.0e6; }
-
-class HaloPack : public GpuOp {
-public:
-  HaloPack(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
-  std::string name() const override { return "he_pack_" + h_->dir(i_).name(); }
-  std::string kind() const override { return "HaloPack"; }
-  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
-  double cost_us() const override { return copy_cost_us(bytes()); }
-  void launch(void *s, Executor &) const override { h_->pack(i_, s); }
-
-private:
-  std::shared_ptr<const HaloExchange> h_;
-  int i_;
-};
-
-class HaloUnpack : public GpuOp {
-public:
-  HaloUnpack(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
-  std::string name() const override { return "he_unpack_" + h_->dir(i_).name(); }
-  std::string kind() const override { return "HaloUnpack"; }
-  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
-  double cost_us() const override { return copy_cost_us(bytes()); }
-  void launch(void *s, Executor &) const override { h_->unpack(i_, s); }
-
-private:
-  std::shared_ptr<const HaloExchange> h_;
-  int i_;
-};
-
-class HaloShift : public GpuOp {
-public:
-  HaloShift(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
-  std::string name() const override { return "he_shift_" + h_->dir(i_).name(); }
-  std::string kind() const override { return h_->uses_rccl() ? "HaloShift" : "HaloCopy"; }
-  double bytes() const override { return 8.0 * double(h_->box_elems(i_)); }
-  // xGMI link ~100 GB/s effective per direction + RCCL launch; self copy ~2.5 TB/s
-  double cost_us() const override {
-    return h_->uses_rccl() ? 8.0 + bytes() / 1.0e5 : 3.0 + bytes() / 2.5e6;
-  }
-  void launch(void *s, Executor &ex) const override { h_->shift(i_, s, ex.stream_index(s)); }
-
-private:
-  std::shared_ptr<const HaloExchange> h_;
-  int i_;
-};
-
-/// direct transport of one direction: interior slab -> neighbour's ghost (no buffers)
-class HaloDirect : public GpuOp {
-public:
-  HaloDirect(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
-  std::string name() const override { return "he_direct_" + h_->dir(i_).name(); }
-  std::string kind() const override { return "HaloDirect"; }
-  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
-  double cost_us() const override { return copy_cost_us(bytes()); }
-  void launch(void *s, Executor &) const override { h_->direct(i_, s); }
-
-private:
-  std::shared_ptr<const HaloExchange> h_;
-  int i_;
-};
-
-/// ipc transport: pack-free put of one direction into the neighbour's grid + arrival signal
-class HaloPut : public GpuOp {
-public:
-  HaloPut(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
-  std::string name() const override { return "he_put_" + h_->dir(i_).name(); }
-  std::string kind() const override { return "HaloPut"; }
-  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
-  // peer stores over one xGMI link (~60 GB/s effective)
-  double cost_us() const override { return 4.0 + bytes() / 2.0 / 6.0e4; }
-  void launch(void *s, Executor &) const override { h_->put_group({i_}, s); }
-
-private:
-  std::shared_ptr<const HaloExchange> h_;
-  int i_;
-};
-
-/// stencil over an interior region (stencil mode)
-class HaloStencil : public GpuOp {
-public:
-  HaloStencil(std::shared_ptr<const HaloExchange> h, int region) : h_(std::move(h)), region_(region) {}
-  std::string name() const override {
-    static const char *n[] = {"st_interior", "st_boundary", "st_full"};
-    return n[region_];
-  }
-  std::string kind() const override { return "Stencil7"; }
-  double bytes() const override {
-    const auto &a = h_->args();
-    const double n3 = double(a.nx) * a.ny * a.nz, in3 = double(a.nx - 2) * (a.ny - 2) * (a.nz - 2);
-    const double cells = region_ == 0 ? in3 : (region_ == 1 ? n3 - in3 : n3);
-    return 16.0 * cells * a.nq;
-  }
-  double cost_us() const override { return 3.0 + bytes() / 4.0e6; }
-  void launch(void *s, Executor &) const override { h_->stencil(region_, s); }
-
-private:
-  std::shared_ptr<const HaloExchange> h_;
-  int region_;
-};
-
-/// ipc transport: device-side wait for the neighbours' puts into my ghosts
-class HaloWait : public GpuOp {
-public:
-  HaloWait(std::shared_ptr<const HaloExchange> h, std::vector<int> dirs, std::string tag)
-      : h_(std::move(h)), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
-  std::string name() const override { return "he_wait_" + tag_; }
-  std::string kind() const override { return "HaloWait"; }
-  double cost_us() const override { return 3.0; }
-  void launch(void *s, Executor &) const override { h_->wait_group(dirs_, s); }
-
-private:
-  std::shared_ptr<const HaloExchange> h_;
-  std::vector<int> dirs_;
-  std::string tag_;
-};
-
-/// one op for a whole group of directions (single kernel launch / single RCCL group)
-class HaloStageGroup : public GpuOp {
-public:
-  // UnpackRelease: unpack IPC receive buffers, then hand them back to the senders (credits)
-  // CopyPut: pack locally, copy-engine (SDMA) copy into the peer's receive buffer, signal
-  enum Stage { Pack, Shift, Unpack, Direct, Put, UnpackRelease, CopyPut };
-  HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag)
-      : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
-  std::string name() const override {
-    static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_", "he_put_",
-                                "he_unpack_", "he_copyput_"};
-    return pre[st_] + tag_;
-  }
-  std::string kind() const override {
-    static const char *k[] = {"HaloPackGroup", "HaloShiftGroup", "HaloUnpackGroup",
-                              "HaloDirectGroup", "HaloPutGroup", "HaloUnpackGroup",
-                              "HaloCopyPutGroup"};
-    return k[st_];
-  }
-  double bytes() const override {
-    double b = 0;
-    for (int i : dirs_) b += 8.0 * double(h_->box_elems(i));
-    return (st_ == Shift ? 1.0 : 2.0) * b;
-  }
-  double cost_us() const override {
-    if (st_ == Shift) return h_->uses_rccl() ? 10.0 + bytes() / 3.0e5 : 3.0 + bytes() / 2.5e6;
-    return copy_cost_us(bytes());
-  }
-  void launch(void *s, Executor &ex) const override {
-    if (st_ == Pack) h_->pack_group(dirs_, s);
-    else if (st_ == Shift) h_->shift_group(dirs_, s, ex.stream_index(s));
-    else if (st_ == Unpack) h_->unpack_group(dirs_, s);
-    else if (st_ == Direct) h_->direct_group(dirs_, s);
-    else if (st_ == Put) h_->put_group(dirs_, s);
-    else if (st_ == CopyPut) h_->copy_put_group(dirs_, s);
-    else h_->ipc_unpack_group(dirs_, s);
-  }
-
-private:
-  std::shared_ptr<const HaloExchange> h_;
-  Stage st_;
-  std::vector<int> dirs_;
-  std::string tag_;
-};
-
-} // namespace
 
 HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.nx > 0 && a_.ny > 0 && a_.nz > 0 && a_.nq > 0 && a_.ghost > 0, "bad halo extents");
@@ -351,8 +177,8 @@ static void axis_range(int d, int n, int g, bool ghost, int &lo, int &ext) {
   }
 }
 
-static kern::BoxDesc make_box(const HaloArgs &a, const HaloExchange::Dir &d, bool ghost,
-                              int64_t xoff, int64_t sy, int64_t sz, int64_t sq) {
+kern::BoxDesc halo_detail::make_box(const HaloArgs &a, const HaloExchange::Dir &d, bool ghost,
+                                    int64_t xoff, int64_t sy, int64_t sz, int64_t sq) {
   int x0, ex, y0, ey, z0, ez;
   axis_range(d.dx, a.nx, a.ghost, ghost, x0, ex);
   axis_range(d.dy, a.ny, a.ghost, ghost, y0, ey);
@@ -502,246 +328,6 @@ void HaloExchange::setup(Ctrl *ctrl) {
   }
   TZ_HIP(hipDeviceSynchronize());
   if (useIpc_ && ipcReady_) ctrl->barrier();
-}
-
-void HaloExchange::ipc_preflight(Ctrl *ctrl) {
-  // One complete exchange through IPC before the search may use it: every ghost must arrive
-  // (no wait timeout) and be right on every rank. A mapping that "works" but does not deliver
-  // (or delivers wrong data) turns the transport off collectively instead of costing a wait
-  // timeout per iteration of every IPC candidate later.
-  std::vector<int> local, remote;
-  for (int i = 0; i < ndirs(); ++i) {
-    if (direct_[i]) local.push_back(i);
-    else if (ipc_[i]) remote.push_back(i);
-  }
-  double bad = 0;
-  std::string why;
-  const double keep = ipcTimeoutS_;
-  ipcTimeoutS_ = std::min(ipcTimeoutS_, 3.0);
-  try {
-    if (!local.empty()) direct_group(local, nullptr);
-    put_group(remote, nullptr);
-    wait_group(remote, nullptr);
-    if (!ipcGrid_) ipc_unpack_group(remote, nullptr);
-    TZ_HIP(hipDeviceSynchronize());
-  } catch (const std::exception &ex) {
-    bad = 1;
-    why = std::string("preflight exchange: ") + ex.what();
-  }
-  // peers may still be putting into my ghosts until they have synchronized too (outside the
-  // try: every rank reaches this collective whatever failed locally)
-  ctrl->barrier();
-  if (bad == 0) {
-    try {
-      const int e = ipc_errors();
-      const uint64_t cells = check_grid();
-      if (e || cells) {
-        bad = 1;
-        why = "preflight exchange: " + std::to_string(e) + " wait timeout(s), " +
-              std::to_string(cells) + " wrong cells";
-      }
-    } catch (const std::exception &ex) {
-      bad = 1;
-      why = std::string("preflight check: ") + ex.what();
-    }
-  }
-  ipcTimeoutS_ = keep;
-  ctrl->allreduce_max(&bad, 1);
-  if (bad != 0) {
-    ipcReady_ = false;
-    TZ_LOG(Warn, "ipc transport disabled: " << (why.empty() ? "failed on another rank" : why));
-    TZ_CHECK(a_.transport != "ipc", "ipc transport requested but " << why);
-  }
-  init_grid();
-}
-
-std::string HaloExchange::setup_ipc(Ctrl *ctrl) {
-  // Collective: every rank makes the same control-plane calls (one allgather) whatever fails
-  // locally, and reports failure as a string, so a rank that cannot export or map never leaves
-  // the others blocked in a mismatched collective.
-  TZ_CHECK(ctrl && ctrl->size() == a_.size, "ipc transport needs a control plane of size " << a_.size);
-  if (const char *v = std::getenv("TZ_IPC_TIMEOUT")) ipcTimeoutS_ = std::atof(v);
-  const size_t nd = size_t(ndirs());
-  const size_t H = sizeof(hipIpcMemHandle_t);
-  std::string mine, err;
-  try {
-    // arrival counters live in uncached memory: a remote GPU's system-scope atomics land in
-    // HBM and the local spin loads (system scope) see them without stale cache lines
-    // [arrivals of direction i | credits of direction i]: a receiver counts the puts it got in
-    // slot i and, once it has consumed them, returns a credit to the sender's slot nd + i
-    TZ_HIP(hipExtMallocWithFlags(&flags_, std::max<size_t>(2 * nd * 8, 64), hipDeviceMallocUncached));
-    TZ_HIP(hipMemset(flags_, 0, 2 * nd * 8));
-    expected_ = DeviceBuffer(nd * 8);
-    TZ_HIP(hipMemset(expected_.get(), 0, nd * 8));
-    sent_ = DeviceBuffer(nd * 8);
-    TZ_HIP(hipMemset(sent_.get(), 0, nd * 8));
-    done_ = DeviceBuffer(nd * kern::kMaxBoxes * sizeof(unsigned int));
-    TZ_HIP(hipMemset(done_.get(), 0, done_.bytes()));
-    err_ = DeviceBuffer(sizeof(int));
-    TZ_HIP(hipMemset(err_.get(), 0, sizeof(int)));
-    TZ_HIP(hipDeviceSynchronize());
-    // exported: [flags][grid] ("grid" mode) or [flags][recv buffer of every direction]
-    auto handle_of = [&](void *p) {
-      hipIpcMemHandle_t h;
-      std::memset(&h, 0, sizeof(h));
-      if (p) TZ_HIP(hipIpcGetMemHandle(&h, p));
-      return std::string(reinterpret_cast<const char *>(&h), H);
-    };
-    mine = handle_of(flags_);
-    if (ipcGrid_) {
-      mine += handle_of(grid());
-    } else {
-      for (int i = 0; i < ndirs(); ++i) mine += handle_of(ipc_[i] ? recv_[i].get() : nullptr);
-    }
-    TZ_LOG(Info, "ipc: exported " << (ipcGrid_ ? "grid" : "receive buffers") << " and flags");
-  } catch (const std::exception &e) {
-    err = std::string("export: ") + e.what();
-    mine.clear();
-  }
-  const std::vector<std::string> all = ctrl->allgather(mine);
-  if (!err.empty()) return err;
-  try {
-    TZ_CHECK(int(all.size()) == a_.size, "allgather returned " << all.size() << " entries");
-    auto open = [&](const std::string &blob, size_t k) {
-      TZ_CHECK(blob.size() >= (k + 1) * H, "a peer exported no IPC handles");
-      hipIpcMemHandle_t h;
-      std::memcpy(&h, blob.data() + k * H, H);
-      void *p = nullptr;
-      TZ_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-      opened_.push_back(p);
-      return p;
-    };
-    peerGrid_.assign(size_t(a_.size), nullptr);
-    peerFlags_.assign(size_t(a_.size), nullptr);
-    peerRecv_.assign(nd, nullptr);
-    for (int i = 0; i < ndirs(); ++i) {
-      if (!ipc_[i]) continue;
-      const int q = nbr_[i];
-      const std::string &blob = all[size_t(q)];
-      if (!peerFlags_[size_t(q)]) {
-        TZ_LOG(Info, "ipc: mapping rank " << q);
-        peerFlags_[size_t(q)] = open(blob, 0);
-        if (ipcGrid_) peerGrid_[size_t(q)] = open(blob, 1);
-      }
-      // my slab facing d_i fills q's ghost side -d_i, staged in q's recv buffer of that side
-      if (!ipcGrid_) peerRecv_[size_t(i)] = open(blob, 1 + size_t(opp_[i]));
-    }
-  } catch (const std::exception &e) {
-    return std::string("map: ") + e.what();
-  }
-  return "";
-}
-
-void HaloExchange::put_group(const std::vector<int> &dirs, void *stream) const {
-  TZ_CHECK(ready() && ipcReady_, "ipc transport not set up");
-  TZ_CHECK(!dirs.empty() && dirs.size() <= size_t(kern::kMaxBoxes), "bad put group");
-  std::vector<kern::MoveDesc> ms;
-  std::vector<kern::BoxDesc> bs;
-  kern::MoveSignal sig;
-  // block counters: one slot range per group, keyed by its first direction (groups of one
-  // schedule are disjoint, so concurrently running puts never share counters)
-  sig.done = done_.as<unsigned int>() + size_t(dirs.front()) * kern::kMaxBoxes;
-  // flow control: put n+1 of direction i may only overwrite the peer's ghosts / receive buffer
-  // after the peer has consumed put n (its credit, returned to my slot nd + i)
-  kern::ipc_wait(static_cast<const unsigned long long *>(flags_) + ndirs(), sent_.as<unsigned long long>(),
-                 dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/1);
-  for (size_t k = 0; k < dirs.size(); ++k) {
-    const int i = dirs[k];
-    TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i], "direction " << i << " is not an ipc put");
-    const int q = nbr_[i];
-    // the receiver counts arrivals of direction i in its slot i
-    sig.flag[k] = static_cast<unsigned long long *>(peerFlags_[size_t(q)]) + i;
-    if (!ipcGrid_) {
-      kern::BoxDesc b = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
-      b.buf = static_cast<double *>(peerRecv_[size_t(i)]);
-      bs.push_back(b);
-      continue;
-    }
-    const kern::BoxDesc s = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
-    const kern::BoxDesc d = make_box(a_, dirs_[opp_[i]], true, xoff_, sy_, sz_, sq_);
-    kern::MoveDesc m;
-    m.src = grid();
-    m.dst = static_cast<double *>(peerGrid_[size_t(q)]);
-    m.src_off = s.grid_off;
-    m.dst_off = d.grid_off;
-    m.s1 = s.s1;
-    m.s2 = s.s2;
-    m.s3 = s.s3;
-    m.len = s.len;
-    m.n1 = s.n1;
-    m.n2 = s.n2;
-    m.n3 = s.n3;
-    ms.push_back(m);
-  }
-  if (ipcGrid_) kern::box_move_many_signal(ms.data(), int(ms.size()), sig, stream);
-  else kern::box_pack_many_signal(grid(), bs.data(), int(bs.size()), sig, stream);
-}
-
-void HaloExchange::copy_put_group(const std::vector<int> &dirs, void *stream) const {
-  // The copy-engine put: pack into my local send buffers (one launch), then one device-to-device
-  // copy per direction into the receiver's IPC-mapped buffer. Across GPUs HIP runs these on the
-  // SDMA engines, so the xGMI transfer itself takes no CUs (they stay free for concurrent local
-  // work); then one small kernel publishes the arrivals. Same credit protocol as put_group.
-  TZ_CHECK(ready() && ipcReady_ && useCopy_ && !ipcGrid_, "ipc copy-engine puts not set up");
-  TZ_CHECK(!dirs.empty() && dirs.size() <= size_t(kern::kMaxBoxes), "bad copy-put group");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  std::vector<kern::BoxDesc> bs;
-  std::vector<unsigned long long *> arrive;
-  for (int i : dirs) {
-    TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i] && send_[i].get() && peerRecv_[size_t(i)],
-             "direction " << i << " is not a copy-engine put");
-    kern::BoxDesc b = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
-    b.buf = send_[i].as<double>();
-    bs.push_back(b);
-    arrive.push_back(static_cast<unsigned long long *>(peerFlags_[size_t(nbr_[i])]) + i);
-  }
-  kern::ipc_wait(static_cast<const unsigned long long *>(flags_) + ndirs(), sent_.as<unsigned long long>(),
-                 dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/1);
-  kern::box_copy_many(grid(), bs.data(), int(bs.size()), false, stream);
-  for (int i : dirs)
-    TZ_HIP(hipMemcpyAsync(peerRecv_[size_t(i)], send_[i].get(), box_elems(i) * sizeof(double),
-                          hipMemcpyDeviceToDevice, s));
-  kern::ipc_signal(arrive.data(), int(arrive.size()), stream);
-}
-
-void HaloExchange::wait_group(const std::vector<int> &dirs, void *stream) const {
-  TZ_CHECK(ready() && ipcReady_, "ipc transport not set up");
-  for (int i : dirs) TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i], "direction " << i << " is not an ipc put");
-  // grid mode: the ghosts are consumed once they arrived (nothing reads them inside the
-  // exchange), so the credit goes back right after the wait; buffers mode returns it after
-  // the unpack (ipc_unpack_group)
-  const std::vector<unsigned long long *> credits = credit_ptrs(dirs);
-  kern::ipc_wait(static_cast<const unsigned long long *>(flags_), expected_.as<unsigned long long>(),
-                 dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/0,
-                 ipcGrid_ ? credits.data() : nullptr);
-}
-
-std::vector<unsigned long long *> HaloExchange::credit_ptrs(const std::vector<int> &dirs) const {
-  // the put that filled my slot i came from nbr(-i); its credit slot for direction i is nd + i
-  std::vector<unsigned long long *> v;
-  for (int i : dirs) {
-    const int from = nbr_[opp_[i]];
-    TZ_CHECK(peerFlags_.size() > size_t(from) && peerFlags_[size_t(from)],
-             "rank " << from << " is not IPC-mapped");
-    v.push_back(static_cast<unsigned long long *>(peerFlags_[size_t(from)]) + ndirs() + i);
-  }
-  return v;
-}
-
-void HaloExchange::ipc_unpack_group(const std::vector<int> &dirs, void *stream) const {
-  TZ_CHECK(ready() && ipcReady_ && !ipcGrid_, "ipc buffers mode not set up");
-  unpack_group(dirs, stream);
-  const std::vector<unsigned long long *> credits = credit_ptrs(dirs);
-  kern::ipc_signal(credits.data(), int(credits.size()), stream);
-}
-
-int HaloExchange::ipc_errors() {
-  if (!useIpc_ || !err_.get()) return 0;
-  int e = 0;
-  TZ_HIP(hipDeviceSynchronize());
-  err_.download(&e, sizeof(e));
-  TZ_HIP(hipMemset(err_.get(), 0, sizeof(int)));
-  return e;
 }
 
 void HaloExchange::init_grid(void *stream) {
@@ -925,321 +511,5 @@ std::vector<int> HaloExchange::pipelined_dirs() const {
 void HaloExchange::pack_all(void *stream) const { pack_group(pipelined_dirs(), stream); }
 void HaloExchange::unpack_all(void *stream) const { unpack_group(pipelined_dirs(), stream); }
 void HaloExchange::shift_all(void *stream) const { shift_group(pipelined_dirs(), stream); }
-
-void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, int via) {
-  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
-  for (int i : dirs) {
-    if (direct_[i] || via != kViaPipe) {
-      OpPtr d;
-      if (direct_[i]) d = std::make_shared<HaloDirect>(self, i);
-      else if (via == kViaPut) d = std::make_shared<HaloPut>(self, i);
-      else d = std::make_shared<HaloStageGroup>(self, HaloStageGroup::CopyPut, std::vector<int>{i},
-                                                dirs_[i].name());
-      g.start_then(d);
-      g.then_finish(d);
-      continue;
-    }
-    auto p = std::make_shared<HaloPack>(self, i);
-    auto s = std::make_shared<HaloShift>(self, i);
-    auto u = std::make_shared<HaloUnpack>(self, opp_[i]);
-    g.start_then(p);
-    g.then(p, s);
-    g.then(s, u);
-    g.then_finish(u);
-  }
-}
-
-void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag,
-                             int via) {
-  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
-  std::vector<int> local, remote;
-  for (int i : dirs) (direct_[i] ? local : remote).push_back(i);
-  if (!local.empty()) {
-    auto d = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Direct, local,
-                                              remote.empty() ? tag : tag + "_self");
-    g.start_then(d);
-    g.then_finish(d);
-  }
-  if (remote.empty()) return;
-  if (via != kViaPipe) {
-    auto d = std::make_shared<HaloStageGroup>(
-        self, via == kViaPut ? HaloStageGroup::Put : HaloStageGroup::CopyPut, remote, tag);
-    g.start_then(d);
-    g.then_finish(d);
-    return;
-  }
-  auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, remote, tag);
-  auto s = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Shift, remote, tag);
-  auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, remote, tag);
-  g.start_then(p);
-  g.then(p, s);
-  g.then(s, u);
-  g.then_finish(u);
-}
-
-void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via,
-                                 const std::string &pre) {
-  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
-  const std::string &f = a_.fuse;
-  const bool singleStage = direct_[dirs.front()] || via != kViaPipe;
-  auto subset = [&](const std::vector<int> &v) {
-    std::vector<int> r;
-    for (int i : v)
-      if (std::find(dirs.begin(), dirs.end(), i) != dirs.end()) r.push_back(i);
-    return r;
-  };
-  if (f == "none") {
-    add_chains(g, dirs, via);
-  } else if (f == "all" || (f == "pack" && singleStage)) {
-    // (direct moves and puts have no pack stage: "pack" degenerates to one fused op)
-    add_fused(g, dirs, "all", via);
-  } else if (f == "pack") {
-    // fused pack / unpack kernels, per-direction transfers
-    auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, "all");
-    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, dirs, "all");
-    g.start_then(p);
-    g.then_finish(u);
-    for (int i : dirs) {
-      auto s = std::make_shared<HaloShift>(self, i);
-      g.then(p, s);
-      g.then(s, u);
-    }
-  } else if (f == "groups" || f == "choice") {
-    // faces and (for 26 neighbours) edges+corners form independent groups; each group is
-    // either one chain per direction or one fused chain. With "choice" the search decides
-    // (ChoiceOp of two CompoundOps; the group touches no other op, so choosing at the group
-    // boundary loses no dependency precision).
-    std::vector<std::pair<std::string, std::vector<int>>> groups;
-    for (auto &gr : std::vector<std::pair<std::string, std::vector<int>>>{
-             {"faces", subset(group_dirs(1))}, {"small", subset(group_dirs(0))}})
-      if (!gr.second.empty()) groups.push_back(gr);
-    if (f == "groups") {
-      for (auto &gr : groups) add_fused(g, gr.second, gr.first, via);
-      return;
-    }
-    // per group: split chains vs one fused chain
-    auto grouped = std::make_shared<Graph>();
-    for (auto &gr : groups) {
-      auto split = std::make_shared<Graph>();
-      add_chains(*split, gr.second, via);
-      auto fused = std::make_shared<Graph>();
-      add_fused(*fused, gr.second, gr.first, via);
-      std::vector<OpPtr> alts = {
-          std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_split", split),
-          std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_fused", fused)};
-      auto choice = std::make_shared<StaticChoiceOp>(pre + "he_" + gr.first, alts);
-      grouped->start_then(choice);
-      grouped->then_finish(choice);
-    }
-    if (groups.size() == 1) {
-      auto c = std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped);
-      g.start_then(c);
-      g.then_finish(c);
-      return;
-    }
-    // two groups: additionally one chain for every direction (a single launch per stage
-    // avoids the two groups' kernels competing for CUs)
-    auto all = std::make_shared<Graph>();
-    add_fused(*all, dirs, "all", via);
-    std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped),
-                              std::make_shared<StaticCompoundOp>(pre + "he_allfused", all)};
-    // remote directions to several peers: one chain per peer as well. Each peer is one xGMI
-    // link, so per-peer transfers on different streams use the links in parallel (copy-engine
-    // copies and RCCL groups issued on one stream would take them one at a time)
-    // Every rank must build the same graph (schedules are broadcast by op name): the split of
-    // directions by peer is the same on every rank of a periodic Cartesian grid, so groups are
-    // kept in order of their first direction and named after it, never after a rank id.
-    std::map<int, std::vector<int>> byPeer;
-    for (int i : dirs)
-      if (!direct_[i]) byPeer[nbr_[i]].push_back(i);
-    if (byPeer.size() > 1 && byPeer.size() < dirs.size()) {
-      std::vector<std::vector<int>> groupsByPeer;
-      for (const auto &kv : byPeer) groupsByPeer.push_back(kv.second);
-      std::sort(groupsByPeer.begin(), groupsByPeer.end());
-      auto peers = std::make_shared<Graph>();
-      for (const auto &grp : groupsByPeer) add_fused(*peers, grp, "p" + dirs_[grp.front()].name(), via);
-      top.push_back(std::make_shared<StaticCompoundOp>(pre + "he_bypeer", peers));
-    }
-    auto choice = std::make_shared<StaticChoiceOp>(pre + "he_exchange", top);
-    g.start_then(choice);
-    g.then_finish(choice);
-  } else {
-    TZ_THROW("fuse must be none, pack, all, groups or choice (got " << f << ")");
-  }
-}
-
-void HaloExchange::add_ipc_part(Graph &g, const std::vector<int> &remote, int via) {
-  // puts wait only for the credit of the previous iteration, so each rank's puts all complete;
-  // the arrival wait runs after them (one spinning kernel per rank, never ahead of its own
-  // puts). The copy-engine variant's op names carry "cp_" (unique in the expanded graph).
-  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
-  const std::string v = via == kViaCopy ? "cp_" : "";
-  auto puts = std::make_shared<Graph>();
-  add_structure(*puts, remote, via, via == kViaCopy ? "cp_" : "ipc_");
-  auto c = std::make_shared<StaticCompoundOp>("he_" + v + "puts", puts);
-  auto w = std::make_shared<HaloWait>(self, remote, v + "remote");
-  g.start_then(c);
-  g.then(c, w);
-  if (ipcGrid_) {
-    g.then_finish(w);
-  } else {
-    // "buffers" mode: my receive buffers are complete after the wait; unpack them
-    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::UnpackRelease, remote, v + "remote");
-    g.then(w, u);
-    g.then_finish(u);
-  }
-}
-
-kern::StencilBox HaloExchange::stencil_box(int x0, int x1, int y0, int y1, int z0, int z1) const {
-  // cells [x0,x1) x [y0,y1) x [z0,z1) of the interior (interior coordinates)
-  kern::StencilBox b;
-  b.in = grid();
-  b.out = out_.as<double>();
-  const int64_t g = a_.ghost;
-  if (a_.order == "xyzq") {
-    b.base = (z0 + g) * sz_ + (y0 + g) * sy_ + (x0 + g) + xoff_;
-    b.row = x1 - x0;
-    b.xs = 1;
-    b.so = sq_;
-    b.nouter = a_.nq;
-  } else {
-    b.base = int64_t(a_.nq) * (x0 + g + xoff_) + (y0 + g) * sy_ + (z0 + g) * sz_;
-    b.row = a_.nq * (x1 - x0);
-    b.xs = a_.nq;
-    b.so = 0;
-    b.nouter = 1;
-  }
-  b.sy = sy_;
-  b.sz = sz_;
-  b.ny = y1 - y0;
-  b.nz = z1 - z0;
-  return b;
-}
-
-void HaloExchange::stencil(int region, void *stream) const {
-  TZ_CHECK(ready() && out_.get(), "stencil mode not set up");
-  const int X = a_.nx, Y = a_.ny, Z = a_.nz;
-  std::vector<kern::StencilBox> boxes;
-  if (region == 2) {
-    boxes.push_back(stencil_box(0, X, 0, Y, 0, Z));
-  } else if (region == 0) {
-    // full rows with the first / last x cell masked: rows stay 16-B aligned
-    if (X > 2 && Y > 2 && Z > 2) {
-      kern::StencilBox b = stencil_box(0, X, 1, Y - 1, 1, Z - 1);
-      b.m0 = b.m1 = b.xs;
-      boxes.push_back(b);
-    }
-  } else {
-    // the shell: two z planes, two y slabs between them, two x slabs inside those
-    boxes.push_back(stencil_box(0, X, 0, Y, 0, 1));
-    if (Z > 1) boxes.push_back(stencil_box(0, X, 0, Y, Z - 1, Z));
-    if (Z > 2) {
-      boxes.push_back(stencil_box(0, X, 0, 1, 1, Z - 1));
-      if (Y > 1) boxes.push_back(stencil_box(0, X, Y - 1, Y, 1, Z - 1));
-      if (Y > 2) {
-        boxes.push_back(stencil_box(0, 1, 1, Y - 1, 1, Z - 1));
-        if (X > 1) boxes.push_back(stencil_box(X - 1, X, 1, Y - 1, 1, Z - 1));
-      }
-    }
-  }
-  // thin boxes (the shell's slabs) share one launch; the rest go one by one
-  std::vector<kern::StencilBox> thin;
-  for (const auto &b : boxes) {
-    if (kern::stencil_thin(b)) thin.push_back(b);
-    else kern::stencil7(b, true, stream);
-  }
-  if (!thin.empty()) kern::stencil7_thin_many(thin.data(), int(thin.size()), stream);
-}
-
-uint64_t HaloExchange::check_stencil(void *stream) {
-  TZ_CHECK(ready() && out_.get(), "stencil mode not set up");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  TZ_HIP(hipMemsetAsync(count_.get(), 0, sizeof(unsigned long long), s));
-  kern::stencil_check(out_.as<double>(), geom(), count_.as<unsigned long long>(), stream);
-  unsigned long long n = 0;
-  TZ_HIP(hipMemcpyAsync(&n, count_.get(), sizeof(n), hipMemcpyDeviceToHost, s));
-  TZ_HIP(hipStreamSynchronize(s));
-  return n;
-}
-
-void HaloExchange::add_to_graph(Graph &g) {
-  if (!a_.stencil) {
-    add_exchange(g);
-    return;
-  }
-  // the exchange as one compound op, shared by both alternatives
-  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
-  auto ex = std::make_shared<Graph>();
-  add_exchange(*ex);
-  auto xchg = std::make_shared<StaticCompoundOp>("he_xchg", ex);
-  // split: interior (needs no ghost) runs beside the exchange, the shell after it
-  auto split = std::make_shared<Graph>();
-  auto interior = std::make_shared<HaloStencil>(self, 0);
-  auto shell = std::make_shared<HaloStencil>(self, 1);
-  split->start_then(interior);
-  split->then_finish(interior);
-  split->start_then(xchg);
-  split->then(xchg, shell);
-  split->then_finish(shell);
-  // full: the whole interior after the exchange (one launch)
-  auto full = std::make_shared<Graph>();
-  auto all = std::make_shared<HaloStencil>(self, 2);
-  full->start_then(xchg);
-  full->then(xchg, all);
-  full->then_finish(all);
-  std::vector<OpPtr> alts = {std::make_shared<StaticCompoundOp>("st_split", split),
-                             std::make_shared<StaticCompoundOp>("st_after", full)};
-  auto c = std::make_shared<StaticChoiceOp>("st_mode", alts);
-  g.start_then(c);
-  g.then_finish(c);
-}
-
-void HaloExchange::add_exchange(Graph &g) {
-  // self-neighbour directions are moved directly and remote directions go through RCCL or IPC
-  // puts; the local moves form their own op(s), the remote directions get the fuse structure
-  // (and the search overlaps the two). With both transports available ("auto" on several
-  // ranks) the transport itself is a ChoiceOp the search decides.
-  std::vector<int> local, remote;
-  for (int i = 0; i < ndirs(); ++i) (direct_[i] ? local : remote).push_back(i);
-  if (remote.empty()) {
-    add_structure(g, all_dirs(), kViaPipe, "");
-    return;
-  }
-  if (!local.empty()) {
-    if (a_.fuse == "none") add_chains(g, local, kViaPipe);
-    else add_fused(g, local, "self", kViaPipe);
-  }
-  // graph-only builds (no setup) assume IPC can be mapped
-  const bool ipc = useIpc_ && (ipcReady_ || !ready());
-  const bool pipe = useRccl_ || a_.transport == "copy";
-  TZ_CHECK(ipc || pipe, "no transport available for the remote directions");
-  // the copy-engine variant needs receive buffers ("buffers" mode)
-  const bool copy = ipc && useCopy_ && !ipcGrid_;
-  std::vector<OpPtr> alts;
-  if (pipe) {
-    auto gr = std::make_shared<Graph>();
-    add_structure(*gr, remote, kViaPipe, "");
-    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_rccl", gr));
-  }
-  if (ipc) {
-    auto gr = std::make_shared<Graph>();
-    add_ipc_part(*gr, remote, kViaPut);
-    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_ipc", gr));
-  }
-  if (copy) {
-    auto gr = std::make_shared<Graph>();
-    add_ipc_part(*gr, remote, kViaCopy);
-    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_sdma", gr));
-  }
-  if (alts.size() > 1) {
-    auto c = std::make_shared<StaticChoiceOp>("he_remote", alts);
-    g.start_then(c);
-    g.then_finish(c);
-  } else if (ipc) {
-    add_ipc_part(g, remote, kViaPut);
-  } else {
-    add_structure(g, remote, kViaPipe, "");
-  }
-}
 
 } // namespace tz

@@ -1,0 +1,419 @@
+// Halo workload, op graph: the GPU ops and the graph builder with its ChoiceOps (per-direction
+// or fused groups, RCCL / IPC / SDMA transport, stencil placement).
+// Reference: src/halo_exchange/ops_halo_exchange.cu:33-84 (HaloExchange::add_to_graph).
+#include "halo_internal.hpp"
+
+namespace tz {
+
+namespace {
+
+// byte-cost model for the simulator: ~5 TB/s effective HBM stream + launch latency
+double copy_cost_us(double bytes) { return 3.0 + bytes / 5.0e6; }
+
+class HaloPack : public GpuOp {
+public:
+  HaloPack(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_pack_" + h_->dir(i_).name(); }
+  std::string kind() const override { return "HaloPack"; }
+  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
+  double cost_us() const override { return copy_cost_us(bytes()); }
+  void launch(void *s, Executor &) const override { h_->pack(i_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+class HaloUnpack : public GpuOp {
+public:
+  HaloUnpack(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_unpack_" + h_->dir(i_).name(); }
+  std::string kind() const override { return "HaloUnpack"; }
+  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
+  double cost_us() const override { return copy_cost_us(bytes()); }
+  void launch(void *s, Executor &) const override { h_->unpack(i_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+class HaloShift : public GpuOp {
+public:
+  HaloShift(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_shift_" + h_->dir(i_).name(); }
+  std::string kind() const override { return h_->uses_rccl() ? "HaloShift" : "HaloCopy"; }
+  double bytes() const override { return 8.0 * double(h_->box_elems(i_)); }
+  // xGMI link ~100 GB/s effective per direction + RCCL launch; self copy ~2.5 TB/s
+  double cost_us() const override {
+    return h_->uses_rccl() ? 8.0 + bytes() / 1.0e5 : 3.0 + bytes() / 2.5e6;
+  }
+  void launch(void *s, Executor &ex) const override { h_->shift(i_, s, ex.stream_index(s)); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+/// direct transport of one direction: interior slab -> neighbour's ghost (no buffers)
+class HaloDirect : public GpuOp {
+public:
+  HaloDirect(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_direct_" + h_->dir(i_).name(); }
+  std::string kind() const override { return "HaloDirect"; }
+  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
+  double cost_us() const override { return copy_cost_us(bytes()); }
+  void launch(void *s, Executor &) const override { h_->direct(i_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+/// ipc transport: pack-free put of one direction into the neighbour's grid + arrival signal
+class HaloPut : public GpuOp {
+public:
+  HaloPut(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
+  std::string name() const override { return "he_put_" + h_->dir(i_).name(); }
+  std::string kind() const override { return "HaloPut"; }
+  double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
+  // peer stores over one xGMI link (~60 GB/s effective)
+  double cost_us() const override { return 4.0 + bytes() / 2.0 / 6.0e4; }
+  void launch(void *s, Executor &) const override { h_->put_group({i_}, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int i_;
+};
+
+/// stencil over an interior region (stencil mode)
+class HaloStencil : public GpuOp {
+public:
+  HaloStencil(std::shared_ptr<const HaloExchange> h, int region) : h_(std::move(h)), region_(region) {}
+  std::string name() const override {
+    static const char *n[] = {"st_interior", "st_boundary", "st_full"};
+    return n[region_];
+  }
+  std::string kind() const override { return "Stencil7"; }
+  double bytes() const override {
+    const auto &a = h_->args();
+    const double n3 = double(a.nx) * a.ny * a.nz, in3 = double(a.nx - 2) * (a.ny - 2) * (a.nz - 2);
+    const double cells = region_ == 0 ? in3 : (region_ == 1 ? n3 - in3 : n3);
+    return 16.0 * cells * a.nq;
+  }
+  double cost_us() const override { return 3.0 + bytes() / 4.0e6; }
+  void launch(void *s, Executor &) const override { h_->stencil(region_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  int region_;
+};
+
+/// ipc transport: device-side wait for the neighbours' puts into my ghosts
+class HaloWait : public GpuOp {
+public:
+  HaloWait(std::shared_ptr<const HaloExchange> h, std::vector<int> dirs, std::string tag)
+      : h_(std::move(h)), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
+  std::string name() const override { return "he_wait_" + tag_; }
+  std::string kind() const override { return "HaloWait"; }
+  double cost_us() const override { return 3.0; }
+  void launch(void *s, Executor &) const override { h_->wait_group(dirs_, s); }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  std::vector<int> dirs_;
+  std::string tag_;
+};
+
+/// one op for a whole group of directions (single kernel launch / single RCCL group)
+class HaloStageGroup : public GpuOp {
+public:
+  // UnpackRelease: unpack IPC receive buffers, then hand them back to the senders (credits)
+  // CopyPut: pack locally, copy-engine (SDMA) copy into the peer's receive buffer, signal
+  enum Stage { Pack, Shift, Unpack, Direct, Put, UnpackRelease, CopyPut };
+  HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag)
+      : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
+  std::string name() const override {
+    static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_", "he_put_",
+                                "he_unpack_", "he_copyput_"};
+    return pre[st_] + tag_;
+  }
+  std::string kind() const override {
+    static const char *k[] = {"HaloPackGroup", "HaloShiftGroup", "HaloUnpackGroup",
+                              "HaloDirectGroup", "HaloPutGroup", "HaloUnpackGroup",
+                              "HaloCopyPutGroup"};
+    return k[st_];
+  }
+  double bytes() const override {
+    double b = 0;
+    for (int i : dirs_) b += 8.0 * double(h_->box_elems(i));
+    return (st_ == Shift ? 1.0 : 2.0) * b;
+  }
+  double cost_us() const override {
+    if (st_ == Shift) return h_->uses_rccl() ? 10.0 + bytes() / 3.0e5 : 3.0 + bytes() / 2.5e6;
+    return copy_cost_us(bytes());
+  }
+  void launch(void *s, Executor &ex) const override {
+    if (st_ == Pack) h_->pack_group(dirs_, s);
+    else if (st_ == Shift) h_->shift_group(dirs_, s, ex.stream_index(s));
+    else if (st_ == Unpack) h_->unpack_group(dirs_, s);
+    else if (st_ == Direct) h_->direct_group(dirs_, s);
+    else if (st_ == Put) h_->put_group(dirs_, s);
+    else if (st_ == CopyPut) h_->copy_put_group(dirs_, s);
+    else h_->ipc_unpack_group(dirs_, s);
+  }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  Stage st_;
+  std::vector<int> dirs_;
+  std::string tag_;
+};
+
+} // namespace
+
+void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, int via) {
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  for (int i : dirs) {
+    if (direct_[i] || via != kViaPipe) {
+      OpPtr d;
+      if (direct_[i]) d = std::make_shared<HaloDirect>(self, i);
+      else if (via == kViaPut) d = std::make_shared<HaloPut>(self, i);
+      else d = std::make_shared<HaloStageGroup>(self, HaloStageGroup::CopyPut, std::vector<int>{i},
+                                                dirs_[i].name());
+      g.start_then(d);
+      g.then_finish(d);
+      continue;
+    }
+    auto p = std::make_shared<HaloPack>(self, i);
+    auto s = std::make_shared<HaloShift>(self, i);
+    auto u = std::make_shared<HaloUnpack>(self, opp_[i]);
+    g.start_then(p);
+    g.then(p, s);
+    g.then(s, u);
+    g.then_finish(u);
+  }
+}
+
+void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag,
+                             int via) {
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  std::vector<int> local, remote;
+  for (int i : dirs) (direct_[i] ? local : remote).push_back(i);
+  if (!local.empty()) {
+    auto d = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Direct, local,
+                                              remote.empty() ? tag : tag + "_self");
+    g.start_then(d);
+    g.then_finish(d);
+  }
+  if (remote.empty()) return;
+  if (via != kViaPipe) {
+    auto d = std::make_shared<HaloStageGroup>(
+        self, via == kViaPut ? HaloStageGroup::Put : HaloStageGroup::CopyPut, remote, tag);
+    g.start_then(d);
+    g.then_finish(d);
+    return;
+  }
+  auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, remote, tag);
+  auto s = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Shift, remote, tag);
+  auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, remote, tag);
+  g.start_then(p);
+  g.then(p, s);
+  g.then(s, u);
+  g.then_finish(u);
+}
+
+void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via,
+                                 const std::string &pre) {
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  const std::string &f = a_.fuse;
+  const bool singleStage = direct_[dirs.front()] || via != kViaPipe;
+  auto subset = [&](const std::vector<int> &v) {
+    std::vector<int> r;
+    for (int i : v)
+      if (std::find(dirs.begin(), dirs.end(), i) != dirs.end()) r.push_back(i);
+    return r;
+  };
+  if (f == "none") {
+    add_chains(g, dirs, via);
+  } else if (f == "all" || (f == "pack" && singleStage)) {
+    // (direct moves and puts have no pack stage: "pack" degenerates to one fused op)
+    add_fused(g, dirs, "all", via);
+  } else if (f == "pack") {
+    // fused pack / unpack kernels, per-direction transfers
+    auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, "all");
+    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, dirs, "all");
+    g.start_then(p);
+    g.then_finish(u);
+    for (int i : dirs) {
+      auto s = std::make_shared<HaloShift>(self, i);
+      g.then(p, s);
+      g.then(s, u);
+    }
+  } else if (f == "groups" || f == "choice") {
+    // faces and (for 26 neighbours) edges+corners form independent groups; each group is
+    // either one chain per direction or one fused chain. With "choice" the search decides
+    // (ChoiceOp of two CompoundOps; the group touches no other op, so choosing at the group
+    // boundary loses no dependency precision).
+    std::vector<std::pair<std::string, std::vector<int>>> groups;
+    for (auto &gr : std::vector<std::pair<std::string, std::vector<int>>>{
+             {"faces", subset(group_dirs(1))}, {"small", subset(group_dirs(0))}})
+      if (!gr.second.empty()) groups.push_back(gr);
+    if (f == "groups") {
+      for (auto &gr : groups) add_fused(g, gr.second, gr.first, via);
+      return;
+    }
+    // per group: split chains vs one fused chain
+    auto grouped = std::make_shared<Graph>();
+    for (auto &gr : groups) {
+      auto split = std::make_shared<Graph>();
+      add_chains(*split, gr.second, via);
+      auto fused = std::make_shared<Graph>();
+      add_fused(*fused, gr.second, gr.first, via);
+      std::vector<OpPtr> alts = {
+          std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_split", split),
+          std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_fused", fused)};
+      auto choice = std::make_shared<StaticChoiceOp>(pre + "he_" + gr.first, alts);
+      grouped->start_then(choice);
+      grouped->then_finish(choice);
+    }
+    if (groups.size() == 1) {
+      auto c = std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped);
+      g.start_then(c);
+      g.then_finish(c);
+      return;
+    }
+    // two groups: additionally one chain for every direction (a single launch per stage
+    // avoids the two groups' kernels competing for CUs)
+    auto all = std::make_shared<Graph>();
+    add_fused(*all, dirs, "all", via);
+    std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped),
+                              std::make_shared<StaticCompoundOp>(pre + "he_allfused", all)};
+    // remote directions to several peers: one chain per peer as well. Each peer is one xGMI
+    // link, so per-peer transfers on different streams use the links in parallel (copy-engine
+    // copies and RCCL groups issued on one stream would take them one at a time)
+    // Every rank must build the same graph (schedules are broadcast by op name): the split of
+    // directions by peer is the same on every rank of a periodic Cartesian grid, so groups are
+    // kept in order of their first direction and named after it, never after a rank id.
+    std::map<int, std::vector<int>> byPeer;
+    for (int i : dirs)
+      if (!direct_[i]) byPeer[nbr_[i]].push_back(i);
+    if (byPeer.size() > 1 && byPeer.size() < dirs.size()) {
+      std::vector<std::vector<int>> groupsByPeer;
+      for (const auto &kv : byPeer) groupsByPeer.push_back(kv.second);
+      std::sort(groupsByPeer.begin(), groupsByPeer.end());
+      auto peers = std::make_shared<Graph>();
+      for (const auto &grp : groupsByPeer) add_fused(*peers, grp, "p" + dirs_[grp.front()].name(), via);
+      top.push_back(std::make_shared<StaticCompoundOp>(pre + "he_bypeer", peers));
+    }
+    auto choice = std::make_shared<StaticChoiceOp>(pre + "he_exchange", top);
+    g.start_then(choice);
+    g.then_finish(choice);
+  } else {
+    TZ_THROW("fuse must be none, pack, all, groups or choice (got " << f << ")");
+  }
+}
+
+void HaloExchange::add_ipc_part(Graph &g, const std::vector<int> &remote, int via) {
+  // puts wait only for the credit of the previous iteration, so each rank's puts all complete;
+  // the arrival wait runs after them (one spinning kernel per rank, never ahead of its own
+  // puts). The copy-engine variant's op names carry "cp_" (unique in the expanded graph).
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  const std::string v = via == kViaCopy ? "cp_" : "";
+  auto puts = std::make_shared<Graph>();
+  add_structure(*puts, remote, via, via == kViaCopy ? "cp_" : "ipc_");
+  auto c = std::make_shared<StaticCompoundOp>("he_" + v + "puts", puts);
+  auto w = std::make_shared<HaloWait>(self, remote, v + "remote");
+  g.start_then(c);
+  g.then(c, w);
+  if (ipcGrid_) {
+    g.then_finish(w);
+  } else {
+    // "buffers" mode: my receive buffers are complete after the wait; unpack them
+    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::UnpackRelease, remote, v + "remote");
+    g.then(w, u);
+    g.then_finish(u);
+  }
+}
+
+void HaloExchange::add_to_graph(Graph &g) {
+  if (!a_.stencil) {
+    add_exchange(g);
+    return;
+  }
+  // the exchange as one compound op, shared by both alternatives
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  auto ex = std::make_shared<Graph>();
+  add_exchange(*ex);
+  auto xchg = std::make_shared<StaticCompoundOp>("he_xchg", ex);
+  // split: interior (needs no ghost) runs beside the exchange, the shell after it
+  auto split = std::make_shared<Graph>();
+  auto interior = std::make_shared<HaloStencil>(self, 0);
+  auto shell = std::make_shared<HaloStencil>(self, 1);
+  split->start_then(interior);
+  split->then_finish(interior);
+  split->start_then(xchg);
+  split->then(xchg, shell);
+  split->then_finish(shell);
+  // full: the whole interior after the exchange (one launch)
+  auto full = std::make_shared<Graph>();
+  auto all = std::make_shared<HaloStencil>(self, 2);
+  full->start_then(xchg);
+  full->then(xchg, all);
+  full->then_finish(all);
+  std::vector<OpPtr> alts = {std::make_shared<StaticCompoundOp>("st_split", split),
+                             std::make_shared<StaticCompoundOp>("st_after", full)};
+  auto c = std::make_shared<StaticChoiceOp>("st_mode", alts);
+  g.start_then(c);
+  g.then_finish(c);
+}
+
+void HaloExchange::add_exchange(Graph &g) {
+  // self-neighbour directions are moved directly and remote directions go through RCCL or IPC
+  // puts; the local moves form their own op(s), the remote directions get the fuse structure
+  // (and the search overlaps the two). With both transports available ("auto" on several
+  // ranks) the transport itself is a ChoiceOp the search decides.
+  std::vector<int> local, remote;
+  for (int i = 0; i < ndirs(); ++i) (direct_[i] ? local : remote).push_back(i);
+  if (remote.empty()) {
+    add_structure(g, all_dirs(), kViaPipe, "");
+    return;
+  }
+  if (!local.empty()) {
+    if (a_.fuse == "none") add_chains(g, local, kViaPipe);
+    else add_fused(g, local, "self", kViaPipe);
+  }
+  // graph-only builds (no setup) assume IPC can be mapped
+  const bool ipc = useIpc_ && (ipcReady_ || !ready());
+  const bool pipe = useRccl_ || a_.transport == "copy";
+  TZ_CHECK(ipc || pipe, "no transport available for the remote directions");
+  // the copy-engine variant needs receive buffers ("buffers" mode)
+  const bool copy = ipc && useCopy_ && !ipcGrid_;
+  std::vector<OpPtr> alts;
+  if (pipe) {
+    auto gr = std::make_shared<Graph>();
+    add_structure(*gr, remote, kViaPipe, "");
+    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_rccl", gr));
+  }
+  if (ipc) {
+    auto gr = std::make_shared<Graph>();
+    add_ipc_part(*gr, remote, kViaPut);
+    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_ipc", gr));
+  }
+  if (copy) {
+    auto gr = std::make_shared<Graph>();
+    add_ipc_part(*gr, remote, kViaCopy);
+    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_sdma", gr));
+  }
+  if (alts.size() > 1) {
+    auto c = std::make_shared<StaticChoiceOp>("he_remote", alts);
+    g.start_then(c);
+    g.then_finish(c);
+  } else if (ipc) {
+    add_ipc_part(g, remote, kViaPut);
+  } else {
+    add_structure(g, remote, kViaPipe, "");
+  }
+}
+
+} // namespace tz
