@@ -71,10 +71,12 @@ def main() -> int:
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=40)
     ap.add_argument("--search-budget-s", type=float, default=120.0)
-    # per candidate: 10 measurements of >= 3 ms each. 20 x 4 ms finds the same best schedule
-    # with twice the search time (profiles/r1_search_len/bench_settings.txt)
-    ap.add_argument("--bench-iters", type=int, default=10)
-    ap.add_argument("--target-secs", type=float, default=0.003)
+    # per candidate: 6 measurements of >= 2 ms each; the 4 best are re-measured interleaved
+    # (--rerank) before the final timing. 20 x 4 ms, 10 x 3 ms, 8 x 2 ms and 5 x 1.5 ms all find
+    # the same best schedule; 6 x 2 ms halves the search wall-clock of 10 x 3 ms
+    # (profiles/r1_search_len/)
+    ap.add_argument("--bench-iters", type=int, default=6)
+    ap.add_argument("--target-secs", type=float, default=0.002)
     ap.add_argument("--strategy", default="FastMin")
     ap.add_argument("--search-mode", default="graph", choices=["eager", "graph"],
                     help="benchmark candidates eagerly or compiled to hipGraphs (default: graph, "
