@@ -149,6 +149,13 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   }
   ipcGrid_ = gridElems_ * sizeof(double) < (size_t(2) << 30);
   if (const char *v = std::getenv("TZ_IPC_GRID")) ipcGrid_ = std::atoi(v) != 0;
+  // In grid mode a receiver hands the credit back as soon as the ghosts arrived, so a sender
+  // one iteration ahead may overwrite them. That is fine while nothing reads them between
+  // exchanges, but the stencil does: it takes buffers mode, where puts land in receive buffers
+  // and the credit waits for the unpack into the grid. (A credit deferred to the next
+  // exchange's start removes the slack that keeps puts from waiting on the peer's current
+  // iteration; with several ranks time-slicing one GPU that stalled waits for seconds.)
+  if (a_.stencil) ipcGrid_ = false;
   // copy-engine puts (buffers mode only): on unless TZ_IPC_COPY=0
   useCopy_ = useIpc_;
   if (const char *v = std::getenv("TZ_IPC_COPY")) useCopy_ = useCopy_ && std::atoi(v) != 0;

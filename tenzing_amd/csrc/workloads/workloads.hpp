@@ -225,7 +225,9 @@ public:
   /// ipc transport: "grid" (puts land directly in the peer's ghost cells) or "buffers" (puts
   /// fill the peer's receive buffers, which it unpacks after the arrival wait). Grids of 2 GiB
   /// or more use "buffers": the dmabuf IPC path of this platform cannot map allocations that
-  /// large (measured, scripts/ipc_probe.py); env TZ_IPC_GRID=0/1 forces a mode.
+  /// large (measured, scripts/ipc_probe.py); env TZ_IPC_GRID=0/1 forces a mode. Grid mode
+  /// returns each credit right after the arrival, so ghosts stay valid only until the peer's
+  /// next put: stencil mode (which reads them after the exchange) always uses "buffers".
   std::string ipc_mode() const { return useIpc_ ? (ipcGrid_ ? "grid" : "buffers") : ""; }
   /// direct transport: move the interior slab facing each direction of `dirs` straight into
   /// the neighbour's ghost region on the opposite side (one launch)
