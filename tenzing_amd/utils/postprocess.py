@@ -133,13 +133,18 @@ def feature_matrix(results: list[Result]):
     cols = []
     # same stream (unordered pairs)
     pairs = [(a, b) for i, a in enumerate(gpu_ops) for b in gpu_ops[i + 1:]]
-    order_pairs = [(a, b) for a in graph_ops for b in graph_ops if a != b]
+    # Start/Finish bracket every schedule: "Start before X" only restates "uses X"
+    ends = ("Start", "Finish")
+    order_pairs = [(a, b) for a in graph_ops for b in graph_ops
+                   if a != b and a not in ends and b not in ends]
+    # "uses X" first: of two identical columns the earlier name is kept, and the choice taken
+    # is the most readable reason for a class
+    for o in optional:
+        names.append(f"uses {o}")
     for a, b in pairs:
         names.append(f"{a} and {b} same stream")
     for a, b in order_pairs:
         names.append(f"{a} before {b}")
-    for o in optional:
-        names.append(f"uses {o}")
     names += ["streams>=2", "streams>=3", "streams>=4"]
     X = np.zeros((len(results), len(names)), dtype=np.int8)
     for ri, r in enumerate(results):
@@ -154,14 +159,14 @@ def feature_matrix(results: list[Result]):
                 stream[op["name"]] = op["stream"]
             pos.setdefault(op["name"], k)
         c = 0
+        for o in optional:
+            X[ri, c] = int(o in pos)
+            c += 1
         for a, b in pairs:
             X[ri, c] = int(a in stream and b in stream and stream[a] == stream[b])
             c += 1
         for a, b in order_pairs:
             X[ri, c] = int(a in pos and b in pos and pos[a] < pos[b])
-            c += 1
-        for o in optional:
-            X[ri, c] = int(o in pos)
             c += 1
         ns = len(set(stream.values()))
         for t in (2, 3, 4):
