@@ -26,6 +26,7 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -34,7 +35,11 @@ namespace tz {
 namespace kern {
 
 BoxTuning &box_tuning() {
-  static BoxTuning t;
+  static BoxTuning t = [] {
+    BoxTuning v;
+    if (const char *e = std::getenv("TZ_XCD_REMAP")) v.xcd_remap = std::atoi(e) != 0;
+    return v;
+  }();
   return t;
 }
 
@@ -75,7 +80,18 @@ struct DevBatch {
   DevDesc d[kMaxBoxes];
   uint32_t block_start[kMaxBoxes + 1];
   int32_t n;
+  uint32_t total;   // logical blocks (the launch may be padded up to a multiple of 8)
+  uint32_t per_xcd; // 0: logical block = blockIdx.x; else blocks per XCD of the remap
 };
+
+// The dispatcher deals workgroups to the 8 XCDs round-robin (hardware block b runs on XCD
+// b % 8). With the remap, XCD x runs logical blocks [x * per_xcd, (x + 1) * per_xcd): each
+// pass of the grid-stride loop then covers one contiguous span of memory per XCD, so rows that
+// cross a block boundary (72-B x-face runs) stay within one L2.
+__device__ __forceinline__ uint32_t logical_block(const DevBatch &b) {
+  if (b.per_xcd == 0) return blockIdx.x;
+  return (blockIdx.x % 8u) * b.per_xcd + blockIdx.x / 8u;
+}
 
 constexpr int kThreads = 256;
 
@@ -210,11 +226,13 @@ __device__ __forceinline__ void move_body(const DevDesc &d, uint32_t tid, uint32
 
 template <int U, bool NT>
 __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b) {
+  const uint32_t lb = logical_block(b);
+  if (lb >= b.total) return; // padding of the remapped launch (no barriers in this kernel)
   int box = 0;
-  while (box + 1 < b.n && blockIdx.x >= b.block_start[box + 1]) ++box;
+  while (box + 1 < b.n && lb >= b.block_start[box + 1]) ++box;
   const DevDesc &d = b.d[box];
   const uint32_t nb = b.block_start[box + 1] - b.block_start[box];
-  const uint32_t tid = (blockIdx.x - b.block_start[box]) * kThreads + threadIdx.x;
+  const uint32_t tid = (lb - b.block_start[box]) * kThreads + threadIdx.x;
   const uint32_t nth = nb * kThreads;
   if (d.vec == 2) move_body<2, U, NT>(d, tid, nth);
   else move_body<1, U, NT>(d, tid, nth);
@@ -507,10 +525,12 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
   if (n > kMaxBoxes) throw std::runtime_error("box_move_many: too many boxes");
   uint32_t total = 0;
   std::vector<int> keep;
-  const DevBatch b = make_move_batch(moves, n, total, keep);
+  DevBatch b = make_move_batch(moves, n, total, keep);
   if (b.n == 0) return;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 g(total);
+  b.total = total;
+  b.per_xcd = box_tuning().xcd_remap ? (total + 7) / 8 : 0;
+  const dim3 g(b.per_xcd ? b.per_xcd * 8 : total);
   if (box_tuning().nt_move) hipLaunchKernelGGL((box_move_many_k<4, true>), g, dim3(kThreads), 0, s, b);
   else hipLaunchKernelGGL((box_move_many_k<4, false>), g, dim3(kThreads), 0, s, b);
   TZ_HIP_LAUNCH_CHECK();

@@ -30,6 +30,7 @@ struct BoxTuning {
   bool nt_unpack = false; // non-temporal grid stores in unpack: +5 % (off)
   int max_blocks = 4096;  // cap per box (grid-stride beyond)
   bool nt_move = true;    // non-temporal source loads in box_move (direct transfers)
+  bool xcd_remap = false; // box_move: give each XCD a contiguous range of logical blocks
 };
 BoxTuning &box_tuning();
 
