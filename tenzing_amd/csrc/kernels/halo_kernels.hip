@@ -37,7 +37,7 @@ namespace kern {
 BoxTuning &box_tuning() {
   static BoxTuning t = [] {
     BoxTuning v;
-    if (const char *e = std::getenv("TZ_XCD_REMAP")) v.xcd_remap = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TZ_XCD_REMAP")) v.xcd_remap = std::atoi(e);
     return v;
   }();
   return t;
@@ -82,6 +82,8 @@ struct DevBatch {
   int32_t n;
   uint32_t total;   // logical blocks (the launch may be padded up to a multiple of 8)
   uint32_t per_xcd; // 0: logical block = blockIdx.x; else blocks per XCD of the remap
+  uint32_t box_xcd; // per-box remap: block_start padded to multiples of 8, nreal = real blocks
+  uint16_t nreal[kMaxBoxes]; // (16 bits: max_blocks <= 65535; keeps the kernarg block < 4 KB)
 };
 
 // The dispatcher deals workgroups to the 8 XCDs round-robin (hardware block b runs on XCD
@@ -231,8 +233,14 @@ __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b) {
   int box = 0;
   while (box + 1 < b.n && lb >= b.block_start[box + 1]) ++box;
   const DevDesc &d = b.d[box];
-  const uint32_t nb = b.block_start[box + 1] - b.block_start[box];
-  const uint32_t tid = (lb - b.block_start[box]) * kThreads + threadIdx.x;
+  uint32_t nb = b.block_start[box + 1] - b.block_start[box];
+  uint32_t j = lb - b.block_start[box];
+  if (b.box_xcd) { // every box spread over all 8 XCDs, one contiguous share of it per XCD
+    j = (j % 8u) * (nb / 8u) + j / 8u;
+    nb = b.nreal[box];
+    if (j >= nb) return;
+  }
+  const uint32_t tid = j * kThreads + threadIdx.x;
   const uint32_t nth = nb * kThreads;
   if (d.vec == 2) move_body<2, U, NT>(d, tid, nth);
   else move_body<1, U, NT>(d, tid, nth);
@@ -528,8 +536,22 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
   DevBatch b = make_move_batch(moves, n, total, keep);
   if (b.n == 0) return;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const int mode = box_tuning().xcd_remap;
+  if (mode == 2) { // pad every box to a multiple of 8 blocks, starting on a multiple of 8
+    uint32_t t = 0;
+    for (int i = 0; i < b.n; ++i) {
+      const uint32_t nb = b.block_start[i + 1] - b.block_start[i];
+      if (nb > 65535) throw std::runtime_error("box_move_many: too many blocks for the remap");
+      b.nreal[i] = uint16_t(nb);
+      b.block_start[i] = t;
+      t += (nb + 7) / 8 * 8;
+    }
+    b.block_start[b.n] = t;
+    total = t;
+    b.box_xcd = 1;
+  }
   b.total = total;
-  b.per_xcd = box_tuning().xcd_remap ? (total + 7) / 8 : 0;
+  b.per_xcd = mode == 1 ? (total + 7) / 8 : 0;
   const dim3 g(b.per_xcd ? b.per_xcd * 8 : total);
   if (box_tuning().nt_move) hipLaunchKernelGGL((box_move_many_k<4, true>), g, dim3(kThreads), 0, s, b);
   else hipLaunchKernelGGL((box_move_many_k<4, false>), g, dim3(kThreads), 0, s, b);

@@ -30,7 +30,8 @@ struct BoxTuning {
   bool nt_unpack = false; // non-temporal grid stores in unpack: +5 % (off)
   int max_blocks = 4096;  // cap per box (grid-stride beyond)
   bool nt_move = true;    // non-temporal source loads in box_move (direct transfers)
-  bool xcd_remap = false; // box_move: give each XCD a contiguous range of logical blocks
+  int xcd_remap = 0; // box_move block order: 0 round-robin, 1 one contiguous range per XCD,
+                     // 2 every box split into 8 contiguous per-XCD shares
 };
 BoxTuning &box_tuning();
 
