@@ -50,9 +50,11 @@ def test_box_copy_pack_unpack_matches_torch(tz, gpu, order, neighbors):
         assert torch.equal(g2, exp), f"unpack mismatch dir {h.dir_name(i)}"
 
 
+@pytest.mark.parametrize("remap", [0, 1, 2])
 @pytest.mark.parametrize("order", ["xyzq", "qxyz"])
-def test_box_move_matches_torch(tz, gpu, order):
-    """direct transfer kernel: interior slab facing d -> ghost on side -d, all 26 at once"""
+def test_box_move_matches_torch(tz, gpu, order, remap):
+    """direct transfer kernel: interior slab facing d -> ghost on side -d, all 26 at once, under
+    each block order (0 round-robin, 1 and 2 the XCD-aware orders with padded launches)"""
     a = tz.HaloArgs()
     a.nx, a.ny, a.nz, a.nq, a.ghost = 20, 12, 9, 3, 2
     a.neighbors, a.order = 26, order
@@ -72,8 +74,13 @@ def test_box_move_matches_torch(tz, gpu, order):
                 do = d["grid_off"] + i2 * s["s2"] + i3 * s["s3"]
                 exp.as_strided((s["n1"], s["len"]), (s["s1"], 1), do).copy_(
                     grid.as_strided((s["n1"], s["len"]), (s["s1"], 1), so))
-    tz._tz.kernels.box_move_many(moves, _stream())
-    torch.cuda.synchronize()
+    prev = tz._tz.kernels.get_xcd_remap()
+    tz._tz.kernels.set_xcd_remap(remap)
+    try:
+        tz._tz.kernels.box_move_many(moves, _stream())
+        torch.cuda.synchronize()
+    finally:
+        tz._tz.kernels.set_xcd_remap(prev)
     assert torch.equal(out, exp)
 
 
