@@ -798,7 +798,7 @@ PYBIND11_MODULE(_tz, m) {
     kern::box_tuning().nt_move = ntMove;
   }, py::arg("unroll") = 4, py::arg("nt_pack") = true, py::arg("nt_unpack") = false,
      py::arg("max_blocks") = 4096, py::arg("nt_move") = true);
-  k.def("set_xcd_remap", [](int mode) { kern::box_tuning().xcd_remap = mode; }, py::arg("mode"));
+  k.def("set_xcd_remap", &kern::set_xcd_remap, py::arg("mode"));
   k.def("get_xcd_remap", []() { return kern::box_tuning().xcd_remap; });
   k.def("get_box_tuning", []() {
     const auto &t = kern::box_tuning();

@@ -50,9 +50,21 @@ EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, d
   while (true) {
     ctrl_.barrier();
     const double t0 = wtime();
-    runner_.run(m.n);
-    double elapsed = wtime() - t0;
-    elapsed = ctrl_.allreduce_max(elapsed); // "true" time is the max over ranks
+    // a run-time failure (launch error, watchdog, op check) may hit one rank only: it travels
+    // with the time in the same max-reduction, so every rank throws together and the next
+    // collective still matches
+    std::string err;
+    try {
+      runner_.run(m.n);
+    } catch (const std::exception &e) {
+      err = e.what();
+    }
+    double red[2] = {wtime() - t0, err.empty() ? 0.0 : 1.0};
+    ctrl_.allreduce_max(red, 2); // "true" time is the max over ranks
+    if (red[1] != 0.0)
+      throw CandidateFailed("schedule run failed" +
+                            (err.empty() ? std::string(" on another rank") : ": " + err));
+    const double elapsed = red[0];
     if (elapsed < targetSecs) {
       const double perSample = std::max(elapsed / double(m.n), 1e-9);
       const double est = targetSecs / perSample * 1.1;
@@ -77,7 +89,8 @@ void EmpiricalBenchmarker::collective_prepare(const std::function<void()> &fn) {
   double bad = err.empty() ? 0.0 : 1.0;
   if (ctrl_.size() > 1) ctrl_.allreduce_max(&bad, 1);
   if (bad != 0.0)
-    TZ_THROW("schedule preparation failed" << (err.empty() ? " on another rank" : ": " + err));
+    throw CandidateFailed("schedule preparation failed" +
+                          (err.empty() ? std::string(" on another rank") : ": " + err));
 }
 
 BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts &opts) {

@@ -27,6 +27,13 @@ namespace tz {
 
 static constexpr double kInf = std::numeric_limits<double>::infinity();
 
+/// A benchmark failure the search may skip: one every rank agreed on (CandidateFailed), or any
+/// failure when there is a single rank. Anything else may be local to one rank, and skipping it
+/// would leave that rank's peers blocked in the benchmark's collectives, so it propagates.
+static bool skippable(const std::exception &e, const Ctrl &ctrl) {
+  return dynamic_cast<const CandidateFailed *>(&e) != nullptr || ctrl.size() == 1;
+}
+
 // ======================================================================== results
 
 int SearchResult::best() const {
@@ -622,11 +629,12 @@ SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &ben
     if (!cached) {
       ScopedTimer t(C, "BENCHMARK");
       if (opts.skip_failed) {
-        // preparation failures (e.g. a schedule that cannot be compiled to a hipGraph) are
-        // agreed on collectively by the benchmarker, so every rank skips the same candidate
+        // preparation and run failures (e.g. a schedule that cannot be compiled to a hipGraph)
+        // are agreed on collectively by the benchmarker, so every rank skips the same candidate
         try {
           br = bench.benchmark(seq, opts.bench);
         } catch (const std::exception &e) {
+          if (!skippable(e, ctrl)) throw;
           failed = true;
           if (root) TZ_LOG(Warn, "mcts iter " << iter << ": candidate skipped: " << e.what());
         }
@@ -751,8 +759,8 @@ SearchResult dfs_explore(const Graph &g, const Platform &plat, Benchmarker &benc
       try {
         sr.res = bench.benchmark(seq, opts.bench);
       } catch (const std::exception &e) {
-        // collective preparation failure: every rank skips this sequence
-        if (!opts.skip_failed) throw;
+        // collective failure: every rank skips this sequence
+        if (!opts.skip_failed || !skippable(e, ctrl)) throw;
         if (root) {
           ++result.failed;
           TZ_LOG(Warn, "dfs sequence " << i << " skipped: " << e.what());

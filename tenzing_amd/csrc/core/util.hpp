@@ -34,6 +34,14 @@ struct Error : public std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+/// A candidate schedule failed on at least one rank and every rank of the control plane knows it
+/// (the benchmarker agreed on the failure through a collective before throwing). Only this error
+/// is safe to skip in a multi-rank search: any other exception may be local to one rank, which
+/// would leave the other ranks inside mismatched collectives.
+struct CandidateFailed : public Error {
+  using Error::Error;
+};
+
 /// Accumulating named phase timers (reference counters::Mcts SELECT_TIME etc.).
 struct Counters {
   std::map<std::string, double> seconds;

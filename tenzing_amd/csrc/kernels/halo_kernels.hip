@@ -26,6 +26,7 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -37,10 +38,20 @@ namespace kern {
 BoxTuning &box_tuning() {
   static BoxTuning t = [] {
     BoxTuning v;
-    if (const char *e = std::getenv("TZ_XCD_REMAP")) v.xcd_remap = std::atoi(e);
+    if (const char *e = std::getenv("TZ_XCD_REMAP")) {
+      const int m = std::atoi(e);
+      if (m >= 0 && m <= 2) v.xcd_remap = m;
+      else std::fprintf(stderr, "[tz] warning: TZ_XCD_REMAP=%s is not 0, 1 or 2; using 0\n", e);
+    }
     return v;
   }();
   return t;
+}
+
+void set_xcd_remap(int mode) {
+  if (mode < 0 || mode > 2)
+    throw std::invalid_argument("xcd_remap must be 0 (round-robin), 1 (per-XCD range) or 2 (per-box)");
+  box_tuning().xcd_remap = mode;
 }
 
 namespace {
@@ -80,19 +91,24 @@ struct DevBatch {
   DevDesc d[kMaxBoxes];
   uint32_t block_start[kMaxBoxes + 1];
   int32_t n;
+};
+
+// XCD block order of box_move_many_k only (the other batch kernels never read it, so it is a
+// kernel argument of its own instead of part of every DevBatch copy)
+struct DevRemap {
   uint32_t total;   // logical blocks (the launch may be padded up to a multiple of 8)
   uint32_t per_xcd; // 0: logical block = blockIdx.x; else blocks per XCD of the remap
   uint32_t box_xcd; // per-box remap: block_start padded to multiples of 8, nreal = real blocks
-  uint16_t nreal[kMaxBoxes]; // (16 bits: max_blocks <= 65535; keeps the kernarg block < 4 KB)
+  uint16_t nreal[kMaxBoxes]; // (16 bits: max_blocks <= 65535)
 };
 
 // The dispatcher deals workgroups to the 8 XCDs round-robin (hardware block b runs on XCD
 // b % 8). With the remap, XCD x runs logical blocks [x * per_xcd, (x + 1) * per_xcd): each
 // pass of the grid-stride loop then covers one contiguous span of memory per XCD, so rows that
 // cross a block boundary (72-B x-face runs) stay within one L2.
-__device__ __forceinline__ uint32_t logical_block(const DevBatch &b) {
-  if (b.per_xcd == 0) return blockIdx.x;
-  return (blockIdx.x % 8u) * b.per_xcd + blockIdx.x / 8u;
+__device__ __forceinline__ uint32_t logical_block(const DevRemap &r) {
+  if (r.per_xcd == 0) return blockIdx.x;
+  return (blockIdx.x % 8u) * r.per_xcd + blockIdx.x / 8u;
 }
 
 constexpr int kThreads = 256;
@@ -227,17 +243,17 @@ __device__ __forceinline__ void move_body(const DevDesc &d, uint32_t tid, uint32
 }
 
 template <int U, bool NT>
-__global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b) {
-  const uint32_t lb = logical_block(b);
-  if (lb >= b.total) return; // padding of the remapped launch (no barriers in this kernel)
+__global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap r) {
+  const uint32_t lb = logical_block(r);
+  if (lb >= r.total) return; // padding of the remapped launch (no barriers in this kernel)
   int box = 0;
   while (box + 1 < b.n && lb >= b.block_start[box + 1]) ++box;
   const DevDesc &d = b.d[box];
   uint32_t nb = b.block_start[box + 1] - b.block_start[box];
   uint32_t j = lb - b.block_start[box];
-  if (b.box_xcd) { // every box spread over all 8 XCDs, one contiguous share of it per XCD
+  if (r.box_xcd) { // every box spread over all 8 XCDs, one contiguous share of it per XCD
     j = (j % 8u) * (nb / 8u) + j / 8u;
-    nb = b.nreal[box];
+    nb = r.nreal[box];
     if (j >= nb) return;
   }
   const uint32_t tid = j * kThreads + threadIdx.x;
@@ -250,6 +266,13 @@ struct DevSignal {
   unsigned int *done;
   unsigned long long *flag[kMaxBoxes];
 };
+
+// explicit kernel arguments are limited to 4 KB; the largest signatures are checked here so a
+// new field cannot push a launch over the limit
+static_assert(sizeof(DevBatch) + sizeof(DevRemap) <= 4096, "box_move_many_k kernargs over 4 KB");
+static_assert(sizeof(DevBatch) + sizeof(DevSignal) <= 4096, "box_move_signal_k kernargs over 4 KB");
+static_assert(sizeof(double *) + sizeof(DevBatch) + sizeof(DevSignal) <= 4096,
+              "box_pack_signal_k kernargs over 4 KB");
 
 __device__ __forceinline__ void signal_box_done(const DevSignal &sig, int box, uint32_t nb);
 
@@ -537,24 +560,25 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
   if (b.n == 0) return;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int mode = box_tuning().xcd_remap;
+  DevRemap r{};
   if (mode == 2) { // pad every box to a multiple of 8 blocks, starting on a multiple of 8
     uint32_t t = 0;
     for (int i = 0; i < b.n; ++i) {
       const uint32_t nb = b.block_start[i + 1] - b.block_start[i];
       if (nb > 65535) throw std::runtime_error("box_move_many: too many blocks for the remap");
-      b.nreal[i] = uint16_t(nb);
+      r.nreal[i] = uint16_t(nb);
       b.block_start[i] = t;
       t += (nb + 7) / 8 * 8;
     }
     b.block_start[b.n] = t;
     total = t;
-    b.box_xcd = 1;
+    r.box_xcd = 1;
   }
-  b.total = total;
-  b.per_xcd = mode == 1 ? (total + 7) / 8 : 0;
-  const dim3 g(b.per_xcd ? b.per_xcd * 8 : total);
-  if (box_tuning().nt_move) hipLaunchKernelGGL((box_move_many_k<4, true>), g, dim3(kThreads), 0, s, b);
-  else hipLaunchKernelGGL((box_move_many_k<4, false>), g, dim3(kThreads), 0, s, b);
+  r.total = total;
+  r.per_xcd = mode == 1 ? (total + 7) / 8 : 0;
+  const dim3 g(r.per_xcd ? r.per_xcd * 8 : total);
+  if (box_tuning().nt_move) hipLaunchKernelGGL((box_move_many_k<4, true>), g, dim3(kThreads), 0, s, b, r);
+  else hipLaunchKernelGGL((box_move_many_k<4, false>), g, dim3(kThreads), 0, s, b, r);
   TZ_HIP_LAUNCH_CHECK();
 }
 

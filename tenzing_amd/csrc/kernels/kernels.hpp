@@ -34,6 +34,8 @@ struct BoxTuning {
                      // 2 every box split into 8 contiguous per-XCD shares
 };
 BoxTuning &box_tuning();
+/// set BoxTuning::xcd_remap; throws std::invalid_argument unless mode is 0, 1 or 2
+void set_xcd_remap(int mode);
 
 /// A box-to-box move between two arrays of the SAME pitched layout: element (x,i1,i2,i3) of
 /// the box at `src + src_off` goes to the same element of the box at `dst + dst_off`

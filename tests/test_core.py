@@ -220,3 +220,19 @@ def test_graph_then_survives_node_reallocation(tz):
     assert g.num_edges() == 600
     for o in ops[:5]:
         assert g.preds(g.find(o.name)) == [0]
+
+
+def test_xcd_remap_mode_is_validated(tz):
+    """only the three block orders exist; a typo must not be recorded as a remap measurement"""
+    k = tz._tz.kernels
+    prev = k.get_xcd_remap()
+    try:
+        for m in (0, 1, 2):
+            k.set_xcd_remap(m)
+            assert k.get_xcd_remap() == m
+        for bad in (-1, 3, 17):
+            with pytest.raises(ValueError):
+                k.set_xcd_remap(bad)
+            assert k.get_xcd_remap() == 2
+    finally:
+        k.set_xcd_remap(prev)

@@ -50,13 +50,17 @@ def test_box_copy_pack_unpack_matches_torch(tz, gpu, order, neighbors):
         assert torch.equal(g2, exp), f"unpack mismatch dir {h.dir_name(i)}"
 
 
+@pytest.mark.parametrize("shape", [(20, 12, 9, 2), (64, 64, 64, 3)])
 @pytest.mark.parametrize("remap", [0, 1, 2])
 @pytest.mark.parametrize("order", ["xyzq", "qxyz"])
-def test_box_move_matches_torch(tz, gpu, order, remap):
+def test_box_move_matches_torch(tz, gpu, order, remap, shape):
     """direct transfer kernel: interior slab facing d -> ghost on side -d, all 26 at once, under
-    each block order (0 round-robin, 1 and 2 the XCD-aware orders with padded launches)"""
+    each block order (0 round-robin, 1 and 2 the XCD-aware orders with padded launches). The
+    64^3 grid gives faces of 9-18 blocks (more than 8 and not a multiple of 8), so the per-box
+    remap's reordering and its grid-stride loop over the real blocks run, not only the padding"""
     a = tz.HaloArgs()
-    a.nx, a.ny, a.nz, a.nq, a.ghost = 20, 12, 9, 3, 2
+    a.nx, a.ny, a.nz, a.ghost = shape
+    a.nq = 3
     a.neighbors, a.order = 26, order
     h = tz.HaloExchange(a)
     grid = torch.randn(h.grid_elems(), dtype=torch.float64, device="cuda")

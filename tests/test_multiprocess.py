@@ -106,6 +106,32 @@ def body_dfs_host():
     return dict(rank=c.rank, n=len(r.sims), p50=[s.res.pct50 for s in r.sims])
 
 
+def body_dfs_one_rank_run_failure():
+    """an op raises on rank 1 only, in the first candidate's first run: every rank must skip that
+    candidate together and carry on with the next one (no rank left in a collective)"""
+    import tenzing_amd as tz
+    from tenzing_amd.parallel import init_ctrl
+
+    c = init_ctrl(timeout_s=60)
+    calls = {"a": 0}
+
+    def fa():
+        calls["a"] += 1
+        if c.rank == 1 and calls["a"] == 1:
+            raise RuntimeError("injected failure on rank 1")
+
+    g = tz.Graph()
+    a, b = tz.PyCpuOp("a", fa), tz.SleepOp("b", 20.0)
+    g.start_then(a)
+    g.start_then(b)
+    g.then_finish(a)
+    g.then_finish(b)
+    o = tz.DfsOpts()
+    o.bench = tz.BenchOpts(n_iters=2, max_retries=1, target_secs=0.001)
+    r = tz.dfs_explore(g, tz.Platform(1), tz.EmpiricalBenchmarker(tz.HostExecutor(1), c), c, o)
+    return dict(rank=c.rank, n=len(r.sims), failed=r.failed)
+
+
 def body_halo_graph_consistency():
     """each rank builds its own halo graph; a schedule from rank 0 deserializes everywhere"""
     import tenzing_amd as tz
@@ -145,6 +171,11 @@ def test_dfs_two_ranks_max_over_ranks(tmp_path):
     assert rs[0]["n"] == 2
     # rank 1 sleeps 400 us in op a: the reported time is the max over ranks
     assert min(rs[0]["p50"]) > 380e-6
+
+
+def test_run_failure_on_one_rank_is_skipped_by_all(tmp_path):
+    rs = _run("body_dfs_one_rank_run_failure", 2, tmp_path)
+    assert rs[0]["failed"] == 1 and rs[0]["n"] == 1
 
 
 def test_halo_schedule_bcast_8ranks(tmp_path):
