@@ -611,6 +611,8 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("pitch_pad", &HaloArgs::pitch_pad)
       .def_readwrite("ghost_align", &HaloArgs::ghost_align)
       .def_readwrite("stencil", &HaloArgs::stencil)
+      .def_readwrite("relay", &HaloArgs::relay)
+      .def_readwrite("relay_fracs", &HaloArgs::relay_fracs)
       .def_readwrite("device", &HaloArgs::device)
       .def("json", [](const HaloArgs &a) { return a.json().dump(); });
   py::class_<HaloExchange, std::shared_ptr<HaloExchange>>(m, "HaloExchange")
@@ -651,6 +653,8 @@ PYBIND11_MODULE(_tz, m) {
       .def("is_direct", &HaloExchange::is_direct)
       .def("is_ipc", &HaloExchange::is_ipc)
       .def("uses_ipc", &HaloExchange::uses_ipc)
+      .def("uses_relay", &HaloExchange::uses_relay)
+      .def("relay_faces", &HaloExchange::relay_faces)
       .def("ipc_mode", &HaloExchange::ipc_mode)
       .def("put_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.put_group(d, P(s)); })
       .def("wait_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.wait_group(d, P(s)); })

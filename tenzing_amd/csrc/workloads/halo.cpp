@@ -26,6 +26,10 @@ Json HaloArgs::json() const {
   j["pitch_pad"] = pitch_pad;
   j["ghost_align"] = ghost_align;
   j["stencil"] = stencil;
+  j["relay"] = relay;
+  Json f = Json::array();
+  for (double v : relay_fracs) f.push_back(v);
+  j["relay_fracs"] = f;
   return j;
 }
 
@@ -159,6 +163,30 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   // copy-engine puts (buffers mode only): on unless TZ_IPC_COPY=0
   useCopy_ = useIpc_;
   if (const char *v = std::getenv("TZ_IPC_COPY")) useCopy_ = useCopy_ && std::atoi(v) != 0;
+
+  // relay routing through the corner peer: a 2x2x2 grid (the only single-node grid where the
+  // corner and edge-diagonal links idle while both faces of an axis share one link), ipc puts
+  // into receive buffers for every face
+  TZ_CHECK(a_.relay == "auto" || a_.relay == "off" || a_.relay == "force",
+           "relay must be auto, off or force (got " << a_.relay << ")");
+  TZ_CHECK(!a_.relay_fracs.empty(), "relay_fracs is empty");
+  for (double f : a_.relay_fracs) TZ_CHECK(f > 0.0 && f < 0.5, "relay fraction " << f << " not in (0, 0.5)");
+  bool facesIpc = true;
+  for (int i : group_dirs(1)) facesIpc = facesIpc && ipc_[i];
+  relay_ = a_.relay != "off" && a_.px == 2 && a_.py == 2 && a_.pz == 2 && useIpc_ && !ipcGrid_ && facesIpc;
+  TZ_CHECK(a_.relay != "force" || relay_,
+           "relay routing forced but needs a 2x2x2 rank grid with ipc puts in buffers mode");
+  corner_ = coord_to_rank(cx_ + 1, cy_ + 1, cz_ + 1);
+  relayOrigin_ = coord_to_rank(cx_ - 1, cy_ - 1, cz_ - 1);
+  fwdTo_.assign(dirs_.size(), -1);
+  fwdFrom_.assign(dirs_.size(), -1);
+  for (size_t i = 0; i < dirs_.size(); ++i) {
+    const Dir &d = dirs_[i];
+    // I forward what my origin (r - e) relayed for direction d to r - e + d; what travels to me
+    // in direction d was sent by me - d and forwarded by me - d + e
+    fwdTo_[i] = coord_to_rank(cx_ - 1 + d.dx, cy_ - 1 + d.dy, cz_ - 1 + d.dz);
+    fwdFrom_[i] = coord_to_rank(cx_ - d.dx + 1, cy_ - d.dy + 1, cz_ - d.dz + 1);
+  }
 }
 
 HaloExchange::~HaloExchange() {
@@ -269,9 +297,23 @@ void HaloExchange::setup(Ctrl *ctrl) {
   for (int i = 0; i < ndirs(); ++i) {
     if (direct_[i]) continue;
     if (pipe_[i] || (ipc_[i] && useCopy_ && !ipcGrid_)) send_[i] = DeviceBuffer(box_elems(i) * sizeof(double));
-    // ipc "buffers" mode needs the receive buffer too (the peer packs straight into it)
+    // ipc "buffers" mode needs the receive buffer too (the peer packs straight into it); the
+    // slack lets a relayed share start on a 128-B boundary behind the direct share
     if (pipe_[i] || (ipc_[i] && !ipcGrid_))
-      recv_[i] = DeviceBuffer(box_elems(opp_[i]) * sizeof(double));
+      recv_[i] = DeviceBuffer((box_elems(opp_[i]) + (relay_ ? 16 : 0)) * sizeof(double));
+  }
+  if (relay_) {
+    // the shares my origin relays through me: its face boxes have my boxes' shapes
+    relayBuf_.resize(ndirs());
+    for (int i : relay_faces()) {
+      size_t most = 0;
+      for (double f : a_.relay_fracs) {
+        kern::BoxDesc A, B;
+        split_box(make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_), f, A, B);
+        most = std::max(most, size_t(B.len) * B.n1 * B.n2 * B.n3);
+      }
+      relayBuf_[i] = DeviceBuffer(most * sizeof(double));
+    }
   }
   if (useIpc_) {
     // collective agreement: if any rank cannot map its peers, nobody uses IPC puts (with a
@@ -284,6 +326,18 @@ void HaloExchange::setup(Ctrl *ctrl) {
     if (!ipcReady_) {
       TZ_LOG(Warn, "ipc transport unavailable" << (why.empty() ? " on another rank" : ": " + why));
       TZ_CHECK(a_.transport != "ipc", "ipc transport requested but unavailable: " << why);
+    }
+    if (relay_) {
+      // relay routing needs more mappings (corner and edge-diagonal peers): agreed separately,
+      // so a failure there costs only the relay alternative
+      double bad = relayWhy_.empty() ? 0.0 : 1.0;
+      ctrl->allreduce_max(&bad, 1);
+      relayReady_ = ipcReady_ && bad == 0.0;
+      if (ipcReady_ && !relayReady_) {
+        TZ_LOG(Warn, "relay routing unavailable"
+                         << (relayWhy_.empty() ? " on another rank" : ": " + relayWhy_));
+        TZ_CHECK(a_.relay != "force", "relay routing forced but unavailable: " << relayWhy_);
+      }
     }
   }
   count_ = DeviceBuffer(sizeof(unsigned long long));
@@ -332,6 +386,7 @@ void HaloExchange::setup(Ctrl *ctrl) {
     TZ_HIP(hipDeviceSynchronize());
     ctrl->barrier();
     ipc_preflight(ctrl);
+    if (relay_ && ipcReady_) relay_preflight(ctrl);
   }
   TZ_HIP(hipDeviceSynchronize());
   if (useIpc_ && ipcReady_) ctrl->barrier();

@@ -170,7 +170,75 @@ private:
   std::string tag_;
 };
 
+/// relay routing stages (HaloArgs::relay): one op each, for every direction at once
+class HaloRelay : public GpuOp {
+public:
+  enum Stage { PutDirect, PutCorner, Forward, Wait, Unpack };
+  HaloRelay(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, double frac)
+      : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), faces_(h_->relay_faces()), frac_(frac) {}
+  std::string name() const override {
+    static const char *post[] = {"putd", "putc", "fwd", "wait", "unpack"};
+    return "he_rl" + std::to_string(int(std::lround(frac_ * 100))) + "_" + post[st_];
+  }
+  std::string kind() const override {
+    static const char *k[] = {"HaloRelayPutDirect", "HaloRelayPutCorner", "HaloRelayForward",
+                              "HaloRelayWait", "HaloRelayUnpack"};
+    return k[st_];
+  }
+  double bytes() const override {
+    double faces = 0, rest = 0;
+    for (int i : dirs_) {
+      const bool face = std::find(faces_.begin(), faces_.end(), i) != faces_.end();
+      (face ? faces : rest) += 8.0 * double(h_->box_elems(i));
+    }
+    if (st_ == PutDirect) return (1.0 - frac_) * faces + rest;
+    if (st_ == PutCorner || st_ == Forward) return frac_ * faces;
+    return st_ == Unpack ? 2.0 * (faces + rest) : 0.0;
+  }
+  // puts and forwards cross xGMI links (~60 GB/s effective each): the direct put uses the 3
+  // face links at once, the corner put one link, a forward 3 edge links
+  double cost_us() const override {
+    if (st_ == Wait) return 3.0;
+    if (st_ == Unpack) return copy_cost_us(bytes());
+    const double links = st_ == PutCorner ? 1.0 : 3.0;
+    return 4.0 + bytes() / links / 6.0e4;
+  }
+  void launch(void *s, Executor &) const override {
+    switch (st_) {
+    case PutDirect: h_->relay_put_direct(dirs_, frac_, s); break;
+    case PutCorner: h_->relay_put_corner(faces_, frac_, s); break;
+    case Forward: h_->relay_forward(faces_, frac_, s); break;
+    case Wait: h_->relay_wait(dirs_, faces_, s); break;
+    case Unpack: h_->relay_unpack(dirs_, faces_, frac_, s); break;
+    }
+  }
+
+private:
+  std::shared_ptr<const HaloExchange> h_;
+  Stage st_;
+  std::vector<int> dirs_, faces_;
+  double frac_;
+};
+
 } // namespace
+
+void HaloExchange::add_relay_part(Graph &g, const std::vector<int> &remote, double frac) {
+  // the corner put feeds the corner peer's forward, so my forward is issued after my corner
+  // put (never ahead of it on a stream, which could deadlock every rank's symmetric
+  // schedule); the direct put runs beside both; the wait needs the direct shares and what my
+  // forwarders relayed, then the unpack hands out the credits
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  auto mk = [&](HaloRelay::Stage st) { return std::make_shared<HaloRelay>(self, st, remote, frac); };
+  auto putd = mk(HaloRelay::PutDirect), putc = mk(HaloRelay::PutCorner), fwd = mk(HaloRelay::Forward),
+       w = mk(HaloRelay::Wait), u = mk(HaloRelay::Unpack);
+  g.start_then(putd);
+  g.start_then(putc);
+  g.then(putc, fwd);
+  g.then(putd, w);
+  g.then(fwd, w);
+  g.then(w, u);
+  g.then_finish(u);
+}
 
 void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, int via) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
@@ -405,10 +473,22 @@ void HaloExchange::add_exchange(Graph &g) {
     add_ipc_part(*gr, remote, kViaCopy);
     alts.push_back(std::make_shared<StaticCompoundOp>("he_via_sdma", gr));
   }
+  if (uses_relay()) {
+    if (a_.relay == "force") alts.clear();
+    for (double f : a_.relay_fracs) {
+      auto gr = std::make_shared<Graph>();
+      add_relay_part(*gr, remote, f);
+      alts.push_back(std::make_shared<StaticCompoundOp>(
+          "he_via_relay" + std::to_string(int(std::lround(f * 100))), gr));
+    }
+  }
   if (alts.size() > 1) {
     auto c = std::make_shared<StaticChoiceOp>("he_remote", alts);
     g.start_then(c);
     g.then_finish(c);
+  } else if (a_.relay == "force") {
+    g.start_then(alts.front());
+    g.then_finish(alts.front());
   } else if (ipc) {
     add_ipc_part(g, remote, kViaPut);
   } else {

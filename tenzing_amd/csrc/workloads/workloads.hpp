@@ -125,6 +125,16 @@ struct HaloArgs {
   // search may update the ghost-free interior while ghosts are in flight and the one-cell
   // boundary shell afterwards, or the whole domain after the exchange (a ChoiceOp)
   bool stencil = false;
+  // two-hop routing of part of every face through the corner peer (2x2x2 rank grid, IPC
+  // "buffers" mode). Each GPU has one xGMI link per peer, and in a 2x2x2 grid both faces of an
+  // axis go to the same peer, so the 3 face links carry almost all bytes while the 3
+  // edge-diagonal links and the corner link idle. A relayed share f of each face goes
+  // r -> r+(1,1,1) (corner link) -> r+d (that rank's edge-diagonal link): every link then
+  // carries at most 0.75 of a face pair for f = 0.25 with overlapped forwarding, or 0.8 for
+  // f = 0.2 with forwarding after arrival (what is built). "auto": offered to the search as a
+  // transport alternative when applicable; "off"; "force": the only remote transport (tests)
+  std::string relay = "auto";
+  std::vector<double> relay_fracs = {0.15, 0.2}; // relayed shares offered (a ChoiceOp)
   int device = -1;
   Json json() const;
 };
@@ -229,6 +239,26 @@ public:
   /// returns each credit right after the arrival, so ghosts stay valid only until the peer's
   /// next put: stencil mode (which reads them after the exchange) always uses "buffers".
   std::string ipc_mode() const { return useIpc_ ? (ipcGrid_ ? "grid" : "buffers") : ""; }
+  /// relay routing (see HaloArgs::relay) is available: rank grid 2x2x2, ipc buffers mode
+  bool uses_relay() const { return relay_ && useIpc_ && (relayReady_ || !ready()); }
+  /// relay routing, direct link: put the first (1 - f) share of every face of `faces` and the
+  /// whole box of every other direction of `dirs` into the neighbours' receive buffers
+  void relay_put_direct(const std::vector<int> &dirs, double frac, void *stream) const;
+  /// relay routing, first hop: put the last share f of every face of `faces` into the corner
+  /// peer's relay buffers (one launch, arrival signals in its relay slots)
+  void relay_put_corner(const std::vector<int> &faces, double frac, void *stream) const;
+  /// relay routing, second hop: wait for my corner-origin's relayed shares, copy them into
+  /// their final receivers' receive buffers behind the direct share, signal those receivers and
+  /// return the relay credits to the origin
+  void relay_forward(const std::vector<int> &faces, double frac, void *stream) const;
+  /// relay routing: wait for every direct put of `dirs` and every forwarded share of `faces`
+  void relay_wait(const std::vector<int> &dirs, const std::vector<int> &faces, void *stream) const;
+  /// relay routing: unpack `dirs` (faces as direct + relayed sub-boxes) and return the credits
+  /// of the direct senders and of the forwarders
+  void relay_unpack(const std::vector<int> &dirs, const std::vector<int> &faces, double frac,
+                    void *stream) const;
+  /// the face directions among the remote ones (what relay routing splits)
+  std::vector<int> relay_faces() const;
   /// direct transport: move the interior slab facing each direction of `dirs` straight into
   /// the neighbour's ghost region on the opposite side (one launch)
   void direct_group(const std::vector<int> &dirs, void *stream) const;
@@ -243,6 +273,7 @@ private:
   void add_structure(Graph &g, const std::vector<int> &dirs, int via,
                      const std::string &pre); // fuse mode over `dirs`
   void add_ipc_part(Graph &g, const std::vector<int> &remote, int via);
+  void add_relay_part(Graph &g, const std::vector<int> &remote, double frac);
   void check_pipelined(int i) const;
   std::string setup_ipc(Ctrl *ctrl); // "" on success, else why IPC cannot be used
   void ipc_preflight(Ctrl *ctrl);    // one verified exchange; disables IPC collectively on failure
@@ -257,9 +288,28 @@ private:
   bool ipcReady_ = false;
   bool useCopy_ = false; // copy-engine puts offered (buffers mode)
   // ipc transport state
-  void *flags_ = nullptr;            // arrival counter per direction (uncached, IPC-exported)
+  // counters per direction, uncached and IPC-exported, in kSlotSets sections of ndirs():
+  // arrivals | credits | relay arrivals | relay credits | forwarded arrivals | forward credits
+  void *flags_ = nullptr;
+  static constexpr int kSlotSets = 6;
   DeviceBuffer expected_, done_, err_;
   DeviceBuffer sent_; // per direction: puts issued so far (credit wait bookkeeping)
+  // relay bookkeeping: relay arrivals expected | relay puts issued | forwarded arrivals
+  // expected | forwards issued (4 x ndirs())
+  DeviceBuffer relayBook_;
+  bool relay_ = false, relayReady_ = false;
+  std::string relayWhy_; // why this rank could not map the relay peers ("" = fine)
+  int corner_ = -1;                          // r + (1,1,1): where my relayed shares go
+  std::vector<DeviceBuffer> relayBuf_;       // per face direction: shares relayed through me
+  std::vector<void *> peerRelay_;            // per face direction: the corner peer's relay buffer
+  std::vector<void *> peerFwdRecv_;          // per face direction: final receiver's buffer
+  std::vector<int> fwdTo_, fwdFrom_;         // per direction: rank I forward to / forwards to me
+  int relayOrigin_ = -1;                     // r - (1,1,1): whose shares I forward
+  /// split a box (and its dense buffer) into the direct share A and the relayed share B along
+  /// its largest dimension; B holds round(frac * n) rows (at least 1)
+  void split_box(const kern::BoxDesc &b, double frac, kern::BoxDesc &A, kern::BoxDesc &B) const;
+  void relay_preflight(Ctrl *ctrl);
+  unsigned long long *peer_slot(int rank, int set, int i) const;
   std::vector<unsigned long long *> credit_ptrs(const std::vector<int> &dirs) const;
   const RcclComm &comm_for(int streamIdx, int dir) const;
   void widen_to_sectors(int ghostDx, kern::MoveDesc &m) const;

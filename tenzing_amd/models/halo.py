@@ -31,6 +31,10 @@ class HaloConfig:
     rank_grid: tuple = ()  # (px, py, pz); () = reference rule (prime factors, smallest dim first)
     ghost_align: int = 16  # x ghost runs aligned to 8 (sector) / 16 (line) elements, 0 = off
     stencil: bool = False  # add a 7-point stencil (interior beside / shell after the exchange)
+    # two-hop routing of a share of every face through the corner peer (2x2x2 rank grid, ipc
+    # receive buffers): "auto" offers it to the search, "off", "force" (only transport)
+    relay: str = "auto"
+    relay_fracs: tuple = (0.15, 0.2)  # relayed shares offered (ChoiceOp)
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":
         a = _tz.HaloArgs()
@@ -45,6 +49,8 @@ class HaloConfig:
         a.pitch_pad = self.pitch_pad
         a.ghost_align = self.ghost_align
         a.stencil = self.stencil
+        a.relay = self.relay
+        a.relay_fracs = [float(f) for f in self.relay_fracs]
         if self.rank_grid:
             a.px, a.py, a.pz = (int(v) for v in self.rank_grid)
         a.rank, a.size, a.device = rank, size, device

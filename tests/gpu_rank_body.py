@@ -30,8 +30,10 @@ def main():
         for fuse in fuses:
             say("build_halo", n, fuse)
             stencil = bool(os.environ.get("TZ_TEST_STENCIL"))
+            relay = os.environ.get("TZ_TEST_RELAY", "auto")
             halo, g = build_halo(HaloConfig(n=n, neighbors=26, order="qxyz", transport="ipc",
-                                            fuse=fuse, stencil=stencil), ctrl, dev)
+                                            fuse=fuse, stencil=stencil, relay=relay), ctrl, dev)
+            out["relay_ready"] = halo.uses_relay()
             say("built")
             rt = tz.HipRuntime(device=dev, n_streams=3, watchdog_s=60.0)
             for mode in [tz.ExecMode.Eager if m == "eager" else tz.ExecMode.Graph for m in modes]:
@@ -63,7 +65,8 @@ def main():
                                     bad2=int(bad2), err=halo.ipc_errors(),
                                     transport=halo.transport(), ipc_mode=halo.ipc_mode(),
                                     copyput=any(o.name.startswith("he_copyput_")
-                                                for o in seq.ops())))
+                                                for o in seq.ops()),
+                                    relay=any(o.name.startswith("he_rl") for o in seq.ops())))
             if os.environ.get("TZ_TEST_NO_MCTS"):
                 continue
             # a short collective search over ipc schedules

@@ -76,6 +76,21 @@ def test_ipc_halo_loopback(gpu, world, mode):
             assert used == (mode == "buffers"), [run["copyput"] for run in r["runs"]]
 
 
+def test_relay_routing_loopback(gpu):
+    """the 2x2x2 grid with every remote direction through relay routing (a share of each face
+    via the corner peer, forwarded over its edge-diagonal link): every ghost right on all 8
+    ranks, eager and as hipGraphs, over repeated exchanges, and in a collective search"""
+    extra = {"TZ_IPC_GRID": "0", "TZ_TEST_N": "24", "TZ_TEST_FUSES": "choice",
+             "TZ_TEST_RELAY": "force"}
+    res = _launch("ipc_halo", 8, extra_env=extra)
+    for r in res:
+        assert r["relay_ready"] and r["mcts_err"] == [0]
+        assert r["mcts"] == ([4] if r["rank"] == 0 else [0])
+        for run in r["runs"]:
+            assert run["relay"], run
+            assert run["bad1"] == 0 and run["bad2"] == 0 and run["err"] == 0, run
+
+
 def test_bench_two_ranks_loopback(gpu, tmp_path):
     """the driver's multi-GPU bench flow (torchrun, one process per rank, collective search,
     best-schedule broadcast, device-side verification, eager + hipGraph timing, max over ranks)

@@ -105,6 +105,10 @@ def test_ipc_transport_graph(tz, fuse, size, mode, monkeypatch):
     seen = set()
     for seed in range(12):
         names = _names(tz, g, seed)
+        if any(n.startswith("he_rl") for n in names):
+            # relay routing (2x2x2, buffers mode): checked in test_relay_routing_graph
+            seen.add("relay")
+            continue
         # buffers mode also offers copy-engine puts (pack locally, SDMA copy, signal): a
         # ChoiceOp between the two, whose op names differ ("cp_")
         v = "cp_" if "he_wait_cp_remote" in names else ""
@@ -121,7 +125,75 @@ def test_ipc_transport_graph(tz, fuse, size, mode, monkeypatch):
             assert [names[k] for k in unpacks] == [f"he_unpack_{v}remote"] and unpacks[0] > w
         if fuse == "none":
             assert len(puts) == n_ipc
+    seen.discard("relay")
     assert seen == ({""} if mode == "grid" else {"", "cp_"})
+
+
+@pytest.mark.parametrize("transport", ["auto", "ipc"])
+def test_relay_routing_graph(tz, transport, monkeypatch):
+    """2x2x2 grid, ipc receive buffers: a share of every face can travel through the corner
+    peer. Each relay alternative is putd / putc -> fwd -> wait -> unpack, the forward never
+    ahead of the rank's own corner put; every rank builds the same names"""
+    monkeypatch.setenv("TZ_IPC_GRID", "0")
+    from tenzing_amd.models import HaloConfig
+
+    graphs, hs = [], []
+    for r in range(8):
+        h = tz._tz.HaloExchange(HaloConfig(n=16, neighbors=26, order="qxyz", fuse="choice",
+                                           transport=transport).args(r, 8, -1))
+        g = tz.Graph()
+        h.add_to_graph(g)
+        hs.append(h)
+        graphs.append(g)
+    h, g = hs[0], graphs[0]
+    assert h.uses_relay() and len(h.relay_faces()) == 6
+    assert g.contains("he_remote")
+    fracs = set()
+    for seed in range(60):
+        seq = tz.random_rollout(tz.State(g, tz.Platform(3)), seed)
+        names = [o.name for o in seq.ops() if isinstance(o, tz._tz.BoundGpuOp)]
+        rl = [n for n in names if n.startswith("he_rl")]
+        if not rl:
+            continue
+        t = rl[0][:len("he_rlNN")]
+        fracs.add(t)
+        k = {st: names.index(f"{t}_{st}") for st in ("putd", "putc", "fwd", "wait", "unpack")}
+        assert k["putc"] < k["fwd"] < k["wait"] and k["putd"] < k["wait"] < k["unpack"]
+        assert len(rl) == 5
+        assert not any(n.startswith(("he_put_", "he_copyput_", "he_shift_")) for n in names)
+        js = seq.json(True)
+        for other in graphs[1:]:
+            tz.OpIndex(other).sequence_from_json(js)
+    assert fracs == {"he_rl15", "he_rl20"}
+    # forced: the only remote transport
+    a = HaloConfig(n=16, neighbors=6, order="qxyz", fuse="choice", transport="ipc", relay="force",
+                   relay_fracs=(0.25,)).args(3, 8, -1)
+    hf = tz._tz.HaloExchange(a)
+    gf = tz.Graph()
+    hf.add_to_graph(gf)
+    assert hf.relay_faces() == list(range(6))
+    for seed in range(5):
+        names = [o.name for o in tz.random_rollout(tz.State(gf, tz.Platform(2)), seed).ops()
+                 if isinstance(o, tz._tz.BoundGpuOp)]
+        assert sorted(names) == sorted(f"he_rl25_{st}" for st in
+                                       ("putd", "putc", "fwd", "wait", "unpack"))
+
+
+def test_relay_routing_needs_2x2x2_and_buffers(tz, monkeypatch):
+    from tenzing_amd.models import HaloConfig
+
+    monkeypatch.setenv("TZ_IPC_GRID", "0")
+    for size in (2, 4):
+        h = tz._tz.HaloExchange(HaloConfig(n=16, transport="ipc").args(0, size, -1))
+        assert not h.uses_relay()
+        with pytest.raises(Exception, match="relay"):
+            tz._tz.HaloExchange(HaloConfig(n=16, transport="ipc", relay="force").args(0, size, -1))
+    h = tz._tz.HaloExchange(HaloConfig(n=16, transport="ipc", relay="off").args(0, 8, -1))
+    assert not h.uses_relay()
+    monkeypatch.setenv("TZ_IPC_GRID", "1")
+    assert not tz._tz.HaloExchange(HaloConfig(n=16, transport="ipc").args(0, 8, -1)).uses_relay()
+    with pytest.raises(Exception, match="relay"):
+        tz._tz.HaloExchange(HaloConfig(n=16, relay_fracs=(0.6,)).args(0, 8, -1))
 
 
 @pytest.mark.parametrize("grid", [(1, 1, 8), (8, 1, 1), (2, 4, 1)])
