@@ -69,7 +69,9 @@ def main() -> int:
                          "search may update the interior while ghosts are in flight")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
-    ap.add_argument("--mcts-iters", type=int, default=40)
+    ap.add_argument("--mcts-iters", type=int, default=0,
+                    help="MCTS iterations (0: 40 on one rank; 120 on several, where the tree "
+                         "adds transport alternatives: RCCL, IPC kernel / SDMA puts, relays)")
     ap.add_argument("--search-budget-s", type=float, default=120.0)
     # per candidate: 6 measurements of >= 2 ms each; the 4 best are re-measured interleaved
     # (--rerank) before the final timing. 20 x 4 ms, 10 x 3 ms, 8 x 2 ms and 5 x 1.5 ms all find
@@ -122,7 +124,7 @@ def main() -> int:
     setup_s = time.time() - t_setup
 
     opts = tz.MctsOpts()
-    opts.n_iters = args.mcts_iters
+    opts.n_iters = args.mcts_iters if args.mcts_iters > 0 else (40 if world == 1 else 120)
     opts.time_budget_s = args.search_budget_s
     opts.strategy = args.strategy
     opts.seed = args.seed
@@ -238,7 +240,7 @@ def main() -> int:
 
     names = [o.name for o in best.ops()]
     via = [t for t, key in (("direct", "he_direct_"), ("rccl", "he_shift_"), ("ipc", "he_put_"),
-                            ("sdma", "he_copyput_"))
+                            ("sdma", "he_copyput_"), ("relay", "he_rl"))
            if any(n.startswith(key) for n in names)]
     if rank == 0:
         bytes_total = halo.exchange_bytes() * world
@@ -293,6 +295,7 @@ def main() -> int:
             "stencil_mode": (("split" if "st_interior" in names else "after")
                              if args.stencil else None),
             "ipc_mode": halo.ipc_mode() or None,
+            "relay_offered": halo.uses_relay(),
         }
         print(json.dumps(out), flush=True)
     return 0 if bad == 0 else 3

@@ -173,16 +173,16 @@ private:
 /// relay routing stages (HaloArgs::relay): one op each, for every direction at once
 class HaloRelay : public GpuOp {
 public:
-  enum Stage { PutDirect, PutCorner, Forward, Wait, Unpack };
+  enum Stage { PutDirect, PutCorner, Forward, Wait, Unpack, ForwardCopy };
   HaloRelay(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, double frac)
       : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), faces_(h_->relay_faces()), frac_(frac) {}
   std::string name() const override {
-    static const char *post[] = {"putd", "putc", "fwd", "wait", "unpack"};
+    static const char *post[] = {"putd", "putc", "fwd", "wait", "unpack", "fwdcp"};
     return "he_rl" + std::to_string(int(std::lround(frac_ * 100))) + "_" + post[st_];
   }
   std::string kind() const override {
     static const char *k[] = {"HaloRelayPutDirect", "HaloRelayPutCorner", "HaloRelayForward",
-                              "HaloRelayWait", "HaloRelayUnpack"};
+                              "HaloRelayWait", "HaloRelayUnpack", "HaloRelayForwardCopy"};
     return k[st_];
   }
   double bytes() const override {
@@ -192,7 +192,7 @@ public:
       (face ? faces : rest) += 8.0 * double(h_->box_elems(i));
     }
     if (st_ == PutDirect) return (1.0 - frac_) * faces + rest;
-    if (st_ == PutCorner || st_ == Forward) return frac_ * faces;
+    if (st_ == PutCorner || st_ == Forward || st_ == ForwardCopy) return frac_ * faces;
     return st_ == Unpack ? 2.0 * (faces + rest) : 0.0;
   }
   // puts and forwards cross xGMI links (~60 GB/s effective each): the direct put uses the 3
@@ -208,6 +208,7 @@ public:
     case PutDirect: h_->relay_put_direct(dirs_, frac_, s); break;
     case PutCorner: h_->relay_put_corner(faces_, frac_, s); break;
     case Forward: h_->relay_forward(faces_, frac_, s); break;
+    case ForwardCopy: h_->relay_forward(faces_, frac_, s, /*sdma=*/true); break;
     case Wait: h_->relay_wait(dirs_, faces_, s); break;
     case Unpack: h_->relay_unpack(dirs_, faces_, frac_, s); break;
     }
@@ -229,8 +230,12 @@ void HaloExchange::add_relay_part(Graph &g, const std::vector<int> &remote, doub
   // forwarders relayed, then the unpack hands out the credits
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   auto mk = [&](HaloRelay::Stage st) { return std::make_shared<HaloRelay>(self, st, remote, frac); };
-  auto putd = mk(HaloRelay::PutDirect), putc = mk(HaloRelay::PutCorner), fwd = mk(HaloRelay::Forward),
-       w = mk(HaloRelay::Wait), u = mk(HaloRelay::Unpack);
+  auto putd = mk(HaloRelay::PutDirect), putc = mk(HaloRelay::PutCorner), w = mk(HaloRelay::Wait),
+       u = mk(HaloRelay::Unpack);
+  // the forward copies by kernel or on the copy engines (CUs left to the direct put)
+  auto fwd = std::make_shared<StaticChoiceOp>(
+      "he_rl" + std::to_string(int(std::lround(frac * 100))) + "_forward",
+      std::vector<OpPtr>{mk(HaloRelay::Forward), mk(HaloRelay::ForwardCopy)});
   g.start_then(putd);
   g.start_then(putc);
   g.then(putc, fwd);

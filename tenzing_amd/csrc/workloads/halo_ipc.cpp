@@ -367,7 +367,8 @@ void HaloExchange::relay_put_corner(const std::vector<int> &faces, double frac, 
   kern::box_pack_many_signal(grid(), bs.data(), int(bs.size()), sig, stream);
 }
 
-void HaloExchange::relay_forward(const std::vector<int> &faces, double frac, void *stream) const {
+void HaloExchange::relay_forward(const std::vector<int> &faces, double frac, void *stream,
+                                 bool sdma) const {
   TZ_CHECK(ready() && relayReady_, "relay routing not set up");
   TZ_CHECK(!faces.empty() && faces.size() <= size_t(kern::kMaxBoxes), "bad relay face group");
   const int nd = ndirs();
@@ -406,7 +407,15 @@ void HaloExchange::relay_forward(const std::vector<int> &faces, double frac, voi
     sig.flag[k] = peer_slot(fwdTo_[i], 4, i);
     credits.push_back(peer_slot(relayOrigin_, 3, i));
   }
-  kern::box_move_many_signal(ms.data(), int(ms.size()), sig, stream);
+  if (!sdma) {
+    kern::box_move_many_signal(ms.data(), int(ms.size()), sig, stream);
+  } else {
+    for (const kern::MoveDesc &m : ms)
+      TZ_HIP(hipMemcpyAsync(m.dst + m.dst_off, m.src, size_t(m.len) * sizeof(double),
+                            hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    // arrivals are published after the copies (stream order), like copy-engine puts
+    for (size_t k = 0; k < faces.size(); ++k) credits.push_back(sig.flag[k]);
+  }
   // the relay buffers are free again: the origin may put its next shares
   kern::ipc_signal(credits.data(), int(credits.size()), stream);
 }

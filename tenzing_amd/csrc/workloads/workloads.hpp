@@ -249,8 +249,9 @@ public:
   void relay_put_corner(const std::vector<int> &faces, double frac, void *stream) const;
   /// relay routing, second hop: wait for my corner-origin's relayed shares, copy them into
   /// their final receivers' receive buffers behind the direct share, signal those receivers and
-  /// return the relay credits to the origin
-  void relay_forward(const std::vector<int> &faces, double frac, void *stream) const;
+  /// return the relay credits to the origin. `sdma`: the copies run on the copy engines
+  /// (hipMemcpyAsync) instead of a kernel, leaving the CUs to the concurrent direct put
+  void relay_forward(const std::vector<int> &faces, double frac, void *stream, bool sdma = false) const;
   /// relay routing: wait for every direct put of `dirs` and every forwarded share of `faces`
   void relay_wait(const std::vector<int> &dirs, const std::vector<int> &faces, void *stream) const;
   /// relay routing: unpack `dirs` (faces as direct + relayed sub-boxes) and return the credits

@@ -66,7 +66,8 @@ def main():
                                     transport=halo.transport(), ipc_mode=halo.ipc_mode(),
                                     copyput=any(o.name.startswith("he_copyput_")
                                                 for o in seq.ops()),
-                                    relay=any(o.name.startswith("he_rl") for o in seq.ops())))
+                                    relay=any(o.name.startswith("he_rl") for o in seq.ops()),
+                                    relay_sdma=any(o.name.endswith("_fwdcp") for o in seq.ops())))
             if os.environ.get("TZ_TEST_NO_MCTS"):
                 continue
             # a short collective search over ipc schedules
