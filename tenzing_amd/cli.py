@@ -25,7 +25,8 @@ def _build_workload(a, ctrl, device, setup):
 
     hc = HaloConfig(n=a.halo_n, nq=a.nq, ghost=a.ghost, neighbors=a.neighbors, order=a.order,
                     fuse=a.fuse, transport=a.transport, stencil=a.stencil)
-    sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport)
+    sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport,
+                    matrix=a.spmv_matrix)
     if a.workload == "halo":
         h, g = build_halo(hc, ctrl, device, setup)
         return g, {"halo": h}
@@ -204,6 +205,8 @@ def main(argv=None) -> int:
     s.add_argument("--stencil", action="store_true",
                    help="halo: add the 7-point stencil (interior beside / shell after the exchange)")
     s.add_argument("--spmv-m", type=int, default=150_000)
+    s.add_argument("--spmv-matrix", default="",
+                   help="Matrix Market file (square) instead of the random band matrix")
     s.add_argument("--spmv-form", default="choice", choices=["choice", "split", "accum"])
     s.add_argument("--spmv-transport", default="auto", choices=["auto", "rccl", "ipc"])
     s.set_defaults(fn=cmd_search)

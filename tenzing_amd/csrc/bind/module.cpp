@@ -664,6 +664,7 @@ PYBIND11_MODULE(_tz, m) {
 
   py::class_<SpmvArgs>(m, "SpmvArgs")
       .def(py::init<>())
+      .def_readwrite("matrix", &SpmvArgs::matrix)
       .def_readwrite("m", &SpmvArgs::m)
       .def_readwrite("bw", &SpmvArgs::bw)
       .def_readwrite("nnz", &SpmvArgs::nnz)
@@ -702,6 +703,24 @@ PYBIND11_MODULE(_tz, m) {
     CsrHost a = random_band_matrix(n, bw, nnz, seed);
     return py::make_tuple(a.rowPtr, a.colInd, a.val);
   });
+  m.def("read_matrix_market", [](const std::string &path) {
+    CsrHost a = read_matrix_market(path);
+    return py::make_tuple(a.rows, a.cols, a.rowPtr, a.colInd, a.val);
+  }, py::arg("path"));
+  m.def("write_matrix_market", [](int64_t rows, int64_t cols, std::vector<int32_t> rowPtr,
+                                  std::vector<int32_t> colInd, std::vector<float> val,
+                                  const std::string &path) {
+    CsrHost a;
+    a.rows = rows;
+    a.cols = cols;
+    a.rowPtr = std::move(rowPtr);
+    a.colInd = std::move(colInd);
+    a.val = std::move(val);
+    TZ_CHECK(int64_t(a.rowPtr.size()) == rows + 1 && a.colInd.size() == a.val.size() &&
+                 int64_t(a.colInd.size()) == int64_t(a.rowPtr.back()),
+             "inconsistent CSR arrays");
+    write_matrix_market(a, path);
+  }, py::arg("rows"), py::arg("cols"), py::arg("row_ptr"), py::arg("col_ind"), py::arg("val"), py::arg("path"));
   m.def("row_partition", &row_partition);
 
   // ------------------------------------------------------------------ raw kernels

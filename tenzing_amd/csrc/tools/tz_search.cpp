@@ -52,7 +52,7 @@ void usage() {
          "  [--target-secs S] [--mode eager|graph] [--sim] [--seed N] [--no-expand-rollout]\n"
          "  [--halo-n N] [--nq N] [--ghost N] [--neighbors 6|26] [--order xyzq|qxyz]\n"
          "  [--fuse none|pack|all|groups|choice] [--graph-unroll K]\n"
-         "  [--transport auto|rccl|ipc|copy|direct] [--rank-grid PXxPYxPZ] [--spmv-m N]\n"
+         "  [--transport auto|rccl|ipc|copy|direct] [--rank-grid PXxPYxPZ] [--spmv-m N] [--spmv-matrix F.mtx]\n"
          "  [--spmv-form choice|split|accum] [--spmv-transport auto|rccl|ipc]\n"
          "  [--spmv-library adaptive|lrb|rowsplit|''] [--cu-partition] [--stencil] [--max-seqs N]\n"
          "  [--rdzv-file PATH]\n"
@@ -142,6 +142,7 @@ int main(int argc, char **argv) {
     if (workload == "spmv" || workload == "halo+spmv") {
       SpmvArgs s;
       s.m = int64_t(a.num("spmv-m", 150000));
+      s.matrix = a.get("spmv-matrix", "");
       s.rank = rank;
       s.size = size;
       s.prefix = workload == "halo+spmv" ? "spmv_" : "";

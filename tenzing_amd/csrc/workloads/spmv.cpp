@@ -10,8 +10,11 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
+#include <fstream>
 #include <random>
+#include <sstream>
 
 namespace tz {
 
@@ -28,6 +31,7 @@ Json SpmvArgs::json() const {
   j["form"] = form;
   j["library"] = library;
   j["transport"] = transport;
+  j["matrix"] = matrix;
   return j;
 }
 
@@ -59,6 +63,80 @@ CsrHost random_band_matrix(int64_t n, int64_t bw, int64_t nnz, uint64_t seed) {
   }
   for (int64_t r = 0; r < n; ++r) A.rowPtr[size_t(r + 1)] += A.rowPtr[size_t(r)];
   return A;
+}
+
+CsrHost read_matrix_market(const std::string &path) {
+  std::ifstream f(path);
+  TZ_CHECK(f, "cannot open " << path);
+  std::string line;
+  TZ_CHECK(std::getline(f, line), path << ": empty file");
+  std::istringstream hs(line);
+  std::string banner, object, format, field, symmetry;
+  hs >> banner >> object >> format >> field >> symmetry;
+  auto lower = [](std::string v) {
+    std::transform(v.begin(), v.end(), v.begin(), [](unsigned char c) { return char(std::tolower(c)); });
+    return v;
+  };
+  object = lower(object), format = lower(format), field = lower(field), symmetry = lower(symmetry);
+  TZ_CHECK(banner == "%%MatrixMarket" && object == "matrix", path << ": not a Matrix Market matrix");
+  TZ_CHECK(format == "coordinate", path << ": only coordinate (sparse) format is supported");
+  TZ_CHECK(field == "real" || field == "integer" || field == "pattern" || field == "double",
+           path << ": unsupported field " << field);
+  TZ_CHECK(symmetry == "general" || symmetry == "symmetric" || symmetry == "skew-symmetric",
+           path << ": unsupported symmetry " << symmetry);
+  while (std::getline(f, line))
+    if (!line.empty() && line[0] != '%') break;
+  int64_t rows = 0, cols = 0, entries = 0;
+  {
+    std::istringstream ss(line);
+    TZ_CHECK(ss >> rows >> cols >> entries, path << ": bad size line");
+  }
+  TZ_CHECK(rows > 0 && cols > 0 && entries >= 0 && rows < (int64_t(1) << 31) && cols < (int64_t(1) << 31),
+           path << ": bad dimensions");
+  std::vector<std::pair<int64_t, float>> e; // (row * cols + col, value)
+  e.reserve(size_t(entries) * (symmetry == "general" ? 1 : 2));
+  for (int64_t k = 0; k < entries; ++k) {
+    do {
+      TZ_CHECK(std::getline(f, line), path << ": " << k << " of " << entries << " entries");
+    } while (line.empty() || line[0] == '%');
+    std::istringstream ss(line);
+    int64_t r = 0, c = 0;
+    double v = 1.0;
+    TZ_CHECK(ss >> r >> c, path << ": bad entry line " << line);
+    if (field != "pattern") TZ_CHECK(ss >> v, path << ": entry without a value: " << line);
+    TZ_CHECK(r >= 1 && r <= rows && c >= 1 && c <= cols, path << ": entry out of range: " << line);
+    --r, --c;
+    e.emplace_back(r * cols + c, float(v));
+    if (symmetry != "general" && r != c) e.emplace_back(c * cols + r, float(symmetry == "symmetric" ? v : -v));
+  }
+  std::sort(e.begin(), e.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+  CsrHost A;
+  A.rows = rows;
+  A.cols = cols;
+  A.rowPtr.assign(size_t(rows + 1), 0);
+  for (size_t k = 0; k < e.size(); ++k) {
+    if (k > 0 && e[k].first == e[k - 1].first) {
+      A.val.back() += e[k].second; // duplicates add up
+      continue;
+    }
+    A.rowPtr[size_t(e[k].first / cols + 1)]++;
+    A.colInd.push_back(int32_t(e[k].first % cols));
+    A.val.push_back(e[k].second);
+  }
+  for (int64_t r = 0; r < rows; ++r) A.rowPtr[size_t(r + 1)] += A.rowPtr[size_t(r)];
+  return A;
+}
+
+void write_matrix_market(const CsrHost &A, const std::string &path) {
+  std::ofstream f(path);
+  TZ_CHECK(f, "cannot write " << path);
+  f << "%%MatrixMarket matrix coordinate real general\n";
+  f << A.rows << " " << A.cols << " " << A.nnz() << "\n";
+  f.precision(9);
+  for (int64_t r = 0; r < A.rows; ++r)
+    for (int32_t j = A.rowPtr[size_t(r)]; j < A.rowPtr[size_t(r + 1)]; ++j)
+      f << r + 1 << " " << A.colInd[size_t(j)] + 1 << " " << A.val[size_t(j)] << "\n";
+  TZ_CHECK(f.good(), "write to " << path << " failed");
 }
 
 std::pair<int64_t, int64_t> row_partition(int64_t n, int rank, int size) {
@@ -204,10 +282,21 @@ private:
 
 DistSpmv::DistSpmv(SpmvArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.size >= 1 && a_.rank >= 0 && a_.rank < a_.size, "bad rank/size");
+  CsrHost A;
+  if (!a_.matrix.empty()) {
+    A = read_matrix_market(a_.matrix);
+    TZ_CHECK(A.rows == A.cols, a_.matrix << ": the SpMV workload needs a square matrix (x is "
+                                          "partitioned like the rows), got " << A.rows << " x " << A.cols);
+    a_.m = A.rows;
+    a_.nnz = A.nnz();
+    a_.bw = 0;
+  } else {
+    if (a_.bw <= 0) a_.bw = std::max<int64_t>(1, a_.m / a_.size);
+    if (a_.nnz <= 0) a_.nnz = 10 * a_.m;
+    A = random_band_matrix(a_.m, a_.bw, a_.nnz, a_.seed);
+  }
   const int64_t n = a_.m;
-  if (a_.bw <= 0) a_.bw = std::max<int64_t>(1, n / a_.size);
-  if (a_.nnz <= 0) a_.nnz = 10 * n;
-  const CsrHost A = random_band_matrix(n, a_.bw, a_.nnz, a_.seed);
+  TZ_CHECK(n >= a_.size, "fewer matrix rows (" << n << ") than ranks (" << a_.size << ")");
   std::tie(r0_, r1_) = row_partition(n, a_.rank, a_.size);
 
   // split my rows into local (own x) and remote (others' x) blocks

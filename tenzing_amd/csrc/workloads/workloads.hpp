@@ -340,10 +340,20 @@ struct CsrHost {
 /// deterministic random band matrix: `nnz` entries with |row - col| < bw, values in [-1,1)
 /// (reference csr_mat.hpp:334-370 uses rand() and all-ones values)
 CsrHost random_band_matrix(int64_t n, int64_t bw, int64_t nnz, uint64_t seed);
+/// Matrix Market coordinate file -> CSR (real / integer / pattern values; general, symmetric
+/// or skew-symmetric storage; 1-based indices; duplicate entries summed). The reference vendors
+/// an MTX reader (thirdparty/cwpearson/mm) but never calls it; here the SpMV workload can run
+/// on any square matrix from a file (SpmvArgs::matrix).
+CsrHost read_matrix_market(const std::string &path);
+/// write A as "matrix coordinate real general" (round trips through read_matrix_market)
+void write_matrix_market(const CsrHost &A, const std::string &path);
 /// rows [r0, r1) owned by rank (remainder to low ranks, reference partition.hpp:21-76)
 std::pair<int64_t, int64_t> row_partition(int64_t n, int rank, int size);
 
 struct SpmvArgs {
+  // Matrix Market file of a square matrix to use instead of the random band matrix ("" = the
+  // reference's random band matrix of m rows); every rank reads it (no setup communication)
+  std::string matrix = "";
   int64_t m = 150000;
   int64_t bw = 0;  // 0 = m / size (reference spmv_run_strategy.cuh:67)
   int64_t nnz = 0; // 0 = 10 * m

@@ -23,6 +23,7 @@ class SpmvConfig:
     library: str = "adaptive"   # rocSPARSE CSR algorithm added to the kernel ChoiceOp ("" = none)
     transport: str = "auto"     # x halo between ranks: rccl | ipc | auto (ChoiceOp over both)
     prefix: str = ""
+    matrix: str = ""            # Matrix Market file of a square matrix instead of the band matrix
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.SpmvArgs":
         a = _tz.SpmvArgs()
@@ -31,6 +32,7 @@ class SpmvConfig:
         a.form = self.form
         a.library = self.library
         a.transport = self.transport
+        a.matrix = self.matrix
         a.rank, a.size, a.device = rank, size, device
         return a
 

@@ -355,3 +355,32 @@ def test_halo_stencil_mode_correct(tz, gpu, order):
             assert halo.check_grid() == 0
             assert halo.check_stencil() == 0
     assert kinds == {True, False}
+
+
+def test_spmv_workload_from_matrix_market_file(tz, gpu, tmp_path):
+    """a square matrix read from a Matrix Market file (symmetric storage, irregular rows)
+    instead of the band matrix: every candidate schedule computes y = A x"""
+    from tenzing_amd.models import SpmvConfig, build_spmv
+    import random
+
+    rnd = random.Random(5)
+    n, lines = 4000, []
+    for r in range(1, n + 1):
+        for _ in range(rnd.choice([0, 1, 3, 40])):  # empty, short and long rows
+            c = rnd.randint(1, r)
+            lines.append(f"{r} {c} {rnd.uniform(-1, 1):.6f}")
+    f = tmp_path / "sym.mtx"
+    f.write_text("%%MatrixMarket matrix coordinate real symmetric\n"
+                 f"{n} {n} {len(lines)}\n" + "\n".join(lines) + "\n")
+    sp, g = build_spmv(SpmvConfig(matrix=str(f)), tz.SelfCtrl(), device=0)
+    assert sp.args.m == n
+    rt = tz.HipRuntime(device=0, n_streams=2)
+    for m in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+        rt.set_mode(m)
+        for seed in range(6):
+            seq = tz.random_rollout(tz.State(g, tz.Platform(2)), seed)
+            sp.reset_y()
+            rt.prepare(seq)
+            rt.run(1)
+            rt.device_sync()
+            assert sp.check() < 1e-4, seq.desc()
