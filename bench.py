@@ -44,6 +44,36 @@ def _start_deadline(seconds: float) -> None:
     t.start()
 
 
+def link_probe(tz, halo, ctrl, iters):
+    """GB/s that one xGMI link carries with each available transport (the +z face to the +z
+    neighbour, every rank at once, one transfer at a time), and the per-link bound of the
+    exchange: the bytes of the busiest link (the peer receiving the most) over the best rate."""
+    dirs = [halo.dir(i) for i in range(halo.ndirs())]
+    if (0, 0, 1) not in dirs:
+        return None
+    i = dirs.index((0, 0, 1))
+    if halo.is_direct(i):
+        return None
+    face = 8.0 * halo.box_elems(i)
+    rates = {}
+    for via in ("put", "sdma", "rccl"):
+        try:
+            t = halo.link_probe(i, via, iters, ctrl)
+            rates[via] = face / t / 1e9
+        except Exception as e:  # noqa: BLE001  (collective: every rank skips together)
+            rates[via] = None
+            if ctrl.rank == 0:
+                print(f"bench.py: link probe {via}: {e}", file=sys.stderr)
+    per_peer = {}
+    for k in range(halo.ndirs()):
+        if not halo.is_direct(k):
+            per_peer[halo.neighbor(k)] = per_peer.get(halo.neighbor(k), 0.0) + 8.0 * halo.box_elems(k)
+    busiest = max(per_peer.values()) if per_peer else 0.0
+    best = max([r for r in rates.values() if r], default=None)
+    return {"face_MB": face / 1e6, "GBps": rates, "busiest_link_MB": busiest / 1e6,
+            "link_bound_ms": (busiest / (best * 1e9) * 1e3) if best else None}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -91,6 +121,9 @@ def main() -> int:
                     help="re-measure the K best distinct candidates interleaved, compiled as "
                          "hipGraphs, and keep the fastest (0: trust the search's ranking)")
     ap.add_argument("--csv", default="", help="write the search results CSV here (rank 0)")
+    ap.add_argument("--link-probe-iters", type=int, default=20,
+                    help="several ranks: after the timing, measure what one xGMI link carries "
+                         "per transport (one face to one peer at a time; 0 = skip)")
     ap.add_argument("--deadline-s", type=float, default=1500.0,
                     help="abort (exit 4) if the whole run takes longer (hung collective)")
     args = ap.parse_args()
@@ -238,6 +271,12 @@ def main() -> int:
     t = t_graph if use_graph else t_eager
     ms = t / args.steps * 1e3
 
+    # per-link bandwidth of each transport (context for the multi-GPU number: an exchange can
+    # not beat the bytes its busiest link carries divided by what one link moves)
+    probe = None
+    if world > 1 and args.link_probe_iters > 0:
+        probe = link_probe(tz, halo, ctrl, args.link_probe_iters)
+
     names = [o.name for o in best.ops()]
     via = [t for t, key in (("direct", "he_direct_"), ("rccl", "he_shift_"), ("ipc", "he_put_"),
                             ("sdma", "he_copyput_"), ("relay", "he_rl"))
@@ -296,6 +335,7 @@ def main() -> int:
                              if args.stencil else None),
             "ipc_mode": halo.ipc_mode() or None,
             "relay_offered": halo.uses_relay(),
+            "link_probe": probe,
         }
         print(json.dumps(out), flush=True)
     return 0 if bad == 0 else 3

@@ -655,6 +655,10 @@ PYBIND11_MODULE(_tz, m) {
       .def("uses_ipc", &HaloExchange::uses_ipc)
       .def("uses_relay", &HaloExchange::uses_relay)
       .def("relay_faces", &HaloExchange::relay_faces)
+      .def("link_probe", [](HaloExchange &h, int dir, const std::string &via, int iters, Ctrl *c) {
+             return h.link_probe(dir, via, iters, c);
+           }, py::arg("dir"), py::arg("via"), py::arg("iters"), py::arg("ctrl"),
+           py::call_guard<py::gil_scoped_release>())
       .def("ipc_mode", &HaloExchange::ipc_mode)
       .def("put_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.put_group(d, P(s)); })
       .def("wait_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.wait_group(d, P(s)); })

@@ -526,6 +526,74 @@ void HaloExchange::relay_preflight(Ctrl *ctrl) {
   init_grid();
 }
 
+double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl *ctrl) {
+  TZ_CHECK(ready() && ctrl && ctrl->size() == a_.size, "link probe needs a set-up exchange and its control plane");
+  TZ_CHECK(dir >= 0 && dir < ndirs() && !direct_[dir], "direction " << dir << " is not remote");
+  TZ_CHECK(iters >= 1, "iters must be positive");
+  const std::vector<int> d{dir};
+  hipStream_t s = nullptr;
+  TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  auto once = [&] {
+    if (via == "put" || via == "sdma") {
+      TZ_CHECK(ipcReady_ && ipc_[dir], "ipc transport not available");
+      if (via == "put") put_group(d, s);
+      else copy_put_group(d, s);
+      wait_group(d, s);
+      if (!ipcGrid_) ipc_unpack_group(d, s);
+    } else if (via == "rccl") {
+      TZ_CHECK(useRccl_ && pipe_[dir], "RCCL transport not available");
+      pack_group(d, s);
+      shift_group(d, s, 0);
+      unpack_group(d, s);
+    } else {
+      TZ_THROW("link probe transport must be put, sdma or rccl (got " << via << ")");
+    }
+  };
+  // agree collectively that every rank can run the probe before any transfer is issued
+  std::string err;
+  if ((via == "put" || via == "sdma") && !(ipcReady_ && ipc_[dir] && (via == "put" || (useCopy_ && !ipcGrid_))))
+    err = via + " unavailable";
+  if (via == "rccl" && !(useRccl_ && pipe_[dir])) err = "rccl unavailable";
+  double bad = err.empty() ? 0.0 : 1.0;
+  ctrl->allreduce_max(&bad, 1);
+  if (bad != 0) {
+    hipStreamDestroy(s);
+    TZ_THROW("link probe: " << (err.empty() ? via + " unavailable on another rank" : err));
+  }
+  // a local failure travels with the collectives (every rank makes the same calls), so all
+  // ranks throw together instead of leaving peers in a barrier
+  auto agree = [&](std::string &e, double *v) {
+    double red[2] = {v ? *v : 0.0, e.empty() ? 0.0 : 1.0};
+    ctrl->allreduce_max(red, 2);
+    if (v) *v = red[0];
+    if (red[1] != 0.0) {
+      hipStreamSynchronize(s);
+      hipStreamDestroy(s);
+      TZ_THROW("link probe (" << via << ") failed" << (e.empty() ? " on another rank" : ": " + e));
+    }
+  };
+  std::string e;
+  try {
+    once(); // warm-up (first-use mappings, RCCL connections)
+    TZ_HIP(hipStreamSynchronize(s));
+  } catch (const std::exception &x) {
+    e = x.what();
+  }
+  agree(e, nullptr);
+  double t = 0;
+  try {
+    const double t0 = wtime();
+    for (int k = 0; k < iters; ++k) once();
+    TZ_HIP(hipStreamSynchronize(s));
+    t = (wtime() - t0) / iters;
+  } catch (const std::exception &x) {
+    e = x.what();
+  }
+  agree(e, &t); // (also: peers may write into my buffers until every rank got here)
+  hipStreamDestroy(s);
+  return t;
+}
+
 int HaloExchange::ipc_errors() {
   if (!useIpc_ || !err_.get()) return 0;
   int e = 0;

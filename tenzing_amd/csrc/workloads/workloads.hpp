@@ -260,6 +260,12 @@ public:
                     void *stream) const;
   /// the face directions among the remote ones (what relay routing splits)
   std::vector<int> relay_faces() const;
+  /// Link probe (collective): every rank moves its slab facing direction `dir` to its
+  /// neighbour there, `iters` times, through `via` ("put": kernel stores into the peer's
+  /// memory, "sdma": copy engines, "rccl": pack + RCCL send/recv + unpack), one transfer at a
+  /// time on one stream. Each transfer crosses one xGMI link per rank, so this measures what one
+  /// link carries with that transport. Returns seconds per transfer, max over ranks.
+  double link_probe(int dir, const std::string &via, int iters, Ctrl *ctrl);
   /// direct transport: move the interior slab facing each direction of `dirs` straight into
   /// the neighbour's ghost region on the opposite side (one launch)
   void direct_group(const std::vector<int> &dirs, void *stream) const;

@@ -91,23 +91,31 @@ def test_relay_routing_loopback(gpu):
             assert run["bad1"] == 0 and run["bad2"] == 0 and run["err"] == 0, run
 
 
-def test_bench_two_ranks_loopback(gpu, tmp_path):
+@pytest.mark.parametrize("mode", ["grid", "buffers"])
+def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     """the driver's multi-GPU bench flow (torchrun, one process per rank, collective search,
-    best-schedule broadcast, device-side verification, eager + hipGraph timing, max over ranks)
-    with both ranks on this one GPU. RCCL refuses two ranks on one device, so this also checks
-    the collective fallback to the IPC transport."""
+    best-schedule broadcast, device-side verification, eager + hipGraph timing, max over ranks,
+    per-link transport probes) with both ranks on this one GPU. RCCL refuses two ranks on one
+    device, so this also checks the collective fallback to the IPC transport."""
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
            "--cells", "64", "--mcts-iters", "6", "--bench-iters", "3", "--deadline-s", "240"]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, TZ_IPC_GRID="1" if mode == "grid" else "0")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     j = json.loads(line)
     assert j["n_gpus"] == 2 and j["steps"] == 6 and j["verified_bad_cells"] == 0
     assert j["transport"] == "direct+ipc" and j["config"]["rank_grid"] == [1, 1, 2]
     assert j["value"] > 0 and j["higher_is_better"] is False
+    assert j["ipc_mode"] == mode
+    p = j["link_probe"]
+    # kernel puts always; copy-engine puts need receive buffers; RCCL is refused in loopback
+    assert p["GBps"]["put"] > 0 and p["GBps"]["rccl"] is None
+    assert (p["GBps"]["sdma"] is not None) == (mode == "buffers")
+    assert p["busiest_link_MB"] > p["face_MB"] > 0 and p["link_bound_ms"] > 0
 
 
 @pytest.mark.parametrize("world,case", [(2, "spmv"), (4, "spmv"), (8, "spmv"), (2, "fused")])
