@@ -45,9 +45,11 @@ def _start_deadline(seconds: float) -> None:
 
 
 def link_probe(tz, halo, ctrl, iters):
-    """GB/s that one xGMI link carries with each available transport (the +z face to the +z
-    neighbour, every rank at once, one transfer at a time), and the per-link bound of the
-    exchange: the bytes of the busiest link (the peer receiving the most) over the best rate."""
+    """GB/s of ONE transfer over one xGMI link with each available transport (the +z face to
+    the +z neighbour, every rank at once, one transfer at a time), and the time the exchange's
+    busiest link (the peer receiving the most bytes) would take at the best of those rates. An
+    exchange runs several transfers per link at once (several streams, copy engines), so it can
+    beat that time; on loopback ranks (one GPU) the rates say nothing about xGMI."""
     dirs = [halo.dir(i) for i in range(halo.ndirs())]
     if (0, 0, 1) not in dirs:
         return None
@@ -71,7 +73,7 @@ def link_probe(tz, halo, ctrl, iters):
     busiest = max(per_peer.values()) if per_peer else 0.0
     best = max([r for r in rates.values() if r], default=None)
     return {"face_MB": face / 1e6, "GBps": rates, "busiest_link_MB": busiest / 1e6,
-            "link_bound_ms": (busiest / (best * 1e9) * 1e3) if best else None}
+            "busiest_link_at_probe_rate_ms": (busiest / (best * 1e9) * 1e3) if best else None}
 
 
 def main() -> int:
