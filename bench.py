@@ -99,6 +99,9 @@ def main() -> int:
     ap.add_argument("--stencil", action="store_true",
                     help="exchange + 7-point stencil per iteration (not the BASELINE metric): the "
                          "search may update the interior while ghosts are in flight")
+    ap.add_argument("--relay", default="auto", choices=["auto", "off", "force"],
+                    help="2x2x2 ranks (8 GPUs): offer relay routing of a share of every face "
+                         "through the corner peer's idle links (auto), never, or only it")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=0,
@@ -150,7 +153,8 @@ def main() -> int:
               file=sys.stderr)
         return 2
     cfg = HaloConfig(n=args.n, neighbors=args.neighbors, fuse=args.fuse, order=args.order,
-                     transport=args.transport, rank_grid=grid, stencil=args.stencil)
+                     transport=args.transport, rank_grid=grid, stencil=args.stencil,
+                     relay=args.relay)
     halo, graph = build_halo(cfg, ctrl, device)
     mode = tz.ExecMode.Graph if args.search_mode == "graph" else tz.ExecMode.Eager
     rt = tz.HipRuntime(device=device, n_streams=args.streams, mode=mode, watchdog_s=120.0,

@@ -24,7 +24,8 @@ def _build_workload(a, ctrl, device, setup):
     from tenzing_amd.models import HaloConfig, SpmvConfig, build_fused, build_halo, build_spmv
 
     hc = HaloConfig(n=a.halo_n, nq=a.nq, ghost=a.ghost, neighbors=a.neighbors, order=a.order,
-                    fuse=a.fuse, transport=a.transport, stencil=a.stencil)
+                    fuse=a.fuse, transport=a.transport, stencil=a.stencil, relay=a.relay,
+                    relay_fracs=tuple(float(f) for f in a.relay_fracs.split(",")))
     sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport,
                     matrix=a.spmv_matrix)
     if a.workload == "halo":
@@ -202,6 +203,10 @@ def main(argv=None) -> int:
     s.add_argument("--order", default="xyzq")
     s.add_argument("--fuse", default="choice")
     s.add_argument("--transport", default="auto")
+    s.add_argument("--relay", default="auto", choices=["auto", "off", "force"],
+                   help="halo, 2x2x2 ranks: route a share of every face through the corner peer")
+    s.add_argument("--relay-fracs", default="0.15,0.2",
+                   help="relayed shares offered to the search (comma-separated)")
     s.add_argument("--stencil", action="store_true",
                    help="halo: add the 7-point stencil (interior beside / shell after the exchange)")
     s.add_argument("--spmv-m", type=int, default=150_000)

@@ -18,6 +18,7 @@
 #include <fstream>
 #include <iostream>
 #include <map>
+#include <sstream>
 #include <string>
 
 using namespace tz;
@@ -55,6 +56,7 @@ void usage() {
          "  [--transport auto|rccl|ipc|copy|direct] [--rank-grid PXxPYxPZ] [--spmv-m N] [--spmv-matrix F.mtx]\n"
          "  [--spmv-form choice|split|accum] [--spmv-transport auto|rccl|ipc]\n"
          "  [--spmv-library adaptive|lrb|rowsplit|''] [--cu-partition] [--stencil] [--max-seqs N]\n"
+         "  [--relay auto|off|force] [--relay-fracs F1,F2]\n"
          "  [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--watchdog S]\n";
@@ -127,6 +129,17 @@ int main(int argc, char **argv) {
       h.transport = a.get("transport", "auto");
       h.order = a.get("order", "xyzq");
       h.stencil = a.flag("stencil");
+      h.relay = a.get("relay", "auto");
+      {
+        // comma-separated relayed shares, e.g. 0.15,0.2
+        const std::string fr = a.get("relay-fracs", "");
+        if (!fr.empty()) {
+          h.relay_fracs.clear();
+          std::stringstream ss(fr);
+          std::string tok;
+          while (std::getline(ss, tok, ',')) h.relay_fracs.push_back(std::stod(tok));
+        }
+      }
       TZ_CHECK(h.order == "xyzq" || h.order == "qxyz", "--order must be xyzq or qxyz");
       h.rank = rank;
       h.size = size;

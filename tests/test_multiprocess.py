@@ -222,3 +222,32 @@ def test_sigint_on_rank0_stops_every_rank(tmp_path):
     assert len(lines) >= 2 and all(len(x.split("|")) > 7 for x in lines[1:])
     # only the search master prints results
     assert [x for x in outs[1][0].strip().splitlines() if not x.startswith("[Gloo]")] == []
+
+
+def test_relay_search_8_ranks_sim(tmp_path):
+    """the relay-routing alternatives through the whole collective search on 8 CPU ranks (the
+    2x2x2 grid, simulated costs): every rank rebuilds the broadcast candidates by name, and
+    rank 0's results hold relayed schedules"""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(8):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="8", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TZ_IPC_GRID="0")
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "tenzing_amd", "search", "--workload", "halo", "--sim",
+             "--neighbors", "26", "--halo-n", "16", "--order", "qxyz", "--fuse", "choice",
+             "--streams", "3", "--iters", "12", "--bench-iters", "2", "--relay", "force",
+             "--csv", str(tmp_path / f"r{r}.csv")],
+            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        outs = [p.communicate(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert [p.returncode for p in procs] == [0] * 8, [o[1][-1500:] for o in outs]
+    rows = (tmp_path / "r0.csv").read_text().strip().splitlines()[1:]
+    assert len(rows) == 12 and all('"he_rl' in row for row in rows)
