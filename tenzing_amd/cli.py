@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 import time
 
@@ -141,7 +142,38 @@ def cmd_search(a) -> int:
             summary["best_pct10_ms"] = res.sims[b].res.pct10 * 1e3
             summary["best_schedule"] = json.loads(res.sims[b].seq.json())
         print(json.dumps(summary))
+    if a.trace_best:
+        _trace_best(a, tz, ctrl, g, res, rt)
     return 0
+
+
+def _trace_best(a, tz, ctrl, g, res, rt) -> None:
+    """Timeline of the best schedule as Chrome trace-event JSON (chrome://tracing, Perfetto):
+    measured per-op device times on hardware (every rank runs it, each writes its own file),
+    the discrete-event model's timeline with --sim."""
+    msg = ""
+    if ctrl.rank == 0 and res.best() >= 0:
+        msg = res.sims[res.best()].seq.json(True)
+    msg = ctrl.bcast(msg, 0).decode()
+    if not msg:
+        return
+    seq = tz.OpIndex(g).sequence_from_json(msg)
+    if a.sim:
+        ex = tz.SimExecutor(a.streams)
+        ex.run_once(seq)
+        spans = [(n, st, 0, t0, t1) for n, st, t0, t1 in ex.trace()]
+    elif isinstance(rt, tz.HipRuntime):
+        spans = rt.trace(seq, a.trace_iters)
+    else:
+        if ctrl.rank == 0:
+            print("--trace-best needs a GPU run or --sim", file=sys.stderr)
+        return
+    path = a.trace_best
+    if ctrl.size > 1:
+        root, ext = os.path.splitext(path)
+        path = f"{root}.r{ctrl.rank}{ext or '.json'}"
+    with open(path, "w") as f:
+        f.write(tz._tz.chrome_trace(spans))
 
 
 def cmd_rules(a) -> int:
@@ -194,6 +226,10 @@ def main(argv=None) -> int:
     s.add_argument("--resume", default="")
     s.add_argument("--csv", default="")
     s.add_argument("--jsonl", default="")
+    s.add_argument("--trace-best", default="",
+                   help="write the best schedule's timeline as Chrome trace JSON (per rank)")
+    s.add_argument("--trace-iters", type=int, default=2,
+                   help="iterations in the --trace-best timeline")
     s.add_argument("--watchdog", type=float, default=120.0)
     s.add_argument("--bind-cpus", action="store_true")
     s.add_argument("--halo-n", type=int, default=512)

@@ -577,7 +577,24 @@ PYBIND11_MODULE(_tz, m) {
       .def("native_stream", [](HipRuntime &r, int s) { return reinterpret_cast<uintptr_t>(r.native_stream(s)); })
       .def("device_sync", &HipRuntime::device_sync, py::call_guard<py::gil_scoped_release>())
       .def("set_watchdog", &HipRuntime::set_watchdog)
-      .def_property("spin_sync", &HipRuntime::spin_sync, &HipRuntime::set_spin_sync);
+      .def_property("spin_sync", &HipRuntime::spin_sync, &HipRuntime::set_spin_sync)
+      .def("trace", [](HipRuntime &r, const Sequence &seq, int iterations) {
+             std::vector<HipRuntime::Span> sp;
+             {
+               py::gil_scoped_release nogil;
+               sp = r.trace(seq, iterations);
+             }
+             py::list l;
+             for (const auto &s : sp) l.append(py::make_tuple(s.name, s.stream, s.iteration, s.start_us, s.end_us));
+             return l;
+           }, py::arg("seq"), py::arg("iterations") = 1,
+           "eager run with timing events around every GPU op: [(name, stream (-1 host), iteration, start_us, end_us)]");
+  m.def("chrome_trace", [](const std::vector<std::tuple<std::string, int, int, double, double>> &spans) {
+    std::vector<HipRuntime::Span> v;
+    for (const auto &t : spans)
+      v.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t)});
+    return chrome_trace(v).dump();
+  }, py::arg("spans"), "Chrome trace-event JSON of (name, stream, iteration, start_us, end_us) spans");
 
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def(py::init([](Ctrl &c, int dev) { return std::make_shared<RcclComm>(c, dev); }))

@@ -205,6 +205,7 @@ void TcpCtrl::allreduce(double *v, size_t n, bool isMax) {
   } else {
     send_frame(peers_[0], buf);
     std::string f = recv_frame(peers_[0]);
+    TZ_CHECK(f.size() == n * sizeof(double), "allreduce size mismatch (mismatched collectives?)");
     std::memcpy(v, f.data(), n * sizeof(double));
   }
 }

@@ -366,6 +366,102 @@ void HipRuntime::select(size_t k) {
   internalUsed_ = 0;
 }
 
+std::vector<HipRuntime::Span> HipRuntime::trace(const Sequence &seq, int iterations) {
+  TZ_CHECK(iterations >= 1, "iterations must be positive");
+  const Sequence keep = seq_;
+  seq_ = seq;
+  event(std::max(0, seq.num_events() - 1));
+  std::vector<hipEvent_t> evs;
+  auto timing_event = [&] {
+    hipEvent_t e;
+    TZ_HIP(hipEventCreate(&e));
+    evs.push_back(e);
+    return e;
+  };
+  struct Pending {
+    size_t span;
+    hipEvent_t a, b;
+  };
+  std::vector<Span> spans;
+  std::vector<Pending> pending;
+  std::string err;
+  try {
+    TZ_HIP(hipDeviceSynchronize());
+    hipEvent_t base = timing_event();
+    TZ_HIP(hipEventRecord(base, S(streams_[0])));
+    TZ_HIP(hipEventSynchronize(base));
+    const double h0 = wtime();
+    for (int it = 0; it < iterations; ++it) {
+      internalUsed_ = 0;
+      for (const auto &e : seq.entries) {
+        const BoundOp &op = *e.op;
+        if (op.op_class() == OpClass::BoundGpu) {
+          const int st = static_cast<const BoundGpuOp &>(op).stream();
+          hipEvent_t a = timing_event(), b = timing_event();
+          TZ_HIP(hipEventRecord(a, S(native_stream(st))));
+          op.run(*this);
+          TZ_HIP(hipEventRecord(b, S(native_stream(st))));
+          pending.push_back({spans.size(), a, b});
+          spans.push_back({op.name(), st, it, 0, 0});
+        } else {
+          const double t0 = wtime();
+          op.run(*this);
+          spans.push_back({op.name(), -1, it, (t0 - h0) * 1e6, (wtime() - h0) * 1e6});
+        }
+      }
+    }
+    TZ_HIP(hipDeviceSynchronize());
+    for (const Pending &p : pending) {
+      float ta = 0, tb = 0;
+      TZ_HIP(hipEventElapsedTime(&ta, base, p.a));
+      TZ_HIP(hipEventElapsedTime(&tb, base, p.b));
+      spans[p.span].start_us = double(ta) * 1e3;
+      spans[p.span].end_us = double(tb) * 1e3;
+    }
+  } catch (const std::exception &e) {
+    err = e.what();
+  }
+  for (hipEvent_t e : evs) hipEventDestroy(e);
+  seq_ = keep;
+  internalUsed_ = 0;
+  if (!err.empty()) throw Error(err);
+  return spans;
+}
+
+Json chrome_trace(const std::vector<HipRuntime::Span> &spans) {
+  Json ev = Json::array();
+  int maxStream = -1;
+  for (const auto &s : spans) maxStream = std::max(maxStream, s.stream);
+  auto meta = [&](int tid, const std::string &name) {
+    Json m, a;
+    m["name"] = "thread_name";
+    m["ph"] = "M";
+    m["pid"] = int64_t(0);
+    m["tid"] = int64_t(tid);
+    a["name"] = name;
+    m["args"] = a;
+    ev.push_back(m);
+  };
+  meta(0, "host");
+  for (int s = 0; s <= maxStream; ++s) meta(s + 1, "stream " + std::to_string(s));
+  for (const auto &s : spans) {
+    Json j, a;
+    j["name"] = s.name;
+    j["ph"] = "X";
+    j["pid"] = int64_t(0);
+    j["tid"] = int64_t(s.stream + 1);
+    j["ts"] = s.start_us;
+    j["dur"] = std::max(0.0, s.end_us - s.start_us);
+    a["iteration"] = int64_t(s.iteration);
+    j["args"] = a;
+    ev.push_back(j);
+  }
+  Json out;
+  out["traceEvents"] = ev;
+  out["displayTimeUnit"] = "ns";
+  return out;
+}
+
 void HipRuntime::run(int64_t n) {
   if (watchdogS_ > 0) deadline_ = wtime() + watchdogS_ * double(std::max<int64_t>(1, n));
   if (graphExec_) {

@@ -88,6 +88,20 @@ public:
   void set_graph_unroll(int u);
   int graph_unroll() const { return unroll_; }
 
+  /// One op of a traced run: GPU ops carry device times (timing events recorded around the
+  /// launch on the op's stream), host ops (syncs, CPU ops) host wall-clock times; both in us
+  /// from the start of the trace (the two clocks are aligned at that start only).
+  struct Span {
+    std::string name;
+    int stream; // -1: host
+    int iteration;
+    double start_us, end_us;
+  };
+  /// Run `seq` eagerly `iterations` times with a timing event before and after every GPU op and
+  /// return the per-op timeline (the mode and prepared sequence stay as they were). The events
+  /// add a little issue overhead, so use this to look at a schedule, not to time it.
+  std::vector<Span> trace(const Sequence &seq, int iterations = 1);
+
 private:
   void *event(int e);
   void *internal_event();
@@ -119,6 +133,10 @@ private:
   std::atomic<bool> stop_{false};
   std::thread watchdog_;
 };
+
+/// Chrome trace-event JSON (chrome://tracing, Perfetto) of a traced timeline: one track per
+/// stream plus a host track
+Json chrome_trace(const std::vector<HipRuntime::Span> &spans);
 
 /// route the core's trace ranges (MCTS phases, schedule ops in eager runs) to roctx
 void enable_roctx(bool on);

@@ -112,3 +112,18 @@ def test_cpp_library_example_sim():
     assert r.returncode == 0, r.stderr[-2000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["candidates"] == 24 and j["best_us"] < j["worst_us"]
+
+
+def test_trace_best_chrome_json_sim(tmp_path):
+    """--trace-best: the best schedule's timeline as Chrome trace events (here the discrete-event
+    model's): one complete event per GPU op, on the track of its stream"""
+    out = tmp_path / "best.json"
+    _py("search", "--workload", "halo", "--sim", "--neighbors", "26", "--halo-n", "32",
+        "--streams", "3", "--iters", "10", "--bench-iters", "2", "--fuse", "none",
+        "--trace-best", str(out))
+    ev = json.loads(out.read_text())["traceEvents"]
+    ops = [e for e in ev if e["ph"] == "X"]
+    names = {e["args"]["name"] for e in ev if e["ph"] == "M"}
+    assert len(ops) == 26 and all(e["name"].startswith("he_direct_") for e in ops)
+    assert all(e["dur"] > 0 and e["ts"] >= 0 for e in ops)
+    assert "host" in names and {f"stream {e['tid'] - 1}" for e in ops} <= names

@@ -384,3 +384,33 @@ def test_spmv_workload_from_matrix_market_file(tz, gpu, tmp_path):
             rt.run(1)
             rt.device_sync()
             assert sp.check() < 1e-4, seq.desc()
+
+
+def test_runtime_trace_timeline(tz, gpu):
+    """HipRuntime.trace: measured device start/end of every GPU op (timing events around each
+    launch), host spans for the syncs; ops on one stream do not overlap, dependent ops start
+    after their producers end; the prepared schedule and mode are left as they were"""
+    halo, g = _small_halo(tz, neighbors=26, transport="direct")
+    rt = tz.HipRuntime(device=0, n_streams=2, mode=tz.ExecMode.Graph, graph_unroll=2)
+    seq = tz.random_rollout(tz.State(g, tz.Platform(2)), 3)
+    rt.prepare(seq)
+    gpu_ops = [o.name for o in seq.ops() if isinstance(o, tz._tz.BoundGpuOp)]
+    spans = rt.trace(seq, 3)
+    dev = [s for s in spans if s[1] >= 0]
+    assert len(dev) == 3 * len(gpu_ops)
+    for name, st, it, t0, t1 in dev:
+        assert 0 <= t0 <= t1 and name in gpu_ops
+    for st in (0, 1):
+        on = sorted((t0, t1) for _, s, _, t0, t1 in dev if s == st)
+        assert all(a[1] <= b[0] + 1e-3 for a, b in zip(on, on[1:]))
+    # iterations follow each other (the schedule ends with host syncs)
+    last0 = max(t1 for _, _, it, _, t1 in dev if it == 0)
+    first1 = min(t0 for _, _, it, t0, _ in dev if it == 1)
+    assert last0 <= first1 + 1e-3
+    assert rt.effective_mode == tz.ExecMode.Graph
+    halo.init_grid()
+    rt.run(1)
+    rt.device_sync()
+    assert halo.check_grid() == 0
+    j = json.loads(tz._tz.chrome_trace(spans))
+    assert sum(e["ph"] == "X" for e in j["traceEvents"]) == len(spans)
