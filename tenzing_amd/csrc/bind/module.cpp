@@ -605,7 +605,10 @@ PYBIND11_MODULE(_tz, m) {
       })
       .def("sendrecv", [](const RcclComm &c, uintptr_t sb, size_t sc, int sp, uintptr_t rb, size_t rc, int rp, int dt, uintptr_t s) {
         c.sendrecv(P(sb), sc, sp, P(rb), rc, rp, dt, P(s));
-      });
+      })
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("aborted", &RcclComm::aborted);
+  m.def("rccl_abort_all", &rccl_abort_all, py::call_guard<py::gil_scoped_release>());
 
   // ------------------------------------------------------------------ workloads
   py::class_<HaloArgs>(m, "HaloArgs")

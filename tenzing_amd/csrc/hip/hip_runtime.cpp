@@ -1,6 +1,7 @@
 #include "hip_runtime.hpp"
 
 #include "core/util.hpp"
+#include "rccl_comm.hpp"
 
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime_api.h>
@@ -73,14 +74,29 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
   }
   if (watchdogS_ > 0) {
     watchdog_ = std::thread([this] {
+      // past the deadline: abort the RCCL communicators (their kernels return, the run ends and
+      // throws, and the benchmarker turns that into a collectively skipped candidate); if the
+      // run still has not returned after a grace period, nothing can unblock it: exit
+      double grace = 0;
       while (!stop_.load()) {
         std::this_thread::sleep_for(std::chrono::milliseconds(200));
         const double d = deadline_.load();
-        if (d > 0 && wtime() > d) {
+        if (d <= 0) {
+          grace = 0;
+          continue;
+        }
+        if (wtime() <= d) continue;
+        if (grace == 0) {
+          const int n = rccl_abort_all();
           std::fprintf(stderr,
                        "[tz] watchdog: schedule iteration exceeded %.1f s (deadlocked "
-                       "communication?); aborting\n",
-                       watchdogS_);
+                       "communication?); aborted %d RCCL communicator(s)\n",
+                       watchdogS_, n);
+          std::fflush(stderr);
+          aborted_ = true;
+          grace = wtime() + std::max(10.0, watchdogS_);
+        } else if (wtime() > grace) {
+          std::fprintf(stderr, "[tz] watchdog: the run did not return after the abort; exiting\n");
           std::fflush(stderr);
           std::_Exit(3);
         }
@@ -463,7 +479,22 @@ Json chrome_trace(const std::vector<HipRuntime::Span> &spans) {
 }
 
 void HipRuntime::run(int64_t n) {
+  aborted_ = false;
   if (watchdogS_ > 0) deadline_ = wtime() + watchdogS_ * double(std::max<int64_t>(1, n));
+  try {
+    run_impl(n);
+  } catch (...) {
+    deadline_ = 0;
+    if (aborted_.exchange(false))
+      TZ_THROW("watchdog: the schedule exceeded " << watchdogS_ << " s per iteration and was aborted");
+    throw;
+  }
+  deadline_ = 0;
+  if (aborted_.exchange(false))
+    TZ_THROW("watchdog: the schedule exceeded " << watchdogS_ << " s per iteration and was aborted");
+}
+
+void HipRuntime::run_impl(int64_t n) {
   if (graphExec_) {
     hipStream_t origin = S(streams_[0]);
     int64_t i = 0;
@@ -486,7 +517,6 @@ void HipRuntime::run(int64_t n) {
       }
     }
   }
-  deadline_ = 0;
 }
 
 } // namespace tz

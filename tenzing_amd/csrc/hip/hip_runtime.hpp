@@ -15,8 +15,10 @@
 //    synchronizer uses, every GPU op is captured alone on its stream into a child graph, and
 //    the child-graph nodes get exactly the dependencies the schedule's events / host syncs
 //    imply. Host synchronizations therefore cost nothing inside a replay;
-//  * a watchdog: a schedule whose iteration exceeds `watchdog_s` (e.g. an RCCL deadlock) aborts
-//    the process with a diagnostic instead of hanging the search.
+//  * a watchdog: when a schedule's iteration exceeds `watchdog_s` (e.g. an RCCL deadlock) it
+//    aborts the process's RCCL communicators (ncclCommAbort), so the blocked run returns and
+//    throws; the benchmarker turns that into a candidate every rank skips. A run that still does
+//    not return after a grace period ends the process with a diagnostic.
 #pragma once
 
 #include "core/benchmark.hpp"
@@ -108,6 +110,7 @@ private:
   void destroy_graph();
   bool recordable(const Sequence &seq) const;
   void *build_graph(int iterations, size_t &nodes, size_t &edges);
+  void run_impl(int64_t n);
 
   int device_ = 0;
   ExecMode mode_;
@@ -130,6 +133,7 @@ private:
 
   double watchdogS_ = 0;
   std::atomic<double> deadline_{0};
+  std::atomic<bool> aborted_{false}; // the watchdog fired during the current run
   std::atomic<bool> stop_{false};
   std::thread watchdog_;
 };

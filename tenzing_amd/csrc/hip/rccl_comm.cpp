@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 
 namespace tz {
 
@@ -15,6 +16,31 @@ namespace tz {
     ncclResult_t r_ = (x);                                                                         \
     if (r_ != ncclSuccess) TZ_THROW(#x << " failed: " << ncclGetErrorString(r_));                  \
   } while (0)
+
+namespace {
+// live communicators, for the watchdog's abort-all (a communicator deregisters on destruction)
+std::mutex g_mu;
+std::vector<RcclComm *> g_live;
+void register_comm(RcclComm *c) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_live.push_back(c);
+}
+void deregister_comm(RcclComm *c) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_live.erase(std::remove(g_live.begin(), g_live.end(), c), g_live.end());
+}
+} // namespace
+
+int rccl_abort_all() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int n = 0;
+  for (RcclComm *c : g_live)
+    if (!c->aborted()) {
+      c->abort();
+      ++n;
+    }
+  return n;
+}
 
 static ncclDataType_t dt(int dtype) {
   switch (dtype) {
@@ -40,6 +66,7 @@ RcclComm::RcclComm(Ctrl &ctrl, int device) : rank_(ctrl.rank()), size_(ctrl.size
   ncclComm_t c = nullptr;
   TZ_NCCL(ncclCommInitRank(&c, size_, id, rank_));
   comm_ = c;
+  register_comm(this);
 }
 
 RcclComm::RcclComm(const std::string &uniqueId, int rank, int size, int device)
@@ -53,14 +80,28 @@ RcclComm::RcclComm(const std::string &uniqueId, int rank, int size, int device)
   ncclComm_t c = nullptr;
   TZ_NCCL(ncclCommInitRank(&c, size_, id, rank_));
   comm_ = c;
+  register_comm(this);
 }
 
 RcclComm::~RcclComm() {
-  if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+  deregister_comm(this);
+  // an aborted communicator has already released its resources
+  if (comm_ && !aborted_.load()) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+}
+
+void RcclComm::abort() {
+  bool expected = false;
+  if (!aborted_.compare_exchange_strong(expected, true)) return;
+  if (comm_) ncclCommAbort(static_cast<ncclComm_t>(comm_));
+}
+
+void RcclComm::check_live() const {
+  TZ_CHECK(!aborted_.load(), "RCCL communicator was aborted (watchdog)");
 }
 
 void RcclComm::sendrecv(const void *sendBuf, size_t sendCount, int sendPeer, void *recvBuf,
                         size_t recvCount, int recvPeer, int dtype, void *stream) const {
+  check_live();
   ncclComm_t c = static_cast<ncclComm_t>(comm_);
   hipStream_t s = static_cast<hipStream_t>(stream);
   TZ_NCCL(ncclGroupStart());
@@ -70,6 +111,7 @@ void RcclComm::sendrecv(const void *sendBuf, size_t sendCount, int sendPeer, voi
 }
 
 void RcclComm::exchange(const std::vector<Xfer> &xs, int dtype, void *stream) const {
+  check_live();
   ncclComm_t c = static_cast<ncclComm_t>(comm_);
   hipStream_t s = static_cast<hipStream_t>(stream);
   TZ_NCCL(ncclGroupStart());
@@ -81,6 +123,7 @@ void RcclComm::exchange(const std::vector<Xfer> &xs, int dtype, void *stream) co
 }
 
 void RcclComm::allreduce_sum(void *buf, size_t count, int dtype, void *stream) const {
+  check_live();
   TZ_NCCL(ncclAllReduce(buf, buf, count, dt(dtype), ncclSum, static_cast<ncclComm_t>(comm_),
                         static_cast<hipStream_t>(stream)));
 }

@@ -15,6 +15,7 @@
 
 #include "core/ctrl.hpp"
 
+#include <atomic>
 #include <memory>
 #include <string>
 #include <vector>
@@ -54,10 +55,21 @@ public:
 
   static std::string version();
 
+  /// ncclCommAbort: RCCL kernels waiting on this communicator return, later operations throw.
+  /// Safe from another thread (the runtime's watchdog) while a stream is blocked in RCCL.
+  void abort();
+  bool aborted() const { return aborted_.load(); }
+
 private:
+  void check_live() const;
   void *comm_ = nullptr;
   int rank_ = 0, size_ = 1;
+  std::atomic<bool> aborted_{false};
 };
+
+/// abort every live communicator of this process (the watchdog's recovery path for a hung
+/// schedule); returns how many were aborted
+int rccl_abort_all();
 
 /// a set of communicators over the same ranks (one per exchange direction)
 std::vector<std::shared_ptr<RcclComm>> make_rccl_comms(Ctrl &ctrl, int device, int n);

@@ -414,3 +414,33 @@ def test_runtime_trace_timeline(tz, gpu):
     assert halo.check_grid() == 0
     j = json.loads(tz._tz.chrome_trace(spans))
     assert sum(e["ph"] == "X" for e in j["traceEvents"]) == len(spans)
+
+
+def test_watchdog_turns_a_hang_into_an_error(tz, gpu):
+    """an iteration longer than the watchdog limit: the watchdog aborts the RCCL
+    communicators (here: a live one-rank communicator) and the run raises instead of ending the
+    process; the runtime stays usable and the benchmarker reports a skippable failure"""
+    comm = tz._tz.RcclComm(tz.SelfCtrl(), 0)
+    g = tz.Graph()
+    slow = tz.BusyKernelOp("slow", 1.5e6)
+    g.start_then(slow)
+    g.then_finish(slow)
+    rt = tz.HipRuntime(device=0, n_streams=1, watchdog_s=0.3)
+    seq = tz.random_rollout(tz.State(g, tz.Platform(1)), 0)
+    rt.prepare(seq)
+    with pytest.raises(Exception, match="watchdog"):
+        rt.run(1)
+    assert comm.aborted
+    with pytest.raises(Exception, match="aborted"):
+        comm.sendrecv(0, 0, 0, 0, 0, 0, 1, 0)
+    # a failing run inside a benchmark is a CandidateFailed every search skips
+    o = tz.DfsOpts()
+    o.bench = tz.BenchOpts(n_iters=1, max_retries=1, target_secs=0.001)
+    r = tz.dfs_explore(g, tz.Platform(1), tz.EmpiricalBenchmarker(rt, tz.SelfCtrl()), tz.SelfCtrl(), o)
+    assert r.failed == 1 and len(r.sims) == 0
+    fast = tz.Graph()
+    k = tz.BusyKernelOp("fast", 10.0)
+    fast.start_then(k)
+    fast.then_finish(k)
+    rt.prepare(tz.random_rollout(tz.State(fast, tz.Platform(1)), 0))
+    rt.run(3)
