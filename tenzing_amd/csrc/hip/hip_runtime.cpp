@@ -78,22 +78,26 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
       // throws, and the benchmarker turns that into a collectively skipped candidate); if the
       // run still has not returned after a grace period, nothing can unblock it: exit
       double grace = 0;
+      uint64_t firedRun = 0;
       while (!stop_.load()) {
         std::this_thread::sleep_for(std::chrono::milliseconds(200));
         const double d = deadline_.load();
-        if (d <= 0) {
-          grace = 0;
-          continue;
-        }
-        if (wtime() <= d) continue;
+        // a new run (or none) since the last firing: start over (the abort may have blocked
+        // this thread across the end of the run it fired for)
+        if (d <= 0 || runGen_.load() != firedRun) grace = 0;
+        if (d <= 0 || wtime() <= d) continue;
         if (grace == 0) {
-          const int n = rccl_abort_all();
+          firedRun = runGen_.load();
+          // flag first, so the run sees it whenever it returns; the abort itself runs on a
+          // thread of its own: it may block for seconds (it frees device memory, which waits
+          // for the device), and this loop must keep watching the next runs meanwhile
+          aborted_ = true;
           std::fprintf(stderr,
                        "[tz] watchdog: schedule iteration exceeded %.1f s (deadlocked "
-                       "communication?); aborted %d RCCL communicator(s)\n",
-                       watchdogS_, n);
+                       "communication?); aborting the RCCL communicators\n",
+                       watchdogS_);
           std::fflush(stderr);
-          aborted_ = true;
+          std::thread([] { rccl_abort_all(); }).detach();
           grace = wtime() + std::max(10.0, watchdogS_);
         } else if (wtime() > grace) {
           std::fprintf(stderr, "[tz] watchdog: the run did not return after the abort; exiting\n");
@@ -479,6 +483,7 @@ Json chrome_trace(const std::vector<HipRuntime::Span> &spans) {
 }
 
 void HipRuntime::run(int64_t n) {
+  ++runGen_;
   aborted_ = false;
   if (watchdogS_ > 0) deadline_ = wtime() + watchdogS_ * double(std::max<int64_t>(1, n));
   try {

@@ -134,6 +134,7 @@ private:
   double watchdogS_ = 0;
   std::atomic<double> deadline_{0};
   std::atomic<bool> aborted_{false}; // the watchdog fired during the current run
+  std::atomic<uint64_t> runGen_{0};  // runs started so far
   std::atomic<bool> stop_{false};
   std::thread watchdog_;
 };
