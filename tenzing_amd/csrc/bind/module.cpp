@@ -259,6 +259,16 @@ PYBIND11_MODULE(_tz, m) {
       .def("start_then", [cop](Graph &g, std::shared_ptr<OpBase> a) { g.start_then(cop(a)); })
       .def("then_finish", [cop](Graph &g, std::shared_ptr<OpBase> a) { g.then_finish(cop(a)); })
       .def("add_edge", &Graph::add_edge)
+      .def("erase", [](Graph &g, const std::string &name) {
+        const int id = g.find(name);
+        TZ_CHECK(id >= 0, "no op named " << name);
+        g.erase(id);
+      }, py::arg("name"), "remove an op and its edges")
+      .def("erase_edge", [](Graph &g, const std::string &a, const std::string &b) {
+        const int ia = g.find(a), ib = g.find(b);
+        TZ_CHECK(ia >= 0 && ib >= 0, "no op named " << (ia < 0 ? a : b));
+        g.erase_edge(ia, ib);
+      }, py::arg("a"), py::arg("b"), "remove the edge a -> b (keep both ops)")
       .def("normalize", &Graph::normalize)
       .def("__len__", &Graph::size)
       .def_property_readonly("capacity", &Graph::capacity)

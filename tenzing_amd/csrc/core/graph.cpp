@@ -132,6 +132,14 @@ void Graph::erase(int id) {
   --n_alive_;
 }
 
+void Graph::erase_edge(int a, int b) {
+  TZ_CHECK(a >= 0 && a < capacity() && b >= 0 && b < capacity(), "bad vertex id");
+  auto &s = nodes_[a].succs;
+  s.erase(std::remove(s.begin(), s.end(), b), s.end());
+  auto &p = nodes_[b].preds;
+  p.erase(std::remove(p.begin(), p.end(), a), p.end());
+}
+
 std::shared_ptr<Graph> Graph::clone_but_replace(int id, const OpPtr &replacement) const {
   auto g = clone();
   TZ_CHECK(id >= 0 && id < capacity() && alive(id), "bad vertex id " << id);

@@ -59,6 +59,8 @@ public:
   /// predecessors/successors, reference graph.hpp:162-219). New vertices get fresh ids.
   std::shared_ptr<Graph> clone_but_expand(int id, const Graph &sub) const;
   void erase(int id);
+  /// remove the edge a -> b if present (reference Graph::erase_edge_only, graph.hpp:448-471)
+  void erase_edge(int a, int b);
 
   // ---- output
   std::string dump_graphviz(const std::string &title = "") const;

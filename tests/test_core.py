@@ -74,6 +74,13 @@ def test_graph_api(tz):
     assert "digraph" in dot and "k3" in dot
     j = json.loads(g.json())
     assert len(j["vertices"]) == 6
+    # erase an edge, then a vertex (reference Graph::erase_edge_only / erase)
+    g.erase_edge("k2", "k4")
+    assert g.num_edges() == 5 and g.find("k4") not in g.succs(k2)
+    g.erase("k3")
+    assert len(g) == 5 and not g.contains("k3") and g.num_edges() == 3
+    with pytest.raises(Exception, match="no op"):
+        g.erase("nope")
 
 
 def test_op_json_schema(tz):
