@@ -39,7 +39,7 @@ def main():
             for mode in [tz.ExecMode.Eager if m == "eager" else tz.ExecMode.Graph for m in modes]:
                 rt.set_mode(mode)
                 rt.set_graph_unroll(3 if mode == tz.ExecMode.Graph else 1)
-                for seed in range(3):
+                for seed in range(int(os.environ.get("TZ_TEST_SEEDS", "3"))):
                     msg = ""
                     if ctrl.rank == 0:
                         msg = tz.random_rollout(tz.State(g, tz.Platform(3)), seed).json(True)
