@@ -38,6 +38,7 @@ namespace kern {
 BoxTuning &box_tuning() {
   static BoxTuning t = [] {
     BoxTuning v;
+    if (const char *e = std::getenv("TZ_PUT_MAX_BLOCKS")) v.put_max_blocks = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("TZ_XCD_REMAP")) {
       const int m = std::atoi(e);
       if (m >= 0 && m <= 2) v.xcd_remap = m;
@@ -136,11 +137,13 @@ DevDesc make_dev(const BoxDesc &b) {
   return d;
 }
 
-uint32_t blocks_for(const DevDesc &d) {
+// `cap`: blocks per box at most (0: BoxTuning::max_blocks)
+uint32_t blocks_for(const DevDesc &d, int cap = 0) {
   const BoxTuning &t = box_tuning();
   const uint64_t per = uint64_t(kThreads) * uint64_t(t.unroll);
   uint64_t b = (uint64_t(d.items) + per - 1) / per;
-  return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(b, uint64_t(t.max_blocks))));
+  const uint64_t m = uint64_t(std::max(1, cap > 0 ? cap : t.max_blocks));
+  return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(b, m)));
 }
 
 typedef double dbl2_t __attribute__((ext_vector_type(2)));
@@ -548,7 +551,8 @@ void box_copy_many(double *grid, const BoxDesc *boxes, int n, bool unpack, void 
 namespace {
 // the device batch of a move launch (shared by the plain and the signalling variant);
 // `keep` maps batch entries back to input boxes
-DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vector<int> &keep);
+DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vector<int> &keep,
+                         int cap = 0);
 } // namespace
 
 void box_move_many(const MoveDesc *moves, int n, void *stream) {
@@ -588,7 +592,7 @@ void box_move_many_signal(const MoveDesc *moves, int n, const MoveSignal &sig, v
   if (!sig.done) throw std::runtime_error("box_move_many_signal: null block counters");
   uint32_t total = 0;
   std::vector<int> keep;
-  const DevBatch b = make_move_batch(moves, n, total, keep);
+  const DevBatch b = make_move_batch(moves, n, total, keep, box_tuning().put_max_blocks);
   if (b.n != n) throw std::runtime_error("box_move_many_signal: empty box (nothing to signal)");
   DevSignal ds{};
   ds.done = sig.done;
@@ -619,7 +623,7 @@ void box_pack_many_signal(double *grid, const BoxDesc *boxes, int n, const MoveS
     b.d[b.n] = d;
     b.block_start[b.n] = total;
     ds.flag[b.n] = sig.flag[i];
-    total += blocks_for(d);
+    total += blocks_for(d, box_tuning().put_max_blocks);
     ++b.n;
   }
   b.block_start[b.n] = total;
@@ -669,7 +673,8 @@ void ipc_signal(unsigned long long *const *signal, int n, void *stream) {
 }
 
 namespace {
-DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vector<int> &keep) {
+DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vector<int> &keep,
+                         int cap) {
   DevBatch b{};
   b.n = 0;
   total = 0;
@@ -700,7 +705,7 @@ DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vec
     }
     b.d[b.n] = d;
     b.block_start[b.n] = total;
-    total += blocks_for(d);
+    total += blocks_for(d, cap);
     keep.push_back(i);
     ++b.n;
   }

@@ -29,6 +29,11 @@ struct BoxTuning {
   bool nt_pack = true;    // non-temporal grid loads in pack: -27 % pack time in pipeline context
   bool nt_unpack = false; // non-temporal grid stores in unpack: +5 % (off)
   int max_blocks = 4096;  // cap per box (grid-stride beyond)
+  // cap per box of the signalling put kernels, whose stores cross xGMI (env
+  // TZ_PUT_MAX_BLOCKS): one link moves ~77 GB/s per direction, which 64 blocks of posted 16-B
+  // stores cover with a wide margin, while thousands of blocks stalled on a link would hold the
+  // CU slots that the concurrent local moves, relay kernels and unpacks need
+  int put_max_blocks = 64;
   bool nt_move = true;    // non-temporal source loads in box_move (direct transfers)
   int xcd_remap = 0; // box_move block order: 0 round-robin, 1 one contiguous range per XCD,
                      // 2 every box split into 8 contiguous per-XCD shares

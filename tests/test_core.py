@@ -243,3 +243,15 @@ def test_xcd_remap_mode_is_validated(tz):
             assert k.get_xcd_remap() == 2
     finally:
         k.set_xcd_remap(prev)
+
+
+def test_put_block_cap_tunable(tz):
+    k = tz._tz.kernels
+    prev = k.get_put_max_blocks()
+    try:
+        k.set_put_max_blocks(128)
+        assert k.get_put_max_blocks() == 128
+        with pytest.raises(Exception):
+            k.set_put_max_blocks(0)
+    finally:
+        k.set_put_max_blocks(prev)
