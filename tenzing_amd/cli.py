@@ -179,7 +179,8 @@ def _trace_best(a, tz, ctrl, g, res, rt) -> None:
 def cmd_rules(a) -> int:
     from tenzing_amd.utils import postprocess
 
-    return postprocess.main([a.results] + (["--out", a.out] if a.out else []))
+    return postprocess.main([a.results] + (["--out", a.out] if a.out else []) +
+                            (["--plots"] if a.plots else []))
 
 
 def cmd_env(a) -> int:
@@ -254,6 +255,7 @@ def main(argv=None) -> int:
     r = sub.add_parser("rules")
     r.add_argument("results")
     r.add_argument("--out", default="")
+    r.add_argument("--plots", action="store_true", help="also write the figures (PDF)")
     r.set_defaults(fn=cmd_rules)
     e = sub.add_parser("env")
     e.add_argument("--topology", action="store_true")

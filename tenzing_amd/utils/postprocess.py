@@ -16,7 +16,10 @@ Pipeline, re-implemented on our result formats:
    all of them — how early the search reveals the rules.
 
 ``python -m tenzing_amd.utils.postprocess results.csv --out prefix_`` writes ``prefix_rules.txt``
-and ``prefix_classes.json``.
+and ``prefix_classes.json``; with ``--plots`` also the reference's figures (matplotlib):
+``prefix_classes.pdf`` (sorted times, the step-kernel response and the class boundaries),
+``prefix_tree.pdf`` (the decision tree) and ``prefix_eval.pdf`` (rule accuracy against the
+number of results trained on).
 """
 from __future__ import annotations
 
@@ -238,14 +241,19 @@ def evaluate_rules(results: list[Result], n: int, labels=None):
     return float(np.mean(clf.predict(X) == labels))
 
 
-def process(results: list[Result], pctl: float = 99.0):
+def process(results: list[Result], pctl: float = 99.0, plots: str = ""):
+    """classes, features, rules; ``plots``: file prefix for the figures ("" = none)"""
     labels, bounds = performance_classes([r.pct10 for r in results], pctl=pctl)
     X, names = feature_matrix(results)
     report = {"n": len(results), "classes": int(labels.max() + 1) if len(labels) else 0,
               "class_bounds_sorted_index": bounds}
+    if plots and len(results):
+        plot_classes([r.pct10 for r in results], labels, bounds, plots + "classes.pdf")
     if report["classes"] < 2 or X.shape[1] == 0:
         return report, []
     clf, err, rules = train_rules(X, labels, names)
+    if plots and clf is not None:
+        plot_tree(clf, names, plots + "tree.pdf")
     cls_times = {}
     for c in range(report["classes"]):
         ts = [r.pct10 for r, l in zip(results, labels) if l == c]
@@ -253,6 +261,68 @@ def process(results: list[Result], pctl: float = 99.0):
     report["train_error"] = err
     report["class_times"] = {str(k): v for k, v in cls_times.items()}
     return report, rules
+
+
+def _plt():
+    import matplotlib
+
+    matplotlib.use("Agg")
+    from matplotlib import pyplot as plt
+
+    return plt
+
+
+def plot_classes(times, labels, bounds, path, radius_frac: float = 0.005):
+    """Reference postprocess.py:25-101 figure: the sorted pct10 times coloured by class, the
+    +1/-1 step-kernel response whose peaks are the class boundaries, and the boundaries."""
+    plt = _plt()
+    times = np.asarray(times, dtype=float) * 1e3
+    order = np.argsort(times, kind="stable")
+    arr = times[order]
+    n = len(arr)
+    kr = max(1, int(math.ceil(n * radius_frac)))
+    conv = np.convolve(arr, np.array([1.0] * kr + [-1.0] * kr), "valid") if n > 2 * kr else np.zeros(0)
+    fig, axs = plt.subplots(2, sharex=True, figsize=(5, 4))
+    axs[0].scatter(np.arange(n), arr, c=np.asarray(labels)[order], s=4, cmap="tab10")
+    axs[0].set_ylabel("pct10 (ms)")
+    axs[1].plot(np.arange(len(conv)) + kr, conv, color="black", linewidth=0.8)
+    axs[1].set_ylabel("step response")
+    axs[1].set_xlabel("schedules, sorted by time")
+    for b in bounds:
+        for ax in axs:
+            ax.axvline(b, color="gray", linestyle=":", linewidth=0.8)
+    fig.tight_layout()
+    fig.savefig(path)
+    plt.close(fig)
+
+
+def plot_tree(clf, names, path):
+    """Reference postprocess.py:254-278 (predict_{depth}.pdf): the trained decision tree."""
+    from sklearn.tree import plot_tree as sk_plot_tree
+
+    plt = _plt()
+    depth = clf.get_depth()
+    fig, ax = plt.subplots(figsize=(max(6, 3 * clf.get_n_leaves()), max(4, 2 * depth)))
+    sk_plot_tree(clf, feature_names=names, class_names=[str(c) for c in clf.classes_],
+                 filled=True, impurity=False, ax=ax, fontsize=7)
+    fig.savefig(path)
+    plt.close(fig)
+
+
+def plot_eval(evals: dict, path):
+    """Reference postprocess.py:719-771 (eval_rules.pdf): accuracy on all results of the rules
+    trained on the first n."""
+    plt = _plt()
+    pts = sorted((int(k), v) for k, v in evals.items() if v is not None)
+    fig, ax = plt.subplots(figsize=(4, 2.5))
+    if pts:
+        ax.plot([p[0] for p in pts], [p[1] for p in pts], marker="o", color="black")
+    ax.set_xlabel("results trained on")
+    ax.set_ylabel("accuracy on all")
+    ax.set_ylim(0, 1.05)
+    fig.tight_layout()
+    fig.savefig(path)
+    plt.close(fig)
 
 
 def format_rules(rules, report) -> str:
@@ -270,10 +340,15 @@ def main(argv=None):
     ap.add_argument("--out", default="")
     ap.add_argument("--pctl", type=float, default=99.0)
     ap.add_argument("--eval", type=int, nargs="*", default=[50, 100, 200, 400])
+    ap.add_argument("--plots", action="store_true",
+                    help="also write the figures (classes, tree, eval) as PDFs next to --out")
     a = ap.parse_args(argv)
     results = load_results(a.results)
-    report, rules = process(results, a.pctl)
+    prefix = (a.out or "rules_") if a.plots else ""
+    report, rules = process(results, a.pctl, plots=prefix)
     report["eval"] = {str(n): evaluate_rules(results, n) for n in a.eval if n < len(results)}
+    if prefix:
+        plot_eval(report["eval"], prefix + "eval.pdf")
     text = format_rules(rules, report)
     sys.stdout.write(text)
     if a.out:

@@ -39,3 +39,22 @@ def test_peaks_on_step_data():
     t = t + rng.normal(0, 0.01, t.size)
     labels, bounds = pp.performance_classes(t, radius_frac=0.02, pctl=95)
     assert len(set(labels)) == 3
+
+
+def test_rules_cli_writes_the_reference_figures(tz, tmp_path):
+    """`rules --plots`: the class figure (sorted times, step response, boundaries), the decision
+    tree and the accuracy-vs-training-size figure, as the reference's postprocess.py draws"""
+    from tenzing_amd.utils import postprocess as pp
+
+    g = diamond(tz, a=10, b=200, c=200, d=10)
+    o = tz.DfsOpts()
+    o.bench = tz.BenchOpts(n_iters=2)
+    r = tz.dfs_explore(g, tz.Platform(2), tz.SimBenchmarker(2, tz.SimParams()), tz.SelfCtrl(), o)
+    path = tmp_path / "r.csv"
+    path.write_text(r.dump_csv())
+    prefix = str(tmp_path / "d_")
+    assert pp.main([str(path), "--out", prefix, "--plots", "--eval", "4", "8"]) == 0
+    for name in ("classes.pdf", "tree.pdf", "eval.pdf", "rules.txt", "classes.json"):
+        f = tmp_path / ("d_" + name)
+        assert f.exists() and f.stat().st_size > 0, name
+    assert (tmp_path / "d_classes.pdf").read_bytes()[:4] == b"%PDF"
