@@ -120,7 +120,7 @@ def main() -> int:
                          "the way the final number is measured; eager rankings can mislead, "
                          "profiles/r1_bench_loopback/)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--graph-unroll", type=int, default=10,
+    ap.add_argument("--graph-unroll", type=int, default=20,
                     help="iterations per hipGraph launch when timing the graph-compiled schedule")
     ap.add_argument("--rerank", type=int, default=4,
                     help="re-measure the K best distinct candidates interleaved, compiled as "
