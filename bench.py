@@ -122,6 +122,9 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--graph-unroll", type=int, default=20,
                     help="iterations per hipGraph launch when timing the graph-compiled schedule")
+    ap.add_argument("--search-graph-unroll", type=int, default=10,
+                    help="iterations per hipGraph launch while benchmarking candidates (shorter "
+                         "graphs compile faster; the ranking does not depend on it)")
     ap.add_argument("--rerank", type=int, default=4,
                     help="re-measure the K best distinct candidates interleaved, compiled as "
                          "hipGraphs, and keep the fastest (0: trust the search's ranking)")
@@ -158,7 +161,7 @@ def main() -> int:
     halo, graph = build_halo(cfg, ctrl, device)
     mode = tz.ExecMode.Graph if args.search_mode == "graph" else tz.ExecMode.Eager
     rt = tz.HipRuntime(device=device, n_streams=args.streams, mode=mode, watchdog_s=120.0,
-                       graph_unroll=args.graph_unroll if args.search_mode == "graph" else 1)
+                       graph_unroll=args.search_graph_unroll if args.search_mode == "graph" else 1)
     bench = tz.EmpiricalBenchmarker(rt, ctrl)
     setup_s = time.time() - t_setup
 
@@ -212,7 +215,7 @@ def main() -> int:
         # interleaved (drift spreads evenly), every candidate compiled to a hipGraph
         t_rr = time.time()
         rt.set_mode(tz.ExecMode.Graph)
-        rt.set_graph_unroll(args.graph_unroll)
+        rt.set_graph_unroll(args.search_graph_unroll)
         ok = 1.0
         try:
             rr = bench.benchmark_many(cands, tz.BenchOpts(n_iters=args.bench_iters, max_retries=1,
@@ -228,7 +231,7 @@ def main() -> int:
                       [p * 1e3 for p in payload["pct10"]], "chosen": k,
                       "wall_s": time.time() - t_rr}
         rt.set_mode(mode)
-        rt.set_graph_unroll(args.graph_unroll if mode == tz.ExecMode.Graph else 1)
+        rt.set_graph_unroll(args.search_graph_unroll if mode == tz.ExecMode.Graph else 1)
 
     # correctness of the winning schedule: one exchange from a fresh grid, every cell checked
     rt.set_mode(tz.ExecMode.Eager)
