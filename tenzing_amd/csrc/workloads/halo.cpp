@@ -163,6 +163,7 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   // copy-engine puts (buffers mode only): on unless TZ_IPC_COPY=0
   useCopy_ = useIpc_;
   if (const char *v = std::getenv("TZ_IPC_COPY")) useCopy_ = useCopy_ && std::atoi(v) != 0;
+  if (const char *v = std::getenv("TZ_COPY_ENGINES")) copyEngines_ = std::max(1, std::min(8, std::atoi(v)));
 
   // relay routing through the corner peer: a 2x2x2 grid (the only single-node grid where the
   // corner and edge-diagonal links idle while both faces of an axis share one link), ipc puts
@@ -190,6 +191,8 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
 }
 
 HaloExchange::~HaloExchange() {
+  for (void *e : copyEvents_) hipEventDestroy(static_cast<hipEvent_t>(e));
+  for (void *s : copyStreams_) hipStreamDestroy(static_cast<hipStream_t>(s));
   for (void *p : opened_) hipIpcCloseMemHandle(p);
   if (flags_) hipFree(flags_);
 }
@@ -338,6 +341,19 @@ void HaloExchange::setup(Ctrl *ctrl) {
                          << (relayWhy_.empty() ? " on another rank" : ": " + relayWhy_));
         TZ_CHECK(a_.relay != "force", "relay routing forced but unavailable: " << relayWhy_);
       }
+    }
+  }
+  if (useIpc_ && useCopy_ && !ipcGrid_) {
+    // the extra copy engines of copy-engine puts (and of the relay's copy-engine forward)
+    for (int k = 1; k < copyEngines_; ++k) {
+      hipStream_t st = nullptr;
+      TZ_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      copyStreams_.push_back(st);
+    }
+    for (int k = 0; k < copyEngines_; ++k) {
+      hipEvent_t ev = nullptr;
+      TZ_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      copyEvents_.push_back(ev);
     }
   }
   count_ = DeviceBuffer(sizeof(unsigned long long));

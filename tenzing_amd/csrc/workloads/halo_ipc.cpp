@@ -234,10 +234,44 @@ void HaloExchange::copy_put_group(const std::vector<int> &dirs, void *stream) co
   kern::ipc_wait(static_cast<const unsigned long long *>(flags_) + ndirs(), sent_.as<unsigned long long>(),
                  dirs.data(), int(dirs.size()), err_.as<int>(), ipcTimeoutS_, stream, /*lag=*/1);
   kern::box_copy_many(grid(), bs.data(), int(bs.size()), false, stream);
-  for (int i : dirs)
-    TZ_HIP(hipMemcpyAsync(peerRecv_[size_t(i)], send_[i].get(), box_elems(i) * sizeof(double),
-                          hipMemcpyDeviceToDevice, s));
+  std::vector<Copy> cs;
+  for (int i : dirs) cs.push_back({peerRecv_[size_t(i)], send_[i].get(), box_elems(i) * sizeof(double)});
+  engine_copies(cs, s);
   kern::ipc_signal(arrive.data(), int(arrive.size()), stream);
+}
+
+void HaloExchange::engine_copies(const std::vector<Copy> &copies, void *stream) const {
+  // Every copy is cut into one chunk per engine, chunk k on engine k: one SDMA engine cannot
+  // fill an xGMI link, several can. Chunks are whole 256-B multiples so every engine moves
+  // aligned spans. Engine 0 is the op's own stream; the others fork from it and join back,
+  // which stream capture records as plain graph edges.
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int E = 1 + int(copyStreams_.size());
+  auto copy = [](void *dst, const void *src, size_t n, hipStream_t st) {
+    if (n) TZ_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, st));
+  };
+  if (E == 1) {
+    for (const Copy &c : copies) copy(c.dst, c.src, c.bytes, s);
+    return;
+  }
+  hipEvent_t fork = static_cast<hipEvent_t>(copyEvents_[0]);
+  TZ_HIP(hipEventRecord(fork, s));
+  for (int k = 1; k < E; ++k) TZ_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(copyStreams_[size_t(k - 1)]), fork, 0));
+  for (const Copy &c : copies) {
+    const size_t per = (c.bytes / size_t(E) + 255) / 256 * 256;
+    for (int k = 0; k < E; ++k) {
+      const size_t off = size_t(k) * per;
+      if (off >= c.bytes) break;
+      hipStream_t st = k == 0 ? s : static_cast<hipStream_t>(copyStreams_[size_t(k - 1)]);
+      copy(static_cast<char *>(c.dst) + off, static_cast<const char *>(c.src) + off,
+           std::min(per, c.bytes - off), st);
+    }
+  }
+  for (int k = 1; k < E; ++k) {
+    hipEvent_t join = static_cast<hipEvent_t>(copyEvents_[size_t(k)]);
+    TZ_HIP(hipEventRecord(join, static_cast<hipStream_t>(copyStreams_[size_t(k - 1)])));
+    TZ_HIP(hipStreamWaitEvent(s, join, 0));
+  }
 }
 
 void HaloExchange::wait_group(const std::vector<int> &dirs, void *stream) const {
@@ -410,9 +444,9 @@ void HaloExchange::relay_forward(const std::vector<int> &faces, double frac, voi
   if (!sdma) {
     kern::box_move_many_signal(ms.data(), int(ms.size()), sig, stream);
   } else {
-    for (const kern::MoveDesc &m : ms)
-      TZ_HIP(hipMemcpyAsync(m.dst + m.dst_off, m.src, size_t(m.len) * sizeof(double),
-                            hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    std::vector<Copy> cs;
+    for (const kern::MoveDesc &m : ms) cs.push_back({m.dst + m.dst_off, m.src, size_t(m.len) * sizeof(double)});
+    engine_copies(cs, stream);
     // arrivals are published after the copies (stream order), like copy-engine puts
     for (size_t k = 0; k < faces.size(); ++k) credits.push_back(sig.flag[k]);
   }

@@ -294,6 +294,23 @@ private:
   std::vector<bool> direct_, ipc_, pipe_; // per direction: self move / IPC put / pack-transfer-unpack
   bool ipcReady_ = false;
   bool useCopy_ = false; // copy-engine puts offered (buffers mode)
+  // copy-engine puts can spread every copy over this many streams (one SDMA engine each; env
+  // TZ_COPY_ENGINES). One engine moves ~60 GB/s, and independent copies on 2 / 4 streams reach
+  // 120 / 235 GB/s. Forking the chunks from the op's stream and joining them back through events
+  // costs more than it gains (19 MB: 58 GB/s on one stream, 33 on two, 15 on four;
+  // scripts/sdma_probe.hip, profiles/r2_sdma/), so the default keeps one stream per op and
+  // leaves engine parallelism to the search (per-direction copy ops on different streams).
+  int copyEngines_ = 1;
+  std::vector<void *> copyStreams_; // engines 1.. (engine 0 is the op's stream)
+  std::vector<void *> copyEvents_;  // fork + one join per extra engine
+  struct Copy {
+    void *dst;
+    const void *src;
+    size_t bytes;
+  };
+  /// issue `copies` on the copy engines behind everything already on `stream`, and make
+  /// `stream` wait for all of them (fork / join through events; captures into hipGraphs)
+  void engine_copies(const std::vector<Copy> &copies, void *stream) const;
   // ipc transport state
   // counters per direction, uncached and IPC-exported, in kSlotSets sections of ndirs():
   // arrivals | credits | relay arrivals | relay credits | forwarded arrivals | forward credits
