@@ -371,18 +371,20 @@ PYBIND11_MODULE(_tz, m) {
 
   // ------------------------------------------------------------------ benchmark
   py::class_<BenchOpts>(m, "BenchOpts")
-      .def(py::init([](int64_t n, int r, double t, bool rs) {
+      .def(py::init([](int64_t n, int r, double t, bool rs, bool dev) {
         BenchOpts o;
         o.n_iters = n;
         o.max_retries = r;
         o.target_secs = t;
         o.small_sample = rs ? RunsTestSmall::Reject : RunsTestSmall::Accept;
+        o.device_timer = dev;
         return o;
       }), py::arg("n_iters") = 1000, py::arg("max_retries") = 10, py::arg("target_secs") = 0.01,
-         py::arg("reject_small_samples") = false)
+         py::arg("reject_small_samples") = false, py::arg("device_timer") = false)
       .def_readwrite("n_iters", &BenchOpts::n_iters)
       .def_readwrite("max_retries", &BenchOpts::max_retries)
-      .def_readwrite("target_secs", &BenchOpts::target_secs);
+      .def_readwrite("target_secs", &BenchOpts::target_secs)
+      .def_readwrite("device_timer", &BenchOpts::device_timer);
 
   py::class_<BenchResult>(m, "BenchResult")
       .def(py::init<>())

@@ -40,12 +40,14 @@ Json BenchOpts::json() const {
   j["nIters"] = n_iters;
   j["maxRetries"] = max_retries;
   j["targetSecs"] = target_secs;
+  if (device_timer) j["deviceTimer"] = true;
   return j;
 }
 
 // ---------------------------------------------------------------- Empirical
 
-EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, double targetSecs) {
+EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, double targetSecs,
+                                                                bool deviceTimer) {
   Measurement m{std::max<int64_t>(1, nHint), 0};
   while (true) {
     ctrl_.barrier();
@@ -54,12 +56,14 @@ EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, d
     // with the time in the same max-reduction, so every rank throws together and the next
     // collective still matches
     std::string err;
+    double dev = -1.0;
     try {
-      runner_.run(m.n);
+      if (deviceTimer) dev = runner_.run_device_timed(m.n);
+      else runner_.run(m.n);
     } catch (const std::exception &e) {
       err = e.what();
     }
-    double red[2] = {wtime() - t0, err.empty() ? 0.0 : 1.0};
+    double red[2] = {dev >= 0 ? dev : wtime() - t0, err.empty() ? 0.0 : 1.0};
     ctrl_.allreduce_max(red, 2); // "true" time is the max over ranks
     if (red[1] != 0.0)
       throw CandidateFailed("schedule run failed" +
@@ -99,11 +103,11 @@ BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts
   int retries = 0;
   int64_t hint = 1;
   for (int left = opts.max_retries; opts.max_retries == 0 || left > 0; --left) {
-    Measurement m = measure(1, opts.target_secs); // warm-up and size the batch
+    Measurement m = measure(1, opts.target_secs, opts.device_timer); // warm-up, size the batch
     hint = m.n;
     times.clear();
     for (int64_t i = 0; i < opts.n_iters; ++i) {
-      m = measure(hint, opts.target_secs);
+      m = measure(hint, opts.target_secs, opts.device_timer);
       hint = std::max(hint, m.n);
       times.push_back(m.time);
     }
@@ -131,7 +135,7 @@ std::vector<BenchResult> EmpiricalBenchmarker::benchmark_many(const std::vector<
   std::vector<int64_t> hint(k, 1);
   for (size_t i = 0; i < k; ++i) {
     runner_.select(i);
-    hint[i] = measure(1, opts.target_secs).n;
+    hint[i] = measure(1, opts.target_secs, opts.device_timer).n;
   }
   std::vector<std::vector<double>> times(k);
   std::mt19937_64 rng(seed + 0x5EEDull);
@@ -148,7 +152,7 @@ std::vector<BenchResult> EmpiricalBenchmarker::benchmark_many(const std::vector<
     std::memcpy(perm.data(), msg.data(), msg.size());
     for (int i : perm) {
       runner_.select(size_t(i));
-      Measurement m = measure(hint[size_t(i)], opts.target_secs);
+      Measurement m = measure(hint[size_t(i)], opts.target_secs, opts.device_timer);
       hint[size_t(i)] = std::max(hint[size_t(i)], m.n);
       times[size_t(i)].push_back(m.time);
     }

@@ -35,6 +35,9 @@ struct BenchOpts {
   int max_retries = 10;        // runs-test retries (reference Opts::maxRetries)
   double target_secs = 0.01;   // each measurement batches runs to at least this wall time
   RunsTestSmall small_sample = RunsTestSmall::Accept;
+  // time each measurement with device events around the batch (GPU time, no host issue or
+  // wake-up latency) when the runner has them; false: host wall clock, like the reference
+  bool device_timer = false;
   Json json() const;
 };
 
@@ -57,6 +60,12 @@ public:
   /// (interleaved benchmarking). Default: re-prepare on every select.
   virtual void prepare_many(const std::vector<Sequence> &seqs) { many_ = seqs; }
   virtual void select(size_t k) { prepare(many_.at(k)); }
+  /// runners with a device clock: run `n` times and return the device time in seconds
+  /// between an event before the first op and one after the last (or < 0 if unsupported)
+  virtual double run_device_timed(int64_t n) {
+    run(n);
+    return -1.0;
+  }
 
 private:
   std::vector<Sequence> many_;
@@ -78,7 +87,7 @@ private:
     int64_t n;
     double time;
   };
-  Measurement measure(int64_t nHint, double targetSecs);
+  Measurement measure(int64_t nHint, double targetSecs, bool deviceTimer = false);
   void collective_prepare(const std::function<void()> &fn);
   ExecutorRunner &runner_;
   Ctrl &ctrl_;

@@ -115,6 +115,8 @@ HipRuntime::~HipRuntime() {
   destroy_graph();
   for (void *e : events_) hipEventDestroy(E(e));
   for (void *e : internal_) hipEventDestroy(E(e));
+  for (void *e : timerEv_)
+    if (e) hipEventDestroy(E(e));
   for (void *s : streams_) hipStreamDestroy(S(s));
 }
 
@@ -384,6 +386,22 @@ void HipRuntime::select(size_t k) {
   graphNodes_ = s.nodes;
   graphEdges_ = s.edges;
   internalUsed_ = 0;
+}
+
+double HipRuntime::run_device_timed(int64_t n) {
+  for (void *&e : timerEv_)
+    if (!e) {
+      hipEvent_t ev;
+      TZ_HIP(hipEventCreate(&ev));
+      e = ev;
+    }
+  TZ_HIP(hipEventRecord(E(timerEv_[0]), S(streams_[0])));
+  run(n);
+  TZ_HIP(hipEventRecord(E(timerEv_[1]), S(streams_[0])));
+  TZ_HIP(hipEventSynchronize(E(timerEv_[1])));
+  float ms = 0;
+  TZ_HIP(hipEventElapsedTime(&ms, E(timerEv_[0]), E(timerEv_[1])));
+  return double(ms) * 1e-3;
 }
 
 std::vector<HipRuntime::Span> HipRuntime::trace(const Sequence &seq, int iterations) {

@@ -67,6 +67,9 @@ public:
   // ExecutorRunner
   void prepare(const Sequence &seq) override;
   void run(int64_t n) override;
+  /// run(n) bracketed by timing events on stream 0 (every op of a schedule follows the first
+  /// event, and the schedule's closing host syncs precede the last): device seconds
+  double run_device_timed(int64_t n) override;
   /// graph mode: every sequence is compiled once and kept; select() switches without rebuilding
   void prepare_many(const std::vector<Sequence> &seqs) override;
   void select(size_t k) override;
@@ -117,6 +120,7 @@ private:
   std::vector<void *> streams_;
   std::vector<void *> events_;   // schedule events
   std::vector<void *> internal_; // StreamWait helpers
+  void *timerEv_[2] = {nullptr, nullptr};
   size_t internalUsed_ = 0;
   Sequence seq_;
   void *graphExec_ = nullptr;  // one iteration

@@ -255,3 +255,16 @@ def test_put_block_cap_tunable(tz):
             k.set_put_max_blocks(0)
     finally:
         k.set_put_max_blocks(prev)
+
+
+def test_device_timer_falls_back_to_host_clock(tz):
+    """runners without a device clock (host executor) keep the host wall clock"""
+    g = tz.Graph()
+    a = tz.SleepOp("a", 300.0)
+    g.start_then(a)
+    g.then_finish(a)
+    seq = tz.random_rollout(tz.State(g, tz.Platform(1)), 0)
+    b = tz.EmpiricalBenchmarker(tz.HostExecutor(1), tz.SelfCtrl())
+    o = tz.BenchOpts(n_iters=3, max_retries=1, target_secs=0.002, device_timer=True)
+    assert o.device_timer
+    assert b.benchmark(seq, o).pct10 > 250e-6

@@ -444,3 +444,26 @@ def test_watchdog_turns_a_hang_into_an_error(tz, gpu):
     fast.then_finish(k)
     rt.prepare(tz.random_rollout(tz.State(fast, tz.Platform(1)), 0))
     rt.run(3)
+
+
+def test_device_timer_measures_gpu_time(tz, gpu):
+    """BenchOpts(device_timer=True): each measurement is the device time between events around
+    the batch, so a 200 us kernel measures ~200 us without the host's issue and wake-up cost
+    (host wall clock is never below it)"""
+    g = tz.Graph()
+    k = tz.BusyKernelOp("k", 200.0)
+    g.start_then(k)
+    g.then_finish(k)
+    seq = tz.random_rollout(tz.State(g, tz.Platform(1)), 0)
+    res = {}
+    for dev in (False, True):
+        for mode in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+            rt = tz.HipRuntime(device=0, n_streams=1, mode=mode)
+            b = tz.EmpiricalBenchmarker(rt, tz.SelfCtrl())
+            r = b.benchmark(seq, tz.BenchOpts(n_iters=5, max_retries=1, target_secs=0.005,
+                                              device_timer=dev))
+            res[(dev, str(mode))] = r.pct10
+    for mode in ("ExecMode.Eager", "ExecMode.Graph"):
+        d, h = res[(True, mode)], res[(False, mode)]
+        assert 190e-6 < d < 240e-6, res
+        assert h >= d * 0.98, res
