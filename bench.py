@@ -44,7 +44,7 @@ def _start_deadline(seconds: float) -> None:
     t.start()
 
 
-def link_probe(tz, halo, ctrl, iters):
+def link_probe(tz, halo, ctrl, iters, rccl=False):
     """GB/s of ONE transfer over one xGMI link with each available transport (the +z face to
     the +z neighbour, every rank at once, one transfer at a time), and the time the exchange's
     busiest link (the peer receiving the most bytes) would take at the best of those rates. An
@@ -58,7 +58,7 @@ def link_probe(tz, halo, ctrl, iters):
         return None
     face = 8.0 * halo.box_elems(i)
     rates = {}
-    for via in ("put", "sdma", "rccl"):
+    for via in ("put", "sdma") + (("rccl",) if rccl else ()):
         try:
             t = halo.link_probe(i, via, iters, ctrl)
             rates[via] = face / t / 1e9
@@ -132,6 +132,9 @@ def main() -> int:
     ap.add_argument("--link-probe-iters", type=int, default=20,
                     help="several ranks: after the timing, measure what one xGMI link carries "
                          "per transport (one face to one peer at a time; 0 = skip)")
+    ap.add_argument("--link-probe-rccl", action="store_true",
+                    help="also probe RCCL (off by default: an RCCL transfer has no device-side "
+                         "timeout, and a hang there would cost the whole run's output)")
     ap.add_argument("--deadline-s", type=float, default=1500.0,
                     help="abort (exit 4) if the whole run takes longer (hung collective)")
     args = ap.parse_args()
@@ -284,7 +287,7 @@ def main() -> int:
     # not beat the bytes its busiest link carries divided by what one link moves)
     probe = None
     if world > 1 and args.link_probe_iters > 0:
-        probe = link_probe(tz, halo, ctrl, args.link_probe_iters)
+        probe = link_probe(tz, halo, ctrl, args.link_probe_iters, args.link_probe_rccl)
 
     names = [o.name for o in best.ops()]
     via = [t for t, key in (("direct", "he_direct_"), ("rccl", "he_shift_"), ("ipc", "he_put_"),
