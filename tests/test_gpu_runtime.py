@@ -465,5 +465,5 @@ def test_device_timer_measures_gpu_time(tz, gpu):
             res[(dev, str(mode))] = r.pct10
     for mode in ("ExecMode.Eager", "ExecMode.Graph"):
         d, h = res[(True, mode)], res[(False, mode)]
-        assert 190e-6 < d < 240e-6, res
+        assert 190e-6 < d < 260e-6, res
         assert h >= d * 0.98, res
