@@ -856,13 +856,15 @@ PYBIND11_MODULE(_tz, m) {
     kern::box_tuning().max_blocks = maxBlocks;
     kern::box_tuning().nt_move = ntMove;
   }, py::arg("unroll") = 4, py::arg("nt_pack") = true, py::arg("nt_unpack") = false,
-     py::arg("max_blocks") = 4096, py::arg("nt_move") = true);
+     py::arg("max_blocks") = 4096, py::arg("nt_move") = false);
   k.def("set_xcd_remap", &kern::set_xcd_remap, py::arg("mode"));
   k.def("set_put_max_blocks", [](int b) {
     TZ_CHECK(b >= 1, "put_max_blocks must be positive");
     kern::box_tuning().put_max_blocks = b;
   }, py::arg("blocks"));
   k.def("get_put_max_blocks", []() { return kern::box_tuning().put_max_blocks; });
+  k.def("set_nt_move_store", [](bool on) { kern::box_tuning().nt_move_store = on; }, py::arg("on"));
+  k.def("get_nt_move_store", []() { return kern::box_tuning().nt_move_store; });
   k.def("get_xcd_remap", []() { return kern::box_tuning().xcd_remap; });
   k.def("get_box_tuning", []() {
     const auto &t = kern::box_tuning();

@@ -39,6 +39,8 @@ BoxTuning &box_tuning() {
   static BoxTuning t = [] {
     BoxTuning v;
     if (const char *e = std::getenv("TZ_PUT_MAX_BLOCKS")) v.put_max_blocks = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("TZ_NT_MOVE_STORE")) v.nt_move_store = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TZ_NT_MOVE_LOAD")) v.nt_move = std::atoi(e) != 0;
     if (const char *e = std::getenv("TZ_XCD_REMAP")) {
       const int m = std::atoi(e);
       if (m >= 0 && m <= 2) v.xcd_remap = m;
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(kThreads) void box_copy_many_k(double *__restrict__
 }
 
 // direct move: src box -> dst box of the same layout (both rows addressed by one index)
-template <int VEC, int U, bool NT>
+template <int VEC, int U, bool NT, bool NTS = false>
 __device__ __forceinline__ void move_body(const DevDesc &d, uint32_t tid, uint32_t nthreads) {
   using T = typename Vec<VEC>::T;
   const double *__restrict__ src = d.src;
@@ -237,15 +239,15 @@ __device__ __forceinline__ void move_body(const DevDesc &d, uint32_t tid, uint32
 #pragma unroll
     for (int k = 0; k < U; ++k) v[k] = ld<NT>(reinterpret_cast<const T *>(src + g[k]));
 #pragma unroll
-    for (int k = 0; k < U; ++k) *reinterpret_cast<T *>(dst + g[k]) = v[k];
+    for (int k = 0; k < U; ++k) st<NTS>(reinterpret_cast<T *>(dst + g[k]), v[k]);
   }
   for (; it < d.items; it += nthreads) {
     const int64_t g = grid_index<VEC>(d, it);
-    *reinterpret_cast<T *>(dst + g) = ld<NT>(reinterpret_cast<const T *>(src + g));
+    st<NTS>(reinterpret_cast<T *>(dst + g), ld<NT>(reinterpret_cast<const T *>(src + g)));
   }
 }
 
-template <int U, bool NT>
+template <int U, bool NT, bool NTS>
 __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap r) {
   const uint32_t lb = logical_block(r);
   if (lb >= r.total) return; // padding of the remapped launch (no barriers in this kernel)
@@ -261,8 +263,8 @@ __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap
   }
   const uint32_t tid = j * kThreads + threadIdx.x;
   const uint32_t nth = nb * kThreads;
-  if (d.vec == 2) move_body<2, U, NT>(d, tid, nth);
-  else move_body<1, U, NT>(d, tid, nth);
+  if (d.vec == 2) move_body<2, U, NT, NTS>(d, tid, nth);
+  else move_body<1, U, NT, NTS>(d, tid, nth);
 }
 
 struct DevSignal {
@@ -581,8 +583,15 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
   r.total = total;
   r.per_xcd = mode == 1 ? (total + 7) / 8 : 0;
   const dim3 g(r.per_xcd ? r.per_xcd * 8 : total);
-  if (box_tuning().nt_move) hipLaunchKernelGGL((box_move_many_k<4, true>), g, dim3(kThreads), 0, s, b, r);
-  else hipLaunchKernelGGL((box_move_many_k<4, false>), g, dim3(kThreads), 0, s, b, r);
+  const BoxTuning &t = box_tuning();
+  if (t.nt_move && t.nt_move_store)
+    hipLaunchKernelGGL((box_move_many_k<4, true, true>), g, dim3(kThreads), 0, s, b, r);
+  else if (t.nt_move)
+    hipLaunchKernelGGL((box_move_many_k<4, true, false>), g, dim3(kThreads), 0, s, b, r);
+  else if (t.nt_move_store)
+    hipLaunchKernelGGL((box_move_many_k<4, false, true>), g, dim3(kThreads), 0, s, b, r);
+  else
+    hipLaunchKernelGGL((box_move_many_k<4, false, false>), g, dim3(kThreads), 0, s, b, r);
   TZ_HIP_LAUNCH_CHECK();
 }
 

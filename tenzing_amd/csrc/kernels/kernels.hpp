@@ -34,7 +34,13 @@ struct BoxTuning {
   // stores cover with a wide margin, while thousands of blocks stalled on a link would hold the
   // CU slots that the concurrent local moves, relay kernels and unpacks need
   int put_max_blocks = 64;
-  bool nt_move = true;    // non-temporal source loads in box_move (direct transfers)
+  // box_move (direct transfers): plain source loads and non-temporal ghost stores. The ghosts
+  // are written once per exchange and nobody reads them inside it, so streaming them past the
+  // caches leaves L2 / Infinity Cache to the interior slabs, which every exchange reads again:
+  // 47.7 -> 44.4 us for the 26-direction move at 512^3 x 3 (scripts/move_ab.py; non-temporal
+  // loads plus stores: 57.7 us). Env TZ_NT_MOVE_LOAD / TZ_NT_MOVE_STORE override.
+  bool nt_move = false;
+  bool nt_move_store = true;
   int xcd_remap = 0; // box_move block order: 0 round-robin, 1 one contiguous range per XCD,
                      // 2 every box split into 8 contiguous per-XCD shares
 };

@@ -204,3 +204,37 @@ def test_stencil7_matches_torch(tz, gpu, order, lds, nx, stencil_tuning):
     assert torch.allclose(got, ref, rtol=1e-13, atol=1e-13), (got - ref).abs().max()
     # nothing outside the box is written
     assert float(O.abs().sum()) == pytest.approx(float(got.abs().sum()), rel=1e-12)
+
+
+@pytest.mark.parametrize("ntload,ntstore", [(False, False), (False, True), (True, False), (True, True)])
+def test_box_move_cache_policies(tz, gpu, ntload, ntstore):
+    """every load / store cache policy of the move kernel moves the same data"""
+    a = tz.HaloArgs()
+    a.nx, a.ny, a.nz, a.ghost, a.nq = 64, 40, 24, 3, 3
+    a.neighbors, a.order = 26, "qxyz"
+    h = tz.HaloExchange(a)
+    grid = torch.randn(h.grid_elems(), dtype=torch.float64, device="cuda")
+    out, exp = grid.clone(), grid.clone()
+    moves = []
+    for i in range(h.ndirs()):
+        s, d = h.pack_box(i), h.unpack_box(h.opposite(i))
+        moves.append(dict(src=out.data_ptr(), dst=out.data_ptr(), src_off=s["grid_off"],
+                          dst_off=d["grid_off"], s1=s["s1"], s2=s["s2"], s3=s["s3"],
+                          len=s["len"], n1=s["n1"], n2=s["n2"], n3=s["n3"]))
+        for i3 in range(s["n3"]):
+            for i2 in range(s["n2"]):
+                so = s["grid_off"] + i2 * s["s2"] + i3 * s["s3"]
+                do = d["grid_off"] + i2 * s["s2"] + i3 * s["s3"]
+                exp.as_strided((s["n1"], s["len"]), (s["s1"], 1), do).copy_(
+                    grid.as_strided((s["n1"], s["len"]), (s["s1"], 1), so))
+    k = tz._tz.kernels
+    prev, prev_st = k.get_box_tuning(), k.get_nt_move_store()
+    try:
+        k.set_box_tuning(prev[0], prev[1], prev[2], prev[3], ntload)
+        k.set_nt_move_store(ntstore)
+        k.box_move_many(moves, _stream())
+        torch.cuda.synchronize()
+    finally:
+        k.set_box_tuning(*prev)
+        k.set_nt_move_store(prev_st)
+    assert torch.equal(out, exp)
