@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--extra", action="store_true", help="also unroll / XCD order / block caps")
     a = ap.parse_args()
     torch.zeros(1, device="cuda")
     h, _ = build_halo(HaloConfig(n=a.n, neighbors=26, order="qxyz", transport="direct"),
@@ -29,13 +30,22 @@ def main():
     st = torch.cuda.current_stream()
     dirs = list(range(h.ndirs()))
     unroll, ntp, ntu, mb, ntm = k.get_box_tuning()
-    variants = {"base": (True, False), "nt_store": (True, True), "no_nt": (False, False),
-                "nt_store_only": (False, True)}
+    # name: (nt loads, nt stores, unroll, xcd remap, max blocks per box)
+    variants = {"r1_default": (True, False, 4, 0, 4096), "nt_both": (True, True, 4, 0, 4096),
+                "plain": (False, False, 4, 0, 4096), "default": (False, True, 4, 0, 4096)}
+    if a.extra:
+        variants.update({"default_u8": (False, True, 8, 0, 4096),
+                         "default_remap1": (False, True, 4, 1, 4096),
+                         "default_remap2": (False, True, 4, 2, 4096),
+                         "default_mb1024": (False, True, 4, 0, 1024),
+                         "default_mb16384": (False, True, 4, 0, 16384)})
     res = {v: [] for v in variants}
+    prev_remap = k.get_xcd_remap()
     for r in range(a.rounds):
-        for name, (ntload, ntstore) in variants.items():
-            k.set_box_tuning(unroll, ntp, ntu, mb, ntload)
+        for name, (ntload, ntstore, u, remap, mbv) in variants.items():
+            k.set_box_tuning(u, ntp, ntu, mbv, ntload)
             k.set_nt_move_store(ntstore)
+            k.set_xcd_remap(remap)
             for _ in range(5):
                 h.direct_group(dirs, st.cuda_stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -46,7 +56,8 @@ def main():
             e1.synchronize()
             res[name].append(e0.elapsed_time(e1) * 1e3 / a.reps)
     k.set_box_tuning(unroll, ntp, ntu, mb, ntm)
-    k.set_nt_move_store(False)
+    k.set_nt_move_store(True)
+    k.set_xcd_remap(prev_remap)
     h.init_grid()
     h.direct_group(dirs, st.cuda_stream)
     torch.cuda.synchronize()
