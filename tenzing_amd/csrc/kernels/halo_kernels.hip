@@ -41,6 +41,8 @@ BoxTuning &box_tuning() {
     if (const char *e = std::getenv("TZ_PUT_MAX_BLOCKS")) v.put_max_blocks = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("TZ_NT_MOVE_STORE")) v.nt_move_store = std::atoi(e) != 0;
     if (const char *e = std::getenv("TZ_NT_MOVE_LOAD")) v.nt_move = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TZ_NT_PACK")) v.nt_pack = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TZ_NT_UNPACK")) v.nt_unpack = std::atoi(e) != 0;
     if (const char *e = std::getenv("TZ_XCD_REMAP")) {
       const int m = std::atoi(e);
       if (m >= 0 && m <= 2) v.xcd_remap = m;
