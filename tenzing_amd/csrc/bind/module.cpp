@@ -855,7 +855,7 @@ PYBIND11_MODULE(_tz, m) {
     kern::box_tuning().nt_unpack = ntUnpack;
     kern::box_tuning().max_blocks = maxBlocks;
     kern::box_tuning().nt_move = ntMove;
-  }, py::arg("unroll") = 4, py::arg("nt_pack") = true, py::arg("nt_unpack") = false,
+  }, py::arg("unroll") = 4, py::arg("nt_pack") = true, py::arg("nt_unpack") = true,
      py::arg("max_blocks") = 4096, py::arg("nt_move") = false);
   k.def("set_xcd_remap", &kern::set_xcd_remap, py::arg("mode"));
   k.def("set_put_max_blocks", [](int b) {

@@ -27,7 +27,11 @@ constexpr int kMaxBoxes = 32;
 struct BoxTuning {
   int unroll = 4;         // items in flight per lane: 4 or 8 (8: no gain, scripts/ktune.py)
   bool nt_pack = true;    // non-temporal grid loads in pack: -27 % pack time in pipeline context
-  bool nt_unpack = false; // non-temporal grid stores in unpack: +5 % (off)
+  // non-temporal ghost stores in unpack: the ghosts are not read again within the exchange.
+  // Round 1 measured +5 % on the one-rank pack -> copy -> unpack chain; the receive-buffer
+  // unpack of the multi-rank exchange gains 7-8 % (2 loopback ranks, 0.228-0.239 -> 0.210-0.218
+  // ms, scripts/nt_multi_ab.sh, profiles/r2_nt/)
+  bool nt_unpack = true;
   int max_blocks = 4096;  // cap per box (grid-stride beyond)
   // cap per box of the signalling put kernels, whose stores cross xGMI (env
   // TZ_PUT_MAX_BLOCKS): one link moves ~77 GB/s per direction, which 64 blocks of posted 16-B
