@@ -114,6 +114,9 @@ def main() -> int:
     # (profiles/r1_search_len/)
     ap.add_argument("--bench-iters", type=int, default=6)
     ap.add_argument("--target-secs", type=float, default=0.002)
+    ap.add_argument("--race-ratio", type=float, default=1.25,
+                    help="stop measuring a candidate once race-min measurements are all slower "
+                         "than this times the best so far (0 = measure every candidate fully)")
     ap.add_argument("--strategy", default="FastMin")
     ap.add_argument("--search-mode", default="graph", choices=["eager", "graph"],
                     help="benchmark candidates eagerly or compiled to hipGraphs (default: graph, "
@@ -173,7 +176,8 @@ def main() -> int:
     opts.time_budget_s = args.search_budget_s
     opts.strategy = args.strategy
     opts.seed = args.seed
-    opts.bench = tz.BenchOpts(n_iters=args.bench_iters, max_retries=3, target_secs=args.target_secs)
+    opts.bench = tz.BenchOpts(n_iters=args.bench_iters, max_retries=3, target_secs=args.target_secs,
+                              race_ratio=args.race_ratio)
     platform = tz.Platform(n_streams=args.streams)
     # candidates that cannot be compiled to a hipGraph are skipped by the search (every rank
     # agrees: preparation is collective); if none could be measured, search eagerly instead
@@ -327,6 +331,7 @@ def main() -> int:
             "search_wall_s": search_wall,
             "mcts_candidates": payload["n_sims"],
             "mcts_skipped": payload["failed"],
+            "mcts_raced": bench.raced,
             "mcts_tree_nodes": payload["tree"],
             "search_mode": "hipgraph" if mode == tz.ExecMode.Graph else "eager",
             "search_best_pct10_ms": best_pct10 * 1e3,

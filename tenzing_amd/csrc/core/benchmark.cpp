@@ -41,6 +41,7 @@ Json BenchOpts::json() const {
   j["maxRetries"] = max_retries;
   j["targetSecs"] = target_secs;
   if (device_timer) j["deviceTimer"] = true;
+  if (race_ratio > 0) j["raceRatio"] = race_ratio;
   return j;
 }
 
@@ -106,10 +107,21 @@ BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts
     Measurement m = measure(1, opts.target_secs, opts.device_timer); // warm-up, size the batch
     hint = m.n;
     times.clear();
+    bool raced = false;
     for (int64_t i = 0; i < opts.n_iters; ++i) {
       m = measure(hint, opts.target_secs, opts.device_timer);
       hint = std::max(hint, m.n);
       times.push_back(m.time);
+      if (opts.race_ratio > 0 && best_ > 0 && int64_t(times.size()) >= opts.race_min &&
+          i + 1 < opts.n_iters &&
+          *std::min_element(times.begin(), times.end()) > opts.race_ratio * best_) {
+        raced = true; // clearly slower than the best so far: enough to rank it
+        break;
+      }
+    }
+    if (raced) {
+      ++raced_;
+      break;
     }
     // per-measurement times are already maxed across ranks inside measure()
     if (compound_test(times, opts.small_sample) && left > 1) {
@@ -122,6 +134,7 @@ BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts
   BenchResult r = BenchResult::from_times(times);
   r.samples_per_measurement = hint;
   r.retries = retries;
+  if (int64_t(times.size()) == opts.n_iters && (best_ == 0.0 || r.pct10 < best_)) best_ = r.pct10;
   return r;
 }
 

@@ -38,6 +38,11 @@ struct BenchOpts {
   // time each measurement with device events around the batch (GPU time, no host issue or
   // wake-up latency) when the runner has them; false: host wall clock, like the reference
   bool device_timer = false;
+  // racing: once `race_min` measurements of a candidate are all slower than race_ratio x the
+  // best pct10 this benchmarker has seen, stop measuring it (a search only needs to know it is
+  // bad). 0 = off. Every rank sees the same max-over-ranks times, so all stop together.
+  double race_ratio = 0.0;
+  int race_min = 2;
   Json json() const;
 };
 
@@ -81,6 +86,10 @@ public:
   /// the schedules instead of biasing whichever ran last. Times are max over ranks.
   std::vector<BenchResult> benchmark_many(const std::vector<Sequence> &seqs, const BenchOpts &opts,
                                           uint64_t seed = 0);
+  /// candidates cut short by racing so far
+  int64_t raced() const { return raced_; }
+  /// forget the best time racing compares against
+  void reset_race() { best_ = 0.0; }
 
 private:
   struct Measurement {
@@ -91,6 +100,8 @@ private:
   void collective_prepare(const std::function<void()> &fn);
   ExecutorRunner &runner_;
   Ctrl &ctrl_;
+  double best_ = 0.0; // best complete pct10 seen (racing); identical on every rank
+  int64_t raced_ = 0;
 };
 
 /// Host-only executor: GPU ops are launched with a null stream, synchronously (tests/CPU runs).

@@ -268,3 +268,22 @@ def test_device_timer_falls_back_to_host_clock(tz):
     o = tz.BenchOpts(n_iters=3, max_retries=1, target_secs=0.002, device_timer=True)
     assert o.device_timer
     assert b.benchmark(seq, o).pct10 > 250e-6
+
+
+def test_racing_cuts_slow_candidates_short(tz):
+    """BenchOpts.race_ratio: after the fast alternative has a complete measurement, clearly
+    slower candidates stop after race_min measurements; the best one keeps full statistics"""
+    g = tz.Graph()
+    alts = [tz.SleepOp("fast", 100.0), tz.SleepOp("slow", 900.0), tz.SleepOp("slower", 1500.0)]
+    c = tz.StaticChoiceOp("pick", alts)
+    g.start_then(c)
+    g.then_finish(c)
+    b = tz.EmpiricalBenchmarker(tz.HostExecutor(1), tz.SelfCtrl())
+    o = tz.DfsOpts()
+    o.bench = tz.BenchOpts(n_iters=6, max_retries=1, target_secs=0.002, race_ratio=1.5)
+    r = tz.dfs_explore(g, tz.Platform(1), b, tz.SelfCtrl(), o)
+    names = [[op.name for op in s.seq.ops()] for s in r.sims]
+    t = {next(n for n in ns if n in ("fast", "slow", "slower")): s.res.pct10 for ns, s in zip(names, r.sims)}
+    assert t["fast"] < t["slow"] < t["slower"]
+    # DFS takes the alternatives in order: fast first, then both slower ones are raced
+    assert names[0] == ["Start", "fast", "Finish"] and b.raced == 2

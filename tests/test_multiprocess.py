@@ -251,3 +251,27 @@ def test_relay_search_8_ranks_sim(tmp_path):
     assert [p.returncode for p in procs] == [0] * 8, [o[1][-1500:] for o in outs]
     rows = (tmp_path / "r0.csv").read_text().strip().splitlines()[1:]
     assert len(rows) == 12 and all('"he_rl' in row for row in rows)
+
+
+def body_racing_two_ranks():
+    """racing decides on max-over-ranks times, so both ranks stop the same candidates"""
+    import tenzing_amd as tz
+    from tenzing_amd.parallel import init_ctrl
+
+    c = init_ctrl(timeout_s=60)
+    g = tz.Graph()
+    alts = [tz.SleepOp("fast", 100.0 * (1 + c.rank)), tz.SleepOp("slow", 1200.0),
+            tz.SleepOp("slower", 2000.0)]
+    ch = tz.StaticChoiceOp("pick", alts)
+    g.start_then(ch)
+    g.then_finish(ch)
+    b = tz.EmpiricalBenchmarker(tz.HostExecutor(1), c)
+    o = tz.DfsOpts()
+    o.bench = tz.BenchOpts(n_iters=5, max_retries=1, target_secs=0.002, race_ratio=1.5)
+    r = tz.dfs_explore(g, tz.Platform(1), b, c, o)
+    return dict(rank=c.rank, n=len(r.sims), raced=b.raced)
+
+
+def test_racing_is_collective(tmp_path):
+    rs = _run("body_racing_two_ranks", 2, tmp_path)
+    assert rs[0]["n"] == 3 and rs[0]["raced"] == rs[1]["raced"] == 2
