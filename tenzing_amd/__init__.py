@@ -52,10 +52,15 @@ def _load_native():
 _tz = _load_native()
 
 from ._tz import (  # noqa: E402,F401
+    AllGatherOp,
+    AllReduceOp,
+    AlltoallvOp,
     BenchOpts,
     BenchResult,
     BoundGpuOp,
+    BroadcastOp,
     BusyKernelOp,
+    CommOp,
     CsvBenchmarker,
     Ctrl,
     DfsOpts,
@@ -80,7 +85,9 @@ from ._tz import (  # noqa: E402,F401
     PyCpuOp,
     PyGpuOp,
     RcclComm,
+    ReduceScatterOp,
     SelfCtrl,
+    SendRecvOp,
     Sequence,
     SimBenchmarker,
     SimExecutor,

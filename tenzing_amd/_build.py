@@ -26,7 +26,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("TZ_OFFLOAD_ARCH", "gfx950")
 
 CORE = ["json", "numeric", "ops", "graph", "state", "serdes", "ctrl", "benchmark", "solve"]
-HIP_HOST = ["hip_runtime", "rccl_comm", "rocsparse_spmv"]
+HIP_HOST = ["hip_runtime", "rccl_comm", "comm_ops", "rocsparse_spmv"]
 WORKLOADS = ["halo", "halo_ipc", "halo_graph", "halo_stencil", "spmv", "workloads_common"]
 KERNELS = ["halo_kernels", "spmv_kernels", "stencil_kernels"]
 

@@ -7,6 +7,7 @@
 
 #include "core/benchmark.hpp"
 #include "core/solve.hpp"
+#include "hip/comm_ops.hpp"
 #include "hip/hip_runtime.hpp"
 #include "hip/rccl_comm.hpp"
 #include "hip/rocsparse_spmv.hpp"
@@ -131,6 +132,17 @@ py::dict box_to_dict(const kern::BoxDesc &b) {
 }
 
 void *P(uintptr_t p) { return reinterpret_cast<void *>(p); }
+
+/// hold a Python object (the tensors behind an op's raw pointers) from C++; released under
+/// the GIL whenever the last C++ owner lets go
+std::shared_ptr<void> py_keep(py::object o) {
+  if (o.is_none()) return nullptr;
+  auto *p = new py::object(std::move(o));
+  return std::shared_ptr<void>(p, [](void *q) {
+    py::gil_scoped_acquire g;
+    delete static_cast<py::object *>(q);
+  });
+}
 
 // native backtrace on a fatal signal, then chain to the previous handler (Python faulthandler)
 struct sigaction g_prevSegv, g_prevAbrt;
@@ -624,9 +636,78 @@ PYBIND11_MODULE(_tz, m) {
       .def("sendrecv", [](const RcclComm &c, uintptr_t sb, size_t sc, int sp, uintptr_t rb, size_t rc, int rp, int dt, uintptr_t s) {
         c.sendrecv(P(sb), sc, sp, P(rb), rc, rp, dt, P(s));
       })
+      .def("allreduce", [](const RcclComm &c, uintptr_t sb, uintptr_t rb, size_t n, int dt, int red, uintptr_t s) {
+        c.allreduce(P(sb), P(rb), n, dt, red, P(s));
+      }, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"), py::arg("red") = 0, py::arg("stream") = 0)
+      .def("allgather", [](const RcclComm &c, uintptr_t sb, uintptr_t rb, size_t n, int dt, uintptr_t s) {
+        c.allgather(P(sb), P(rb), n, dt, P(s));
+      }, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"), py::arg("stream") = 0)
+      .def("reduce_scatter", [](const RcclComm &c, uintptr_t sb, uintptr_t rb, size_t n, int dt, int red, uintptr_t s) {
+        c.reduce_scatter(P(sb), P(rb), n, dt, red, P(s));
+      }, py::arg("send"), py::arg("recv"), py::arg("recv_count"), py::arg("dtype"), py::arg("red") = 0, py::arg("stream") = 0)
+      .def("broadcast", [](const RcclComm &c, uintptr_t sb, uintptr_t rb, size_t n, int root, int dt, uintptr_t s) {
+        c.broadcast(P(sb), P(rb), n, root, dt, P(s));
+      }, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("root"), py::arg("dtype"), py::arg("stream") = 0)
+      .def_static("dtype_size", &RcclComm::dtype_size)
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("aborted", &RcclComm::aborted);
   m.def("rccl_abort_all", &rccl_abort_all, py::call_guard<py::gil_scoped_release>());
+  m.def("make_rccl_comms", &make_rccl_comms, py::arg("ctrl"), py::arg("device"), py::arg("n"),
+        "n communicators over the same ranks (one per logical stream), one broadcast of ids");
+
+  // ------------------------------------------------------------------ communication ops
+  py::class_<CommOp, GpuOp, std::shared_ptr<CommOp>>(m, "CommOp")
+      .def_property_readonly("dtype", &CommOp::dtype)
+      .def_property_readonly("n_comms", [](const CommOp &o) { return o.comms().size(); });
+  py::class_<SendRecvOp, CommOp, std::shared_ptr<SendRecvOp>>(m, "SendRecvOp")
+      .def(py::init([](std::string name, CommSet comms, uintptr_t sb, size_t sc, int sp, uintptr_t rb,
+                       size_t rc, int rp, int dt, py::object keep) {
+             return std::make_shared<SendRecvOp>(std::move(name), std::move(comms), P(sb), sc, sp,
+                                                 P(rb), rc, rp, dt, py_keep(std::move(keep)));
+           }), py::arg("name"), py::arg("comms"), py::arg("send"), py::arg("send_count"),
+           py::arg("send_peer"), py::arg("recv"), py::arg("recv_count"), py::arg("recv_peer"),
+           py::arg("dtype"), py::arg("keep") = py::none());
+  py::class_<AlltoallvOp, CommOp, std::shared_ptr<AlltoallvOp>>(m, "AlltoallvOp")
+      .def(py::init([](std::string name, CommSet comms,
+                       const std::vector<std::tuple<uintptr_t, size_t, int, uintptr_t, size_t, int>> &xs,
+                       int dt, py::object keep) {
+             std::vector<RcclComm::Xfer> v;
+             for (const auto &t : xs)
+               v.push_back({P(std::get<0>(t)), std::get<1>(t), std::get<2>(t), P(std::get<3>(t)),
+                            std::get<4>(t), std::get<5>(t)});
+             return std::make_shared<AlltoallvOp>(std::move(name), std::move(comms), std::move(v), dt,
+                                                  py_keep(std::move(keep)));
+           }), py::arg("name"), py::arg("comms"), py::arg("xfers"), py::arg("dtype"),
+           py::arg("keep") = py::none(),
+           "xfers: [(send, send_count, send_peer, recv, recv_count, recv_peer)]");
+  py::class_<AllReduceOp, CommOp, std::shared_ptr<AllReduceOp>>(m, "AllReduceOp")
+      .def(py::init([](std::string name, CommSet comms, uintptr_t sb, uintptr_t rb, size_t n, int dt,
+                       int red, py::object keep) {
+             return std::make_shared<AllReduceOp>(std::move(name), std::move(comms), P(sb), P(rb), n,
+                                                  dt, red, py_keep(std::move(keep)));
+           }), py::arg("name"), py::arg("comms"), py::arg("send"), py::arg("recv"), py::arg("count"),
+           py::arg("dtype"), py::arg("red") = 0, py::arg("keep") = py::none());
+  py::class_<AllGatherOp, CommOp, std::shared_ptr<AllGatherOp>>(m, "AllGatherOp")
+      .def(py::init([](std::string name, CommSet comms, uintptr_t sb, uintptr_t rb, size_t n, int dt,
+                       py::object keep) {
+             return std::make_shared<AllGatherOp>(std::move(name), std::move(comms), P(sb), P(rb), n,
+                                                  dt, py_keep(std::move(keep)));
+           }), py::arg("name"), py::arg("comms"), py::arg("send"), py::arg("recv"), py::arg("count"),
+           py::arg("dtype"), py::arg("keep") = py::none());
+  py::class_<ReduceScatterOp, CommOp, std::shared_ptr<ReduceScatterOp>>(m, "ReduceScatterOp")
+      .def(py::init([](std::string name, CommSet comms, uintptr_t sb, uintptr_t rb, size_t n, int dt,
+                       int red, py::object keep) {
+             return std::make_shared<ReduceScatterOp>(std::move(name), std::move(comms), P(sb), P(rb),
+                                                      n, dt, red, py_keep(std::move(keep)));
+           }), py::arg("name"), py::arg("comms"), py::arg("send"), py::arg("recv"),
+           py::arg("recv_count"), py::arg("dtype"), py::arg("red") = 0, py::arg("keep") = py::none());
+  py::class_<BroadcastOp, CommOp, std::shared_ptr<BroadcastOp>>(m, "BroadcastOp")
+      .def(py::init([](std::string name, CommSet comms, uintptr_t sb, uintptr_t rb, size_t n, int root,
+                       int dt, py::object keep) {
+             return std::make_shared<BroadcastOp>(std::move(name), std::move(comms), P(sb), P(rb), n,
+                                                  root, dt, py_keep(std::move(keep)));
+           }), py::arg("name"), py::arg("comms"), py::arg("send"), py::arg("recv"), py::arg("count"),
+           py::arg("root"), py::arg("dtype"), py::arg("keep") = py::none());
 
   // ------------------------------------------------------------------ workloads
   py::class_<HaloArgs>(m, "HaloArgs")

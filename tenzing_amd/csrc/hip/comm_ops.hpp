@@ -1,0 +1,163 @@
+// Communication ops for user graphs: stream-ordered RCCL point-to-point and collectives.
+//
+// Reference: include/tenzing/mpi/ops_mpi.hpp:17-192 and src/mpi/ops_mpi.cpp:11-49 (`Irecv`,
+// `Isend`, `Ialltoallv`, `Wait`, `OwningWaitall`, `MultiWait`). Those are host-issued MPI
+// CpuOps on device buffers (CUDA-aware MPI); completion is a separate host `Wait` op. Here a
+// transfer is a GpuOp that the search binds to a HIP stream like any kernel:
+//  * "wait" is the stream order itself. A successor on the same stream needs nothing, one on
+//    another stream gets an event edge from the synchronizer, a host successor gets an event
+//    sync. There is no host round trip between a kernel and the transfer that follows it.
+//  * every transfer captures into the schedule's hipGraph (RCCL kernels are capturable).
+//  * point-to-point ops are grouped (ncclGroupStart/End): a send-and-receive pair, or a whole
+//    all-to-all-v, is one op. A lone blocking send on a stream could wait forever for a receive
+//    queued behind it; a group cannot.
+//  * RCCL matches operations per communicator in issue order, so a communicator must not be
+//    driven from two streams at once. An op on logical stream k uses `comms[k % comms.size()]`:
+//    give one communicator per stream (`make_rccl_comms(ctrl, device, n_streams)`) and every rank,
+//    running the same schedule, issues the same operations on each communicator in the same order.
+// Buffers are raw device pointers owned by the caller; `keep` holds whatever owns them (a torch
+// tensor from Python) for as long as the op lives.
+#pragma once
+
+#include "core/ops.hpp"
+#include "hip/rccl_comm.hpp"
+
+#include <algorithm>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace tz {
+
+using CommSet = std::vector<std::shared_ptr<RcclComm>>;
+
+/// common part: name, communicators, dtype, buffer owner
+class CommOp : public GpuOp {
+public:
+  CommOp(std::string name, CommSet comms, int dtype, std::shared_ptr<void> keep);
+  std::string name() const override { return name_; }
+  Json json() const override; // {"name", "kind"} (ops are found by name when deserializing)
+  int dtype() const { return dtype_; }
+  const CommSet &comms() const { return comms_; }
+
+protected:
+  /// the communicator of the logical stream this launch runs on
+  const RcclComm &comm_for(void *stream, Executor &ex) const;
+  size_t esize() const { return RcclComm::dtype_size(dtype_); }
+  int nranks() const;
+  /// simulator cost: latency + bytes over one xGMI link (~75 GB/s per direction)
+  static double link_cost_us(double bytes, double latency_us = 8.0) {
+    return latency_us + bytes / 7.5e4;
+  }
+
+private:
+  std::string name_;
+  CommSet comms_;
+  int dtype_;
+  std::shared_ptr<void> keep_;
+};
+
+/// grouped send of `send_count` elements to `send_peer` and receive of `recv_count` elements
+/// from `recv_peer` (either count may be 0) — the reference's Isend + Irecv + Waitall
+class SendRecvOp : public CommOp {
+public:
+  SendRecvOp(std::string name, CommSet comms, const void *send, size_t send_count, int send_peer,
+             void *recv, size_t recv_count, int recv_peer, int dtype,
+             std::shared_ptr<void> keep = nullptr);
+  std::string kind() const override { return "RcclSendRecv"; }
+  double bytes() const override { return double(send_count_ + recv_count_) * double(esize()); }
+  double cost_us() const override { return link_cost_us(double(std::max(send_count_, recv_count_)) * double(esize())); }
+  void launch(void *stream, Executor &ex) const override;
+
+private:
+  const void *send_;
+  size_t send_count_;
+  int send_peer_;
+  void *recv_;
+  size_t recv_count_;
+  int recv_peer_;
+};
+
+/// grouped multi-peer exchange (the reference's Ialltoallv): one send and/or receive per entry
+class AlltoallvOp : public CommOp {
+public:
+  AlltoallvOp(std::string name, CommSet comms, std::vector<RcclComm::Xfer> xfers, int dtype,
+              std::shared_ptr<void> keep = nullptr);
+  std::string kind() const override { return "RcclAlltoallv"; }
+  double bytes() const override;
+  double cost_us() const override;
+  void launch(void *stream, Executor &ex) const override;
+
+private:
+  std::vector<RcclComm::Xfer> xfers_;
+};
+
+/// all-reduce (in place when send == recv); red: RcclComm::Sum/Prod/Max/Min
+class AllReduceOp : public CommOp {
+public:
+  AllReduceOp(std::string name, CommSet comms, const void *send, void *recv, size_t count,
+              int dtype, int red = RcclComm::Sum, std::shared_ptr<void> keep = nullptr);
+  std::string kind() const override { return "RcclAllReduce"; }
+  double bytes() const override { return double(count_) * double(esize()); }
+  double cost_us() const override;
+  void launch(void *stream, Executor &ex) const override;
+
+private:
+  const void *send_;
+  void *recv_;
+  size_t count_;
+  int red_;
+};
+
+/// all-gather: `count` elements per rank into recv (size * count, rank-major)
+class AllGatherOp : public CommOp {
+public:
+  AllGatherOp(std::string name, CommSet comms, const void *send, void *recv, size_t count,
+              int dtype, std::shared_ptr<void> keep = nullptr);
+  std::string kind() const override { return "RcclAllGather"; }
+  double bytes() const override { return double(count_) * double(esize()) * double(nranks()); }
+  double cost_us() const override;
+  void launch(void *stream, Executor &ex) const override;
+
+private:
+  const void *send_;
+  void *recv_;
+  size_t count_;
+};
+
+/// reduce-scatter: send holds size * recv_count elements, rank r keeps reduced block r
+class ReduceScatterOp : public CommOp {
+public:
+  ReduceScatterOp(std::string name, CommSet comms, const void *send, void *recv,
+                  size_t recv_count, int dtype, int red = RcclComm::Sum,
+                  std::shared_ptr<void> keep = nullptr);
+  std::string kind() const override { return "RcclReduceScatter"; }
+  double bytes() const override { return double(recv_count_) * double(esize()) * double(nranks()); }
+  double cost_us() const override;
+  void launch(void *stream, Executor &ex) const override;
+
+private:
+  const void *send_;
+  void *recv_;
+  size_t recv_count_;
+  int red_;
+};
+
+/// broadcast of `count` elements from `root`'s send buffer into every rank's recv buffer
+class BroadcastOp : public CommOp {
+public:
+  BroadcastOp(std::string name, CommSet comms, const void *send, void *recv, size_t count,
+              int root, int dtype, std::shared_ptr<void> keep = nullptr);
+  std::string kind() const override { return "RcclBroadcast"; }
+  double bytes() const override { return double(count_) * double(esize()); }
+  double cost_us() const override { return link_cost_us(bytes(), 10.0); }
+  void launch(void *stream, Executor &ex) const override;
+
+private:
+  const void *send_;
+  void *recv_;
+  size_t count_;
+  int root_;
+};
+
+} // namespace tz

@@ -47,8 +47,28 @@ static ncclDataType_t dt(int dtype) {
   case 0: return ncclFloat32;
   case 1: return ncclFloat64;
   case 2: return ncclInt32;
+  case 3: return ncclFloat16;
+  case 4: return ncclBfloat16;
+  case 5: return ncclInt64;
+  case 6: return ncclUint8;
   default: TZ_THROW("bad dtype " << dtype);
   }
+}
+
+static ncclRedOp_t red_op(int red) {
+  switch (red) {
+  case RcclComm::Sum: return ncclSum;
+  case RcclComm::Prod: return ncclProd;
+  case RcclComm::Max: return ncclMax;
+  case RcclComm::Min: return ncclMin;
+  default: TZ_THROW("bad reduction " << red);
+  }
+}
+
+size_t RcclComm::dtype_size(int dtype) {
+  static const size_t sz[] = {4, 8, 4, 2, 2, 8, 1};
+  TZ_CHECK(dtype >= 0 && dtype < 7, "bad dtype " << dtype);
+  return sz[dtype];
 }
 
 RcclComm::RcclComm(Ctrl &ctrl, int device) : rank_(ctrl.rank()), size_(ctrl.size()) {
@@ -125,6 +145,34 @@ void RcclComm::exchange(const std::vector<Xfer> &xs, int dtype, void *stream) co
 void RcclComm::allreduce_sum(void *buf, size_t count, int dtype, void *stream) const {
   check_live();
   TZ_NCCL(ncclAllReduce(buf, buf, count, dt(dtype), ncclSum, static_cast<ncclComm_t>(comm_),
+                        static_cast<hipStream_t>(stream)));
+}
+
+void RcclComm::allreduce(const void *send, void *recv, size_t count, int dtype, int red,
+                         void *stream) const {
+  check_live();
+  TZ_NCCL(ncclAllReduce(send, recv, count, dt(dtype), red_op(red), static_cast<ncclComm_t>(comm_),
+                        static_cast<hipStream_t>(stream)));
+}
+
+void RcclComm::allgather(const void *send, void *recv, size_t count, int dtype, void *stream) const {
+  check_live();
+  TZ_NCCL(ncclAllGather(send, recv, count, dt(dtype), static_cast<ncclComm_t>(comm_),
+                        static_cast<hipStream_t>(stream)));
+}
+
+void RcclComm::reduce_scatter(const void *send, void *recv, size_t recvCount, int dtype, int red,
+                              void *stream) const {
+  check_live();
+  TZ_NCCL(ncclReduceScatter(send, recv, recvCount, dt(dtype), red_op(red),
+                            static_cast<ncclComm_t>(comm_), static_cast<hipStream_t>(stream)));
+}
+
+void RcclComm::broadcast(const void *send, void *recv, size_t count, int root, int dtype,
+                         void *stream) const {
+  check_live();
+  TZ_CHECK(root >= 0 && root < size_, "broadcast root " << root << " out of range");
+  TZ_NCCL(ncclBroadcast(send, recv, count, dt(dtype), root, static_cast<ncclComm_t>(comm_),
                         static_cast<hipStream_t>(stream)));
 }
 

@@ -37,7 +37,8 @@ public:
   int size() const { return size_; }
 
   /// grouped point-to-point: send `sendCount` elements to `sendPeer` and receive `recvCount`
-  /// into `recvBuf` from `recvPeer` (either count may be 0); dtype: 0=f32, 1=f64, 2=i32
+  /// into `recvBuf` from `recvPeer` (either count may be 0); dtype: 0=f32, 1=f64, 2=i32,
+  /// 3=f16, 4=bf16, 5=i64, 6=u8
   void sendrecv(const void *sendBuf, size_t sendCount, int sendPeer, void *recvBuf,
                 size_t recvCount, int recvPeer, int dtype, void *stream) const;
   /// grouped multi-peer exchange (all-to-all-v style)
@@ -52,6 +53,20 @@ public:
   void exchange(const std::vector<Xfer> &xs, int dtype, void *stream) const;
   /// in-place all-reduce sum (f32/f64) — used by tests and device-side checks
   void allreduce_sum(void *buf, size_t count, int dtype, void *stream) const;
+
+  /// reduction operators of the collectives below
+  enum Red { Sum = 0, Prod = 1, Max = 2, Min = 3 };
+  /// out-of-place (or in place: send == recv) all-reduce of `count` elements
+  void allreduce(const void *send, void *recv, size_t count, int dtype, int red, void *stream) const;
+  /// every rank contributes `count` elements; recv holds size()*count, rank-major
+  void allgather(const void *send, void *recv, size_t count, int dtype, void *stream) const;
+  /// send holds size()*recvCount elements; rank r receives the reduced block r
+  void reduce_scatter(const void *send, void *recv, size_t recvCount, int dtype, int red,
+                      void *stream) const;
+  /// root's `send` (count elements) lands in every rank's `recv`
+  void broadcast(const void *send, void *recv, size_t count, int root, int dtype, void *stream) const;
+  /// bytes of one element of `dtype`
+  static size_t dtype_size(int dtype);
 
   static std::string version();
 
