@@ -111,6 +111,7 @@ from ._tz import (  # noqa: E402,F401
     mcts_explore,
     random_rollout,
     remove_redundant_syncs,
+    resolve_graph,
     strategy_names,
     verify,
 )

@@ -1,9 +1,11 @@
-"""``python -m tenzing_amd`` — search / replay / rules / env.
+"""``python -m tenzing_amd`` — search / run / replay / rules / env.
 
   python -m tenzing_amd search --workload halo --solver mcts --strategy FastMin --iters 100
   python -m tenzing_amd search --workload spmv --solver dfs --max-seqs 15000 --csv spmv.csv
   python -m tenzing_amd search --workload halo --replay halo.csv      # MCTS on recorded timings
   python -m tenzing_amd search --workload fused --sim                  # hardware-free (cost model)
+  python -m tenzing_amd search --workload halo --save-best best.json   # search once ...
+  python -m tenzing_amd run best.json --iters 1000                     # ... deploy many times
   python -m tenzing_amd rules spmv.csv --out spmv_                     # design rules
   python -m tenzing_amd env --topology
 
@@ -142,10 +144,105 @@ def cmd_search(a) -> int:
         if b >= 0:
             summary["best_pct10_ms"] = res.sims[b].res.pct10 * 1e3
             summary["best_schedule"] = json.loads(res.sims[b].seq.json())
+            if a.save_best:
+                _save_best(a, tz, ctrl, res.sims[b])
         print(json.dumps(summary))
     if a.trace_best:
         _trace_best(a, tz, ctrl, g, res, rt)
     return 0
+
+
+# search options that describe the workload and the platform (what `run` needs to rebuild the
+# graph a saved schedule refers to); solver and measurement options are not part of it
+_WORKLOAD_KEYS = ("workload", "noop_width", "streams", "halo_n", "nq", "ghost", "neighbors",
+                  "order", "fuse", "transport", "relay", "relay_fracs", "stencil", "spmv_m",
+                  "spmv_matrix", "spmv_form", "spmv_transport", "cu_partition",
+                  "stream_priorities")
+
+
+def _save_best(a, tz, ctrl, sim) -> None:
+    """The best schedule plus everything needed to run it again: the workload options, the
+    rank count and the reference's schedule JSON (ops by name, `in_graph` flags)."""
+    doc = {"tenzing_amd": tz.__version__, "ranks": ctrl.size, "mode": a.mode,
+           "pct10_ms": sim.res.pct10 * 1e3,
+           "args": {k: getattr(a, k) for k in _WORKLOAD_KEYS},
+           "schedule": json.loads(sim.seq.json(True))}
+    with open(a.save_best, "w") as f:
+        json.dump(doc, f, indent=1)
+
+
+def load_schedule(doc: dict, ctrl, device: int, setup: bool):
+    """(workload options, graph, workload objects, sequence) of a `--save-best` document. The
+    workload is rebuilt from the saved options, the schedule is rebuilt by op name and checked
+    race-free against the graph it executes (choices resolved, compounds expanded)."""
+    import tenzing_amd as tz
+
+    w = _parser().parse_args(["search"])
+    for k, v in doc["args"].items():
+        setattr(w, k, v)
+    g, wl = _build_workload(w, ctrl, device, setup)
+    seq = tz.OpIndex(g).sequence_from_json(json.dumps(doc["schedule"]))
+    bad = tz.verify(seq, tz.resolve_graph(g, seq), w.streams)
+    if bad:
+        raise SystemExit("schedule is not race-free on this graph: " + "; ".join(bad[:5]))
+    return w, g, wl, seq
+
+
+def cmd_run(a) -> int:
+    """Run a saved schedule without searching: rebuild the workload, rebuild the sequence by op
+    name, prove it race-free on the graph it executes, check the results once, then time it."""
+    import tenzing_amd as tz
+    from tenzing_amd.parallel import init_ctrl, select_device
+
+    with open(a.schedule) as f:
+        doc = json.load(f)
+    ctrl = init_ctrl()
+    if ctrl.size != doc["ranks"]:
+        raise SystemExit(f"schedule was searched on {doc['ranks']} ranks, this run has {ctrl.size}")
+    if doc["args"]["workload"] == "noop":
+        raise SystemExit("run: the no-op workload has no GPU work")
+    device = select_device()
+    if device < 0:
+        raise SystemExit("run: no GPU visible")
+    w, g, wl, seq = load_schedule(doc, ctrl, device, True)
+    mode = a.mode or doc.get("mode", "graph")
+    prio = [int(x) for x in w.stream_priorities.split(",")] if w.stream_priorities else []
+    rt = tz.HipRuntime(device=device, n_streams=w.streams, priorities=prio,
+                       cu_partition=w.cu_partition,
+                       mode=tz.ExecMode.Graph if mode == "graph" else tz.ExecMode.Eager,
+                       watchdog_s=a.watchdog, graph_unroll=a.graph_unroll)
+    if "halo" in wl:
+        wl["halo"].init_grid()
+    if "spmv" in wl:
+        wl["spmv"].reset_y()
+    rt.device_sync()
+    rt.prepare(seq)
+    rt.run(1)
+    rt.device_sync()
+    out = {"schedule": a.schedule, "workload": w.workload, "ranks": ctrl.size,
+           "streams": w.streams, "mode": "graph" if rt.effective_mode == tz.ExecMode.Graph
+           else "eager"}
+    ok = True
+    if "halo" in wl:
+        out["halo_bad_cells"] = int(ctrl.allreduce_sum([float(wl["halo"].check_grid())])[0])
+        ok &= out["halo_bad_cells"] == 0
+    if "spmv" in wl:
+        out["spmv_max_rel_err"] = ctrl.allreduce_max([wl["spmv"].check()])[0]
+        ok &= out["spmv_max_rel_err"] < 1e-4
+    rt.run(a.warmup)
+    rt.device_sync()
+    ctrl.barrier()
+    t0 = time.perf_counter()
+    rt.run(a.iters)
+    rt.device_sync()
+    dt = ctrl.allreduce_max([time.perf_counter() - t0])[0]
+    out["iters"] = a.iters
+    out["ms_per_iter"] = dt / max(a.iters, 1) * 1e3
+    out["searched_pct10_ms"] = doc.get("pct10_ms")
+    out["correct"] = bool(ok)
+    if ctrl.rank == 0:
+        print(json.dumps(out))
+    return 0 if ok else 1
 
 
 def _trace_best(a, tz, ctrl, g, res, rt) -> None:
@@ -194,6 +291,11 @@ def cmd_env(a) -> int:
 
 
 def main(argv=None) -> int:
+    a = _parser().parse_args(argv)
+    return a.fn(a)
+
+
+def _parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="python -m tenzing_amd", description=__doc__.splitlines()[0])
     sub = ap.add_subparsers(dest="cmd", required=True)
     s = sub.add_parser("search")
@@ -232,6 +334,8 @@ def main(argv=None) -> int:
     s.add_argument("--resume", default="")
     s.add_argument("--csv", default="")
     s.add_argument("--jsonl", default="")
+    s.add_argument("--save-best", default="",
+                   help="write the best schedule and its workload options as JSON (for `run`)")
     s.add_argument("--trace-best", default="",
                    help="write the best schedule's timeline as Chrome trace JSON (per rank)")
     s.add_argument("--trace-iters", type=int, default=2,
@@ -265,8 +369,16 @@ def main(argv=None) -> int:
     e = sub.add_parser("env")
     e.add_argument("--topology", action="store_true")
     e.set_defaults(fn=cmd_env)
-    a = ap.parse_args(argv)
-    return a.fn(a)
+    u = sub.add_parser("run", help="run a schedule saved by `search --save-best` (no search)")
+    u.add_argument("schedule")
+    u.add_argument("--iters", type=int, default=1000)
+    u.add_argument("--warmup", type=int, default=50)
+    u.add_argument("--mode", default="", choices=["", "eager", "graph"],
+                   help="default: the mode the schedule was searched in")
+    u.add_argument("--graph-unroll", type=int, default=20)
+    u.add_argument("--watchdog", type=float, default=120.0)
+    u.set_defaults(fn=cmd_run)
+    return ap
 
 
 if __name__ == "__main__":

@@ -362,6 +362,10 @@ PYBIND11_MODULE(_tz, m) {
       .def("canonical_key", &State::canonical_key)
       .def("equivalent", [](const State &a, const State &b) { return equivalent(a, b); });
 
+  m.def("resolve_graph", [](const Graph &g, const Sequence &s) {
+    return std::const_pointer_cast<Graph>(resolve_graph(g, s));
+  }, py::arg("graph"), py::arg("seq"),
+     "the graph `seq` executed: compounds expanded, each choice replaced by the alternative it runs");
   m.def("verify", [](const Sequence &s, const Graph &g, int n) {
     std::vector<std::string> out;
     for (auto &v : verify(s, g, n)) out.push_back(v.desc());

@@ -553,6 +553,58 @@ int remove_redundant_syncs(Sequence &seq, const Graph &g, int nStreams) {
   return removed;
 }
 
+namespace {
+bool runs_any(const OpPtr &op, const std::set<std::string> &names) {
+  if (names.count(op->name())) return true;
+  if (op->op_class() == OpClass::Compound) {
+    const auto &sub = *static_cast<const CompoundOp &>(*op).graph();
+    for (int v : sub.vertices())
+      if (v != Graph::kStart && v != Graph::kFinish && runs_any(sub.op(v), names)) return true;
+  } else if (op->op_class() == OpClass::Choice) {
+    for (const auto &alt : static_cast<const ChoiceOp &>(*op).choices())
+      if (runs_any(alt, names)) return true;
+  }
+  return false;
+}
+} // namespace
+
+GraphPtr resolve_graph(const Graph &g, const Sequence &seq) {
+  std::set<std::string> names;
+  for (const auto &e : seq.entries) {
+    const OpClass c = e.op->op_class();
+    if (c == OpClass::BoundGpu)
+      names.insert(static_cast<const BoundGpuOp &>(*e.op).unbound()->name());
+    else if (c != OpClass::Sync)
+      names.insert(e.op->name());
+  }
+  auto cur = std::make_shared<Graph>(g);
+  for (bool changed = true; changed;) {
+    changed = false;
+    for (int v : cur->vertices()) {
+      const OpPtr op = cur->op(v);
+      if (op->op_class() == OpClass::Compound) {
+        cur = cur->clone_but_expand(v, *static_cast<const CompoundOp &>(*op).graph());
+        changed = true;
+        break;
+      }
+      if (op->op_class() == OpClass::Choice) {
+        OpPtr pick;
+        for (const auto &alt : static_cast<const ChoiceOp &>(*op).choices()) {
+          if (!runs_any(alt, names)) continue;
+          TZ_CHECK(!pick, "sequence runs two alternatives of " << op->name() << ": "
+                                                               << pick->name() << ", " << alt->name());
+          pick = alt;
+        }
+        TZ_CHECK(pick, "sequence runs no alternative of " << op->name());
+        cur = cur->clone_but_replace(v, pick);
+        changed = true;
+        break;
+      }
+    }
+  }
+  return cur;
+}
+
 Sequence random_rollout(State s, std::mt19937_64 &rng) {
   while (!s.complete()) {
     auto ds = s.get_decisions();

@@ -182,6 +182,12 @@ struct Violation {
 /// final State's graph); ops are matched by name.
 std::vector<Violation> verify(const Sequence &seq, const Graph &g, int nStreams);
 
+/// The graph a complete sequence executed: every CompoundOp expanded and every ChoiceOp
+/// replaced by the one alternative whose ops the sequence runs (ops matched by name). Throws if
+/// a choice has no such alternative, or more than one. With it, `verify(seq, resolve_graph(g,
+/// seq), S)` checks a schedule that was loaded from a file rather than built by a State.
+GraphPtr resolve_graph(const Graph &g, const Sequence &seq);
+
 /// Remove synchronization ops whose removal keeps every edge covered (fix-point, scanning from
 /// the end). Returns the number removed. Reference: Schedule::remove_redundant_syncs.
 int remove_redundant_syncs(Sequence &seq, const Graph &g, int nStreams);

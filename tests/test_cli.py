@@ -127,3 +127,29 @@ def test_trace_best_chrome_json_sim(tmp_path):
     assert len(ops) == 26 and all(e["name"].startswith("he_direct_") for e in ops)
     assert all(e["dur"] > 0 and e["ts"] >= 0 for e in ops)
     assert "host" in names and {f"stream {e['tid'] - 1}" for e in ops} <= names
+
+
+def test_save_best_then_load(tmp_path):
+    """search --save-best writes a self-contained schedule; `run`'s loader rebuilds the graph
+    from the saved options and proves the schedule race-free on it (no GPU: graph only)"""
+    import tenzing_amd as tz
+    from tenzing_amd import cli
+
+    path = tmp_path / "best.json"
+    out = _py("search", "--workload", "fused", "--sim", "--streams", "3", "--iters", "15",
+              "--neighbors", "26", "--bench-iters", "2", "--save-best", str(path))
+    s = json.loads(out.strip().splitlines()[-1])
+    doc = json.loads(path.read_text())
+    assert doc["ranks"] == 1 and doc["args"]["workload"] == "fused" and doc["args"]["streams"] == 3
+    assert abs(doc["pct10_ms"] - s["best_pct10_ms"]) < 1e-9
+    assert all("in_graph" in op for op in doc["schedule"])
+    w, g, wl, seq = cli.load_schedule(doc, tz.SelfCtrl(), -1, False)
+    assert w.neighbors == 26 and len(seq) == len(doc["schedule"])
+    # a tampered schedule (a cross-stream wait removed) is refused
+    waits = [i for i, op in enumerate(doc["schedule"]) if op.get("kind") == "CudaStreamWaitEvent"]
+    if waits:
+        bad = dict(doc, schedule=[op for i, op in enumerate(doc["schedule"]) if i != waits[0]])
+        import pytest
+
+        with pytest.raises(SystemExit, match="race-free"):
+            cli.load_schedule(bad, tz.SelfCtrl(), -1, False)

@@ -287,3 +287,60 @@ def test_racing_cuts_slow_candidates_short(tz):
     assert t["fast"] < t["slow"] < t["slower"]
     # DFS takes the alternatives in order: fast first, then both slower ones are raced
     assert names[0] == ["Start", "fast", "Finish"] and b.raced == 2
+
+
+def _nested_choice_graph(tz):
+    sub = tz.Graph()
+    x = tz.SimGpuOp("x", 5)
+    inner = tz.StaticChoiceOp("y", [tz.SimGpuOp("y_slow", 50), tz.SimGpuOp("y_fast", 5)])
+    sub.start_then(x)
+    sub.then(x, inner)
+    sub.then_finish(inner)
+    alt_a = tz.StaticCompoundOp("form_a", sub)
+    alt_b = tz.SimGpuOp("form_b", 30)
+    g = tz.Graph()
+    pre = tz.SimGpuOp("pre", 3)
+    top = tz.StaticChoiceOp("form", [alt_a, alt_b])
+    g.start_then(pre)
+    g.then(pre, top)
+    g.then_finish(top)
+    return g
+
+
+def test_resolve_graph_verifies_loaded_schedules(tz):
+    """a schedule read back from JSON is checked against the graph it executed: choices
+    replaced by the alternative it ran, compounds expanded"""
+    g = _nested_choice_graph(tz)
+    idx = tz.OpIndex(g)
+    seen = set()
+    for seed in range(40):
+        st = tz.State(g, tz.Platform(2))
+        seq = tz.random_rollout(st, seed)
+        back = idx.sequence_from_json(seq.json(True))
+        fg = tz.resolve_graph(g, back)
+        names = {fg.op(v).name for v in fg.vertices()}
+        assert not {"form", "y", "form_a"} & names  # nothing left to choose or expand
+        assert tz.verify(back, fg, 2) == []
+        ran = {op.name for op in back.ops()}
+        seen.add(frozenset(ran & {"form_b", "y_slow", "y_fast"}))
+    assert len(seen) == 3  # every resolution path was exercised
+    # an alternative that is not run cannot be resolved
+    with pytest.raises(tz.TzError, match="no alternative"):
+        tz.resolve_graph(g, tz.Sequence())
+
+
+def test_resolve_graph_flags_a_dropped_sync(tz):
+    g = _nested_choice_graph(tz)
+    for seed in range(40):
+        seq = tz.random_rollout(tz.State(g, tz.Platform(2, symmetric_streams=False)), seed)
+        ops = seq.ops()
+        syncs = [i for i, op in enumerate(ops) if op.kind == "CudaStreamWaitEvent"]
+        if not syncs:
+            continue
+        cut = tz.Sequence()
+        for i, op in enumerate(ops):
+            if i != syncs[0]:
+                cut.append(op)
+        assert tz.verify(cut, tz.resolve_graph(g, cut), 2) != []
+        return
+    pytest.skip("no rollout needed a cross-stream wait")

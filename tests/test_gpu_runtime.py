@@ -467,3 +467,33 @@ def test_device_timer_measures_gpu_time(tz, gpu):
         d, h = res[(True, mode)], res[(False, mode)]
         assert 190e-6 < d < 260e-6, res
         assert h >= d * 0.98, res
+
+
+@pytest.mark.parametrize("workload", ["halo", "fused"])
+def test_search_save_best_then_run(tz, gpu, tmp_path, workload):
+    """search once, deploy many: the saved schedule is rebuilt by name in a fresh process,
+    proven race-free, checked for correct results and timed as a hipGraph"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = tmp_path / "best.json"
+
+    def cli(*args):
+        r = subprocess.run([sys.executable, "-m", "tenzing_amd", *args], cwd=root,
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    s = cli("search", "--workload", workload, "--halo-n", "64", "--neighbors", "26", "--order",
+            "qxyz", "--spmv-m", "20000", "--streams", "3", "--iters", "8", "--bench-iters", "3",
+            "--target-secs", "0.001", "--mode", "graph", "--graph-unroll", "4",
+            "--save-best", str(path))
+    assert path.exists() and s["best_pct10_ms"] > 0
+    r = cli("run", str(path), "--iters", "200", "--warmup", "10")
+    assert r["correct"] and r["mode"] == "graph" and r["ms_per_iter"] > 0
+    if workload == "halo":
+        assert r["halo_bad_cells"] == 0
+    else:
+        assert r["halo_bad_cells"] == 0 and r["spmv_max_rel_err"] < 1e-4
