@@ -116,6 +116,8 @@ from ._tz import (  # noqa: E402,F401
     verify,
 )
 
+from .search import search  # noqa: E402,F401
+
 __version__ = _tz.version()
 
 NATIVE_PATH = _tz.__file__

@@ -1,0 +1,73 @@
+"""One-call schedule search for a user graph.
+
+``tz.search(graph, ...)`` wires up what every driver otherwise assembles by hand: the control
+plane (this process alone, or every rank under ``torchrun``), the HIP runtime or a hardware-free
+benchmarker, the benchmark options and the solver. The reference's drivers do the same wiring in
+C++ (tenzing-mcts/examples/halo_run_strategy.hpp:135-160, tenzing-dfs/examples/spmv.cu:100-120).
+
+    import tenzing_amd as tz
+    res = tz.search(g, streams=2, iters=100)                  # MCTS on the GPU, hipGraph candidates
+    res = tz.search(g, streams=2, solver="dfs", sim=True)     # exhaustive, cost model, no GPU
+    best = res.sims[res.best()]
+"""
+from __future__ import annotations
+
+from . import _tz
+
+
+def search(graph, streams: int = 2, solver: str = "mcts", iters: int = 100,
+           strategy: str = "FastMin", mode: str = "graph", graph_unroll: int = 8,
+           bench_iters: int = 10, target_secs: float = 0.002, race_ratio: float = 0.0,
+           max_seqs: int = -1, sim: bool = False, replay: str = "", ctrl=None,
+           device: int | None = None, seed: int = 0, time_budget_s: float = 0.0,
+           watchdog_s: float = 0.0, symmetric_streams: bool = True):
+    """Search the schedules of ``graph`` on ``streams`` streams and return the SearchResult.
+
+    solver: "mcts" (``iters`` iterations, ``strategy``) or "dfs" (up to ``max_seqs``
+    schedules). Candidates are timed on the GPU (``mode`` "graph": each compiled to a hipGraph
+    with ``graph_unroll`` iterations per launch; "eager"), with the discrete-event model
+    (``sim``) or from a results CSV (``replay``). ``ctrl``: the control plane (default: this
+    process alone, or every rank when launched by torchrun); ``device``: the GPU (default: the
+    local rank's)."""
+    if solver not in ("mcts", "dfs"):
+        raise ValueError("solver must be 'mcts' or 'dfs'")
+    if mode not in ("graph", "eager"):
+        raise ValueError("mode must be 'graph' or 'eager'")
+    if ctrl is None:
+        from .parallel import init_ctrl
+
+        ctrl = init_ctrl()
+    plat = _tz.Platform(streams, symmetric_streams=symmetric_streams)
+    bo = _tz.BenchOpts(n_iters=bench_iters, max_retries=3, target_secs=target_secs,
+                       race_ratio=race_ratio)
+    rt = None
+    if replay:
+        bench = _tz.CsvBenchmarker(replay, graph)
+    elif sim:
+        bench = _tz.SimBenchmarker(streams)
+    else:
+        if device is None:
+            from .parallel import select_device
+
+            device = select_device()
+        if device < 0:
+            raise RuntimeError("no GPU visible: pass sim=True or replay=<csv>")
+        rt = _tz.HipRuntime(device=device, n_streams=streams,
+                            mode=_tz.ExecMode.Graph if mode == "graph" else _tz.ExecMode.Eager,
+                            watchdog_s=watchdog_s, graph_unroll=graph_unroll)
+        bench = _tz.EmpiricalBenchmarker(rt, ctrl)
+    if solver == "dfs":
+        o = _tz.DfsOpts()
+        o.max_seqs = max_seqs
+        o.bench = bo
+        res = _tz.dfs_explore(graph, plat, bench, ctrl, o)
+    else:
+        o = _tz.MctsOpts()
+        o.n_iters = iters
+        o.strategy = strategy
+        o.seed = seed
+        o.time_budget_s = time_budget_s
+        o.bench = bo
+        res = _tz.mcts_explore(graph, plat, bench, ctrl, o)
+    del bench, rt  # the runtime (and its streams) goes before the caller's tensors
+    return res

@@ -201,3 +201,27 @@ def test_failed_candidates_are_skipped(tz):
     o.skip_failed = False
     with pytest.raises(Exception):
         tz.mcts_explore(g, tz.Platform(2), bench, tz.SelfCtrl(), o)
+
+
+def test_one_call_search_sim_and_dfs(tz, tmp_path):
+    """tz.search wires control plane, benchmarker and solver for a user graph"""
+    g = tz.Graph()
+    k = [tz.SimGpuOp(f"k{i}", us) for i, us in enumerate((20, 100, 100, 20), 1)]
+    g.start_then(k[0])
+    g.then(k[0], k[1])
+    g.then(k[0], k[2])
+    g.then(k[1], k[3])
+    g.then(k[2], k[3])
+    g.then_finish(k[3])
+    r1 = tz.search(g, streams=2, iters=20, sim=True, ctrl=tz.SelfCtrl())
+    assert len(r1.sims) == 20
+    r2 = tz.search(g, streams=2, solver="dfs", sim=True, ctrl=tz.SelfCtrl())
+    best = r2.sims[r2.best()].res.pct10
+    # the two big kernels on different streams overlap: ~140 us instead of 240
+    assert best < 200e-6
+    csv = tmp_path / "d.csv"
+    csv.write_text(r2.dump_csv())
+    r3 = tz.search(g, streams=2, iters=15, replay=str(csv), ctrl=tz.SelfCtrl())
+    assert abs(r3.sims[r3.best()].res.pct10 - best) < 1e-12
+    with pytest.raises(ValueError):
+        tz.search(g, solver="bfs", sim=True, ctrl=tz.SelfCtrl())
