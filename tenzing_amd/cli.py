@@ -26,11 +26,20 @@ def _build_workload(a, ctrl, device, setup):
     import tenzing_amd as tz
     from tenzing_amd.models import HaloConfig, SpmvConfig, build_fused, build_halo, build_spmv
 
+    grid = ()
+    if a.rank_grid:
+        try:
+            grid = tuple(int(v) for v in a.rank_grid.lower().split("x"))
+        except ValueError:
+            grid = ()
+        if len(grid) != 3:
+            raise SystemExit("--rank-grid must look like 2x2x2")
     hc = HaloConfig(n=a.halo_n, nq=a.nq, ghost=a.ghost, neighbors=a.neighbors, order=a.order,
                     fuse=a.fuse, transport=a.transport, stencil=a.stencil, relay=a.relay,
-                    relay_fracs=tuple(float(f) for f in a.relay_fracs.split(",")))
+                    relay_fracs=tuple(float(f) for f in a.relay_fracs.split(",")),
+                    rank_grid=grid)
     sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport,
-                    matrix=a.spmv_matrix)
+                    matrix=a.spmv_matrix, library=a.spmv_library)
     if a.workload == "halo":
         h, g = build_halo(hc, ctrl, device, setup)
         return g, {"halo": h}
@@ -154,10 +163,29 @@ def cmd_search(a) -> int:
 
 # search options that describe the workload and the platform (what `run` needs to rebuild the
 # graph a saved schedule refers to); solver and measurement options are not part of it
+# (the same keys, with the same meaning, as `tz-search --save-best` writes)
 _WORKLOAD_KEYS = ("workload", "noop_width", "streams", "halo_n", "nq", "ghost", "neighbors",
-                  "order", "fuse", "transport", "relay", "relay_fracs", "stencil", "spmv_m",
-                  "spmv_matrix", "spmv_form", "spmv_transport", "cu_partition",
-                  "stream_priorities")
+                  "order", "fuse", "transport", "relay", "relay_fracs", "stencil", "rank_grid",
+                  "spmv_m", "spmv_matrix", "spmv_form", "spmv_transport", "spmv_library",
+                  "cu_partition", "stream_priorities")
+
+
+def _saved_args(args: dict):
+    """The search options of a saved document, parsed like a command line (so values written
+    as strings by the native CLI get the same types)."""
+    argv = ["search"]
+    for k, v in args.items():
+        if k not in _WORKLOAD_KEYS:
+            continue
+        if k == "workload" and v == "halo+spmv":  # the native CLI's name for it
+            v = "fused"
+        flag = "--" + k.replace("_", "-")
+        if isinstance(v, bool):
+            if v:
+                argv.append(flag)
+        else:
+            argv.append(f"{flag}={v}")
+    return _parser().parse_args(argv)
 
 
 def _save_best(a, tz, ctrl, sim) -> None:
@@ -177,9 +205,7 @@ def load_schedule(doc: dict, ctrl, device: int, setup: bool):
     race-free against the graph it executes (choices resolved, compounds expanded)."""
     import tenzing_amd as tz
 
-    w = _parser().parse_args(["search"])
-    for k, v in doc["args"].items():
-        setattr(w, k, v)
+    w = _saved_args(doc["args"])
     g, wl = _build_workload(w, ctrl, device, setup)
     seq = tz.OpIndex(g).sequence_from_json(json.dumps(doc["schedule"]))
     bad = tz.verify(seq, tz.resolve_graph(g, seq), w.streams)
@@ -199,7 +225,7 @@ def cmd_run(a) -> int:
     ctrl = init_ctrl()
     if ctrl.size != doc["ranks"]:
         raise SystemExit(f"schedule was searched on {doc['ranks']} ranks, this run has {ctrl.size}")
-    if doc["args"]["workload"] == "noop":
+    if doc["args"].get("workload") == "noop":
         raise SystemExit("run: the no-op workload has no GPU work")
     device = select_device()
     if device < 0:
@@ -355,6 +381,9 @@ def _parser() -> argparse.ArgumentParser:
                    help="relayed shares offered to the search (comma-separated)")
     s.add_argument("--stencil", action="store_true",
                    help="halo: add the 7-point stencil (interior beside / shell after the exchange)")
+    s.add_argument("--rank-grid", default="", help="halo rank grid PXxPYxPZ (default: prime factors)")
+    s.add_argument("--spmv-library", default="adaptive",
+                   help="rocSPARSE CSR algorithm offered beside the hand-written kernels ('' = none)")
     s.add_argument("--spmv-m", type=int, default=150_000)
     s.add_argument("--spmv-matrix", default="",
                    help="Matrix Market file (square) instead of the random band matrix")

@@ -13,6 +13,8 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -59,7 +61,39 @@ void usage() {
          "  [--relay auto|off|force] [--relay-fracs F1,F2]\n"
          "  [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
-         "  [--checkpoint PATH] [--resume PATH] [--watchdog S]\n";
+         "  [--checkpoint PATH] [--resume PATH] [--watchdog S] [--race-ratio R]\n"
+         "  [--save-best PATH]      write the best schedule + workload options (JSON)\n"
+         "  [--run PATH [--run-iters N] [--run-warmup N]]\n"
+         "                          run a saved schedule (this CLI's or python -m tenzing_amd's)\n"
+         "                          without searching: verified race-free, checked, timed\n";
+}
+
+/// python-style option key ("halo_n") of a CLI option ("halo-n")
+std::string py_key(std::string k) {
+  for (char &c : k)
+    if (c == '-') c = '_';
+  return k;
+}
+
+/// options of a saved schedule document -> this CLI's options (the document may come from
+/// `tz-search --save-best` or `python -m tenzing_amd search --save-best`)
+void load_saved_args(const Json &args, Args &a) {
+  for (const auto &kv : args.as_object()) {
+    std::string k = kv.first;
+    for (char &c : k)
+      if (c == '_') c = '-';
+    const Json &v = kv.second;
+    if (v.is_bool()) {
+      if (v.as_bool()) a.kv[k] = "1";
+      else a.kv.erase(k);
+    } else if (v.is_string()) {
+      if (v.as_string().empty()) a.kv.erase(k);
+      else a.kv[k] = v.as_string();
+    } else {
+      a.kv[k] = v.dump();
+    }
+  }
+  if (a.get("workload", "") == "fused") a.kv["workload"] = "halo+spmv";
 }
 
 } // namespace
@@ -89,6 +123,17 @@ int main(int argc, char **argv) {
     }
   }
   try {
+    Json saved;
+    if (a.flag("run")) {
+      std::ifstream f(a.get("run", ""));
+      TZ_CHECK(f, "cannot open " << a.get("run", ""));
+      std::stringstream ss;
+      ss << f.rdbuf();
+      saved = Json::parse(ss.str());
+      load_saved_args(saved.at("args"), a);
+      if (!a.flag("mode") && saved.contains("mode")) a.kv["mode"] = saved.at("mode").as_string();
+      TZ_CHECK(!a.flag("sim"), "--run needs a GPU");
+    }
     const int rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", 0);
     const int size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1);
     const int local = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", rank);
@@ -116,23 +161,47 @@ int main(int argc, char **argv) {
       TZ_HIP(hipSetDevice(device));
     }
 
+    if (a.flag("run")) {
+      const int64_t want = saved.at("ranks").as_int();
+      TZ_CHECK(want == size, "schedule was searched on " << want << " ranks, this run has " << size);
+    }
+    // the workload options in effect (python-style keys: what --save-best records)
+    Json wargs = Json::object();
+    auto opt = [&](const std::string &k, const std::string &d) {
+      const std::string v = a.get(k, d);
+      wargs[py_key(k)] = v;
+      return v;
+    };
+    auto optn = [&](const std::string &k, double d) {
+      const double v = a.num(k, d);
+      if (v == std::floor(v) && std::fabs(v) < 9e15) wargs[py_key(k)] = int64_t(v);
+      else wargs[py_key(k)] = v;
+      return v;
+    };
+    auto optf = [&](const std::string &k) {
+      const bool v = a.flag(k);
+      wargs[py_key(k)] = v;
+      return v;
+    };
+    wargs["workload"] = workload;
+    wargs["streams"] = streams;
     auto g = std::make_shared<Graph>();
     std::shared_ptr<HaloExchange> halo;
     std::shared_ptr<DistSpmv> spmv;
     if (workload == "halo" || workload == "halo+spmv") {
       HaloArgs h;
-      h.nx = h.ny = h.nz = int(a.num("halo-n", 512));
-      h.nq = int(a.num("nq", 3));
-      h.ghost = int(a.num("ghost", 3));
-      h.neighbors = int(a.num("neighbors", 6));
-      h.fuse = a.get("fuse", "none");
-      h.transport = a.get("transport", "auto");
-      h.order = a.get("order", "xyzq");
-      h.stencil = a.flag("stencil");
-      h.relay = a.get("relay", "auto");
+      h.nx = h.ny = h.nz = int(optn("halo-n", 512));
+      h.nq = int(optn("nq", 3));
+      h.ghost = int(optn("ghost", 3));
+      h.neighbors = int(optn("neighbors", 6));
+      h.fuse = opt("fuse", "none");
+      h.transport = opt("transport", "auto");
+      h.order = opt("order", "xyzq");
+      h.stencil = optf("stencil");
+      h.relay = opt("relay", "auto");
       {
         // comma-separated relayed shares, e.g. 0.15,0.2
-        const std::string fr = a.get("relay-fracs", "");
+        const std::string fr = opt("relay-fracs", "0.15,0.2");
         if (!fr.empty()) {
           h.relay_fracs.clear();
           std::stringstream ss(fr);
@@ -143,7 +212,7 @@ int main(int argc, char **argv) {
       TZ_CHECK(h.order == "xyzq" || h.order == "qxyz", "--order must be xyzq or qxyz");
       h.rank = rank;
       h.size = size;
-      const std::string rg = a.get("rank-grid", "");
+      const std::string rg = opt("rank-grid", "");
       if (!rg.empty()) {
         TZ_CHECK(std::sscanf(rg.c_str(), "%dx%dx%d", &h.px, &h.py, &h.pz) == 3,
                  "--rank-grid must look like 2x2x2");
@@ -154,14 +223,14 @@ int main(int argc, char **argv) {
     }
     if (workload == "spmv" || workload == "halo+spmv") {
       SpmvArgs s;
-      s.m = int64_t(a.num("spmv-m", 150000));
-      s.matrix = a.get("spmv-matrix", "");
+      s.m = int64_t(optn("spmv-m", 150000));
+      s.matrix = opt("spmv-matrix", "");
       s.rank = rank;
       s.size = size;
       s.prefix = workload == "halo+spmv" ? "spmv_" : "";
-      s.form = a.get("spmv-form", "choice");
-      s.transport = a.get("spmv-transport", "auto");
-      s.library = a.get("spmv-library", "adaptive");
+      s.form = opt("spmv-form", "choice");
+      s.transport = opt("spmv-transport", "auto");
+      s.library = opt("spmv-library", "adaptive");
       spmv = std::make_shared<DistSpmv>(s);
       if (!sim) spmv->setup(ctrl.get());
       spmv->add_to_graph(*g);
@@ -184,7 +253,7 @@ int main(int argc, char **argv) {
 
     Platform plat = Platform::make_n_streams(streams);
     // CU-partitioned streams are distinguishable resources: no symmetric-stream pruning
-    if (a.flag("cu-partition")) plat.symmetric_streams = false;
+    if (optf("cu-partition")) plat.symmetric_streams = false;
     std::unique_ptr<HipRuntime> rt;
     std::unique_ptr<Benchmarker> bench;
     if (sim) {
@@ -194,7 +263,7 @@ int main(int argc, char **argv) {
       ro.n_streams = streams;
       ro.mode = a.get("mode", "eager") == "graph" ? ExecMode::Graph : ExecMode::Eager;
       ro.watchdog_s = a.num("watchdog", 60);
-      ro.graph_unroll = int(a.num("graph-unroll", 1));
+      ro.graph_unroll = int(a.num("graph-unroll", a.flag("run") ? 20 : 1));
       ro.cu_partition = a.flag("cu-partition");
       rt = std::make_unique<HipRuntime>(ro);
       bench = std::make_unique<EmpiricalBenchmarker>(*rt, *ctrl);
@@ -202,6 +271,51 @@ int main(int argc, char **argv) {
     BenchOpts bo;
     bo.n_iters = int64_t(a.num("bench-iters", 50));
     bo.target_secs = a.num("target-secs", 0.01);
+    bo.race_ratio = a.num("race-ratio", 0.0);
+
+    if (a.flag("run")) {
+      // a saved schedule: rebuilt by op name, proven race-free on the graph it executes,
+      // checked once from a fresh state, then timed (max over ranks)
+      const Sequence seq = OpIndex(*g).sequence_from_json(saved.at("schedule"));
+      const auto bad = verify(seq, *resolve_graph(*g, seq), streams);
+      TZ_CHECK(bad.empty(), "schedule is not race-free on this graph: " << bad.front().desc());
+      if (halo) halo->init_grid();
+      if (spmv) spmv->reset_y();
+      rt->device_sync();
+      rt->prepare(seq);
+      rt->run(1);
+      rt->device_sync();
+      double bad_cells = halo ? double(halo->check_grid()) + double(halo->ipc_errors()) : 0.0;
+      double err = spmv ? spmv->check() : 0.0;
+      ctrl->allreduce_sum(&bad_cells, 1);
+      ctrl->allreduce_max(&err, 1);
+      const int64_t iters = int64_t(a.num("run-iters", 1000));
+      rt->run(int64_t(a.num("run-warmup", 50)));
+      rt->device_sync();
+      ctrl->barrier();
+      const auto t0 = std::chrono::steady_clock::now();
+      rt->run(iters);
+      rt->device_sync();
+      double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      ctrl->allreduce_max(&dt, 1);
+      const bool ok = bad_cells == 0 && err < 1e-4;
+      if (rank == 0) {
+        Json o;
+        o["schedule"] = a.get("run", "");
+        o["workload"] = workload;
+        o["ranks"] = size;
+        o["streams"] = streams;
+        o["mode"] = rt->effective_mode() == ExecMode::Graph ? "graph" : "eager";
+        o["iters"] = iters;
+        o["ms_per_iter"] = dt / double(std::max<int64_t>(iters, 1)) * 1e3;
+        if (halo) o["halo_bad_cells"] = int64_t(bad_cells);
+        if (spmv) o["spmv_max_rel_err"] = err;
+        if (saved.contains("pct10_ms")) o["searched_pct10_ms"] = saved.at("pct10_ms");
+        o["correct"] = ok;
+        std::cout << o.dump() << "\n";
+      }
+      return ok ? 0 : 3;
+    }
 
     SearchResult res;
     if (a.get("solver", "mcts") == "dfs") {
@@ -272,6 +386,17 @@ int main(int argc, char **argv) {
       }
       if (bad >= 0) s["verified_bad_cells"] = bad;
       std::cerr << s.dump() << "\n";
+      if (a.flag("save-best") && b >= 0) {
+        Json doc;
+        doc["tenzing_amd"] = std::string("native");
+        doc["ranks"] = size;
+        doc["mode"] = a.get("mode", "eager");
+        doc["pct10_ms"] = res.sims[b].res.pct10 * 1e3;
+        doc["args"] = wargs;
+        doc["schedule"] = res.sims[b].seq.json(true);
+        std::ofstream f(a.get("save-best", "best.json"));
+        f << doc.dump() << "\n";
+      }
     }
     return bad > 0 ? 3 : 0;
   } catch (const std::exception &e) {

@@ -153,3 +153,23 @@ def test_save_best_then_load(tmp_path):
 
         with pytest.raises(SystemExit, match="race-free"):
             cli.load_schedule(bad, tz.SelfCtrl(), -1, False)
+
+
+def test_native_save_best_loads_in_python(tmp_path):
+    """tz-search --save-best writes the same document format as the Python CLI (python-style
+    option keys, the reference's schedule JSON), so either CLI can run the other's schedules"""
+    import tenzing_amd as tz
+    from tenzing_amd import cli
+
+    path = tmp_path / "nbest.json"
+    exe = os.path.join(ROOT, "tenzing_amd", "bin", "tz-search")
+    r = subprocess.run([exe, "--sim", "--workload", "halo+spmv", "--neighbors", "26", "--streams",
+                        "3", "--iters", "12", "--bench-iters", "2", "--fuse", "choice",
+                        "--save-best", str(path), "--csv", str(tmp_path / "n.csv")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    doc = json.loads(path.read_text())
+    assert doc["args"]["halo_n"] == 512 and doc["args"]["workload"] == "halo+spmv"
+    assert doc["args"]["fuse"] == "choice" and doc["args"]["stencil"] is False
+    w, g, wl, seq = cli.load_schedule(doc, tz.SelfCtrl(), -1, False)
+    assert w.workload == "fused" and w.streams == 3 and len(seq) == len(doc["schedule"])

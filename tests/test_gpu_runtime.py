@@ -497,3 +497,10 @@ def test_search_save_best_then_run(tz, gpu, tmp_path, workload):
         assert r["halo_bad_cells"] == 0
     else:
         assert r["halo_bad_cells"] == 0 and r["spmv_max_rel_err"] < 1e-4
+    # the native CLI runs the same document
+    exe = os.path.join(root, "tenzing_amd", "bin", "tz-search")
+    n = subprocess.run([exe, "--run", str(path), "--run-iters", "200", "--run-warmup", "10"],
+                       cwd=root, capture_output=True, text=True, timeout=240)
+    assert n.returncode == 0, n.stderr[-3000:]
+    rn = json.loads(n.stdout.strip().splitlines()[-1])
+    assert rn["correct"] and rn["mode"] == "graph" and rn["halo_bad_cells"] == 0
