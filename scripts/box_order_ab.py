@@ -28,8 +28,8 @@ def main():
                       tz.SelfCtrl(), device=0)
     st = torch.cuda.current_stream()
     dirs = list(range(h.ndirs()))
-    kind = {i: sum(1 for c in (h.dir(i).dx, h.dir(i).dy, h.dir(i).dz) if c) for i in dirs}
-    xface = [i for i in dirs if kind[i] == 1 and h.dir(i).dx != 0]
+    kind = {i: sum(1 for c in h.dir(i) if c) for i in dirs}  # dir(i) = (dx, dy, dz)
+    xface = [i for i in dirs if kind[i] == 1 and h.dir(i)[0] != 0]
     faces = [i for i in dirs if kind[i] == 1]
     rest = [i for i in dirs if kind[i] > 1]
     orders = {

@@ -3,8 +3,9 @@
 // IPC / SDMA transport: halo_ipc.cpp; op graph: halo_graph.cpp; stencil: halo_stencil.cpp.
 #include "halo_internal.hpp"
 
-namespace tz {
+#include <algorithm>
 
+namespace tz {
 
 Json HaloArgs::json() const {
   Json j;
@@ -526,7 +527,16 @@ void HaloExchange::shift_group(const std::vector<int> &dirs, void *stream, int s
   }
 }
 
-void HaloExchange::direct_group(const std::vector<int> &dirs, void *stream) const {
+void HaloExchange::direct_group(const std::vector<int> &dirs_in, void *stream) const {
+  // faces first, then edges, then corners: blocks are dispatched box by box in batch order,
+  // and leaving the many small edge/corner boxes for the last waves measured best (fused
+  // 26-direction move 44.13 us vs 44.23 in the natural order and 45.18 with the small boxes
+  // first; scripts/box_order_ab.py, profiles/r2_box_order/)
+  std::vector<int> dirs = dirs_in;
+  std::stable_sort(dirs.begin(), dirs.end(), [&](int a, int b) {
+    auto k = [&](int i) { return (dirs_[i].dx != 0) + (dirs_[i].dy != 0) + (dirs_[i].dz != 0); };
+    return k(a) < k(b);
+  });
   std::vector<kern::MoveDesc> ms;
   for (int i : dirs) {
     TZ_CHECK(i >= 0 && i < ndirs() && direct_[i], "direction " << i << " is not a direct (self) transfer");
