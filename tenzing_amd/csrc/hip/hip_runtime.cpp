@@ -199,12 +199,22 @@ void HipRuntime::stream_wait(int waiter, int waitee) {
 
 void HipRuntime::device_sync() { TZ_HIP(hipDeviceSynchronize()); }
 
+void HipRuntime::destroy_exec(void *exec) {
+  if (!exec) return;
+  hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec));
+  auto it = graphOf_.find(exec);
+  if (it != graphOf_.end()) {
+    hipGraphDestroy(static_cast<hipGraph_t>(it->second));
+    graphOf_.erase(it);
+  }
+}
+
 void HipRuntime::destroy_graph() {
   if (!slots_.empty()) {
     // the current graphs are borrowed from a slot
     for (Slot &s : slots_) {
-      if (s.exec) hipGraphExecDestroy(static_cast<hipGraphExec_t>(s.exec));
-      if (s.execU) hipGraphExecDestroy(static_cast<hipGraphExec_t>(s.execU));
+      destroy_exec(s.exec);
+      destroy_exec(s.execU);
     }
     slots_.clear();
     graphExec_ = graphExecU_ = nullptr;
@@ -212,12 +222,12 @@ void HipRuntime::destroy_graph() {
     return;
   }
   if (graphExec_) {
-    hipGraphExecDestroy(static_cast<hipGraphExec_t>(graphExec_));
+    destroy_exec(graphExec_);
     graphExec_ = nullptr;
     graphNodes_ = graphEdges_ = 0;
   }
   if (graphExecU_) {
-    hipGraphExecDestroy(static_cast<hipGraphExec_t>(graphExecU_));
+    destroy_exec(graphExecU_);
     graphExecU_ = nullptr;
   }
 }
@@ -312,15 +322,20 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
     }
     hipGraphExec_t exec = nullptr;
     TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-    TZ_HIP(hipGraphDestroy(graph));
+    graphOf_[exec] = graph; // destroyed with the exec (destroy_exec)
     graph = nullptr;
     nodesOut = real;
     edgesOut = edges;
     TZ_LOG(Debug, "graph mode: " << iterations << " iteration(s), " << real << " nodes, " << edges
                                  << " edges");
     // upload once so the first timed launch does not pay for it
-    TZ_HIP(hipGraphUpload(exec, S(streams_[0])));
-    TZ_HIP(hipStreamSynchronize(S(streams_[0])));
+    try {
+      TZ_HIP(hipGraphUpload(exec, S(streams_[0])));
+      TZ_HIP(hipStreamSynchronize(S(streams_[0])));
+    } catch (...) {
+      destroy_exec(exec);
+      throw;
+    }
     return exec;
   } catch (...) {
     if (graph) hipGraphDestroy(graph);
@@ -365,8 +380,8 @@ void HipRuntime::prepare_many(const std::vector<Sequence> &seqs) {
     }
   } catch (...) {
     for (Slot &s : slots) {
-      if (s.exec) hipGraphExecDestroy(static_cast<hipGraphExec_t>(s.exec));
-      if (s.execU) hipGraphExecDestroy(static_cast<hipGraphExec_t>(s.execU));
+      destroy_exec(s.exec);
+      destroy_exec(s.execU);
     }
     throw;
   }

@@ -27,6 +27,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace tz {
@@ -125,6 +126,10 @@ private:
   Sequence seq_;
   void *graphExec_ = nullptr;  // one iteration
   void *graphExecU_ = nullptr; // unroll_ iterations
+  // the source graph of every instantiated exec, destroyed together with it (not right after
+  // instantiation: some HIP releases keep referring to the source graph's nodes from the exec)
+  std::unordered_map<void *, void *> graphOf_;
+  void destroy_exec(void *exec);
   int unroll_ = 1;
   bool spinSync_ = true;
   size_t graphNodes_ = 0, graphEdges_ = 0;
