@@ -504,3 +504,21 @@ def test_search_save_best_then_run(tz, gpu, tmp_path, workload):
     assert n.returncode == 0, n.stderr[-3000:]
     rn = json.loads(n.stdout.strip().splitlines()[-1])
     assert rn["correct"] and rn["mode"] == "graph" and rn["halo_bad_cells"] == 0
+
+
+def test_graph_mode_many_prepares(tz, gpu):
+    """regression: a prepare/run loop over many schedules in graph mode (with and without
+    unrolling) crashed inside hipGraphLaunch while each source hipGraph was destroyed right after
+    instantiation; source graphs now live as long as their execs"""
+    halo, g = _small_halo(tz, neighbors=26, fuse="choice", order="qxyz", n=128)
+    seqs = [tz.random_rollout(tz.State(g, tz.Platform(4)), s) for s in range(24)]
+    for unroll in (1, 6):
+        rt = tz.HipRuntime(device=0, n_streams=4, mode=tz.ExecMode.Graph, graph_unroll=unroll)
+        for seq in seqs:
+            halo.init_grid()
+            rt.prepare(seq)
+            assert rt.effective_mode == tz.ExecMode.Graph
+            rt.run(unroll + 1)
+            rt.device_sync()
+            assert halo.check_grid() == 0, seq.desc()
+        del rt
