@@ -404,6 +404,13 @@ TEST(choice_and_compound_in_search) {
   OpIndex idx(*g);
   Sequence back = idx.sequence_from_json(Json::parse(r.sims[0].seq.json().dump()));
   CHECK(back.canonical_key() == r.sims[0].seq.canonical_key());
+  // ... and verify against the graph they executed (choice resolved, compound expanded)
+  for (const auto &sim : r.sims) {
+    Sequence loaded = idx.sequence_from_json(sim.seq.json(true));
+    GraphPtr fg = resolve_graph(*g, loaded);
+    CHECK(fg->find("comp") < 0 && fg->find("y") < 0 && fg->find("x") >= 0);
+    CHECK(verify(loaded, *fg, 2).empty());
+  }
 }
 
 TEST(mcts_checkpoint_resume) {
