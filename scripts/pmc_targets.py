@@ -3,7 +3,8 @@
 (all 26 directions), fused pack / unpack, the SpMV kernels and rocSPARSE's CSR SpMV, each a
 few times.
 
-  rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --output-format csv -d out -- python3 scripts/pmc_targets.py
+  rocprofv3 --pmc FETCH_SIZE --output-format csv -d out -- python3 scripts/pmc_targets.py
+  rocprofv3 --pmc WRITE_SIZE ... -- python3 scripts/pmc_targets.py --only-move 20   # headline only
 """
 import os
 import sys
@@ -20,6 +21,14 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     hd, _ = build_halo(HaloConfig(n=512, neighbors=26, order="qxyz", transport="direct"),
                        tz.SelfCtrl(), device=0)
+    if len(sys.argv) > 2 and sys.argv[1] == "--only-move":
+        # steady state of the headline: the 26-direction move back to back, as in the hipGraph
+        # loop (the caches hold what the previous exchange left)
+        alld = list(range(hd.ndirs()))
+        for _ in range(int(sys.argv[2])):
+            hd.direct_group(alld, st)
+        torch.cuda.synchronize()
+        return
     hc, _ = build_halo(HaloConfig(n=512, neighbors=26, order="qxyz", transport="copy"),
                        tz.SelfCtrl(), device=0)
     alld = list(range(hd.ndirs()))
