@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -47,6 +48,11 @@ Json BenchOpts::json() const {
 
 // ---------------------------------------------------------------- Empirical
 
+EmpiricalBenchmarker::EmpiricalBenchmarker(ExecutorRunner &runner, Ctrl &ctrl)
+    : runner_(runner), ctrl_(ctrl) {
+  if (const char *e = std::getenv("TZ_HALF_GAP_SIZING")) halfGapSizing_ = std::atoi(e) != 0;
+}
+
 EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, double targetSecs,
                                                                 bool deviceTimer) {
   Measurement m{std::max<int64_t>(1, nHint), 0};
@@ -73,8 +79,20 @@ EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, d
     if (elapsed < targetSecs) {
       const double perSample = std::max(elapsed / double(m.n), 1e-9);
       const double est = targetSecs / perSample * 1.1;
-      m.n += int64_t(std::ceil((est - double(m.n)) * 0.5));
+      if (halfGapSizing_) {
+        m.n += int64_t(std::ceil((est - double(m.n)) * 0.5));
+      } else {
+        // a batch that ran for an eighth of the target or more is long enough to time, so it
+        // sizes the next batch directly (the 10 % margin lands it past the target); a shorter
+        // one is dominated by launch latency and grows 8x at most. A candidate is sized in ~3
+        // runs (about 1.3x the target) instead of ~6 runs (about 4.5x) when closing half the
+        // gap per run.
+        const int64_t jump = int64_t(std::ceil(est));
+        m.n = elapsed >= targetSecs / 8 ? jump : std::min(jump, m.n * 8);
+      }
       m.n = std::max<int64_t>(m.n, 1);
+      const int64_t k = std::max<int64_t>(1, runner_.batch_multiple());
+      m.n = (m.n + k - 1) / k * k;
     } else {
       m.time = elapsed / double(m.n);
       return m;

@@ -71,6 +71,9 @@ public:
     run(n);
     return -1.0;
   }
+  /// batch sizes that run without a remainder (a compiled graph of K unrolled iterations: K),
+  /// so a measurement times the same launches as a long run does
+  virtual int64_t batch_multiple() const { return 1; }
 
 private:
   std::vector<Sequence> many_;
@@ -78,7 +81,7 @@ private:
 
 class EmpiricalBenchmarker : public Benchmarker {
 public:
-  EmpiricalBenchmarker(ExecutorRunner &runner, Ctrl &ctrl) : runner_(runner), ctrl_(ctrl) {}
+  EmpiricalBenchmarker(ExecutorRunner &runner, Ctrl &ctrl);
   BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) override;
   /// Several schedules measured interleaved (reference src/benchmarker.cpp:21-76): every
   /// iteration runs each schedule once (one batched measurement) in a random order chosen by
@@ -102,6 +105,9 @@ private:
   Ctrl &ctrl_;
   double best_ = 0.0; // best complete pct10 seen (racing); identical on every rank
   int64_t raced_ = 0;
+  // batch sizing closes half the gap to the target per run (round-1 rule, env
+  // TZ_HALF_GAP_SIZING=1 for A/B runs; must be the same on every rank)
+  bool halfGapSizing_ = false;
 };
 
 /// Host-only executor: GPU ops are launched with a null stream, synchronously (tests/CPU runs).

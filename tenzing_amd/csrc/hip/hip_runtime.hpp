@@ -71,6 +71,7 @@ public:
   /// run(n) bracketed by timing events on stream 0 (every op of a schedule follows the first
   /// event, and the schedule's closing host syncs precede the last): device seconds
   double run_device_timed(int64_t n) override;
+  int64_t batch_multiple() const override { return graphExecU_ ? unroll_ : 1; }
   /// graph mode: every sequence is compiled once and kept; select() switches without rebuilding
   void prepare_many(const std::vector<Sequence> &seqs) override;
   void select(size_t k) override;
