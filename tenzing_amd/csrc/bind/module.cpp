@@ -656,6 +656,8 @@ PYBIND11_MODULE(_tz, m) {
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("aborted", &RcclComm::aborted);
   m.def("rccl_abort_all", &rccl_abort_all, py::call_guard<py::gil_scoped_release>());
+  m.def("node_identity", []() { return py::bytes(node_identity()); },
+        "this machine as exchanged with IPC handles (host name | boot id, fixed size)");
   m.def("make_rccl_comms", &make_rccl_comms, py::arg("ctrl"), py::arg("device"), py::arg("n"),
         "n communicators over the same ranks (one per logical stream), one broadcast of ids");
 

@@ -92,7 +92,7 @@ std::string HaloExchange::setup_ipc(Ctrl *ctrl) {
       if (p) TZ_HIP(hipIpcGetMemHandle(&h, p));
       return std::string(reinterpret_cast<const char *>(&h), H);
     };
-    mine = handle_of(flags_);
+    mine = node_identity() + handle_of(flags_);
     if (ipcGrid_) {
       mine += handle_of(grid());
     } else {
@@ -109,11 +109,15 @@ std::string HaloExchange::setup_ipc(Ctrl *ctrl) {
   }
   const std::vector<std::string> all = ctrl->allgather(mine);
   if (!err.empty()) return err;
+  const std::string me = node_identity();
   auto open = [&](const std::string &blob, size_t k) {
-    TZ_CHECK(blob.size() >= (k + 1) * H, "a peer exported no IPC handles");
+    TZ_CHECK(blob.size() >= kNodeIdBytes + (k + 1) * H, "a peer exported no IPC handles");
+    // a handle is only meaningful on the node that exported it
+    TZ_CHECK(blob.compare(0, kNodeIdBytes, me) == 0, "a peer runs on another node");
+    const char *at = blob.data() + kNodeIdBytes + k * H;
     hipIpcMemHandle_t h;
-    std::memcpy(&h, blob.data() + k * H, H);
-    TZ_CHECK(std::any_of(blob.data() + k * H, blob.data() + (k + 1) * H, [](char c) { return c != 0; }),
+    std::memcpy(&h, at, H);
+    TZ_CHECK(std::any_of(at, at + H, [](char c) { return c != 0; }),
              "a peer exported no IPC handle in slot " << k);
     void *p = nullptr;
     TZ_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));

@@ -545,6 +545,7 @@ std::string DistSpmv::setup_ipc(Ctrl *ctrl) {
     TZ_HIP(hipMemset(err_.get(), 0, sizeof(int)));
     TZ_HIP(hipDeviceSynchronize());
     hipIpcMemHandle_t h;
+    mine = node_identity();
     TZ_HIP(hipIpcGetMemHandle(&h, flags_));
     mine.append(reinterpret_cast<const char *>(&h), H);
     TZ_HIP(hipIpcGetMemHandle(&h, dXr_.get()));
@@ -556,6 +557,7 @@ std::string DistSpmv::setup_ipc(Ctrl *ctrl) {
   }
   const std::vector<std::string> all = ctrl->allgather(mine);
   if (!err.empty()) return err;
+  const std::string me = node_identity();
   try {
     TZ_CHECK(all.size() == P, "allgather returned " << all.size() << " entries");
     peerXr_.assign(P, nullptr);
@@ -564,10 +566,13 @@ std::string DistSpmv::setup_ipc(Ctrl *ctrl) {
     for (int q = 0; q < a_.size; ++q) {
       if (q == a_.rank || (sendCount_[q] == 0 && recvCount_[q] == 0)) continue;
       const std::string &blob = all[size_t(q)];
-      TZ_CHECK(blob.size() == 2 * H + P * sizeof(int32_t), "rank " << q << " exported no IPC handles");
+      TZ_CHECK(blob.size() == kNodeIdBytes + 2 * H + P * sizeof(int32_t),
+               "rank " << q << " exported no IPC handles");
+      // a handle is only meaningful on the node that exported it
+      TZ_CHECK(blob.compare(0, kNodeIdBytes, me) == 0, "rank " << q << " runs on another node");
       auto open = [&](size_t k) {
         hipIpcMemHandle_t h;
-        std::memcpy(&h, blob.data() + k * H, H);
+        std::memcpy(&h, blob.data() + kNodeIdBytes + k * H, H);
         void *ptr = nullptr;
         TZ_HIP(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
         opened_.push_back(ptr);
@@ -576,7 +581,8 @@ std::string DistSpmv::setup_ipc(Ctrl *ctrl) {
       peerFlags_[size_t(q)] = open(0);
       if (sendCount_[q] > 0) {
         peerXr_[size_t(q)] = open(1);
-        std::memcpy(&peerRecvOff_[size_t(q)], blob.data() + 2 * H + size_t(a_.rank) * sizeof(int32_t),
+        std::memcpy(&peerRecvOff_[size_t(q)],
+                    blob.data() + kNodeIdBytes + 2 * H + size_t(a_.rank) * sizeof(int32_t),
                     sizeof(int32_t));
       }
     }

@@ -92,6 +92,12 @@ private:
   int blocks_;
 };
 
+/// This machine, as a fixed-size string (host name and boot id): the IPC transports exchange it
+/// with their handles and map a peer's memory only when the peer runs on the same node. A
+/// handle from another node must never be opened.
+constexpr size_t kNodeIdBytes = 96;
+std::string node_identity();
+
 // ------------------------------------------------------------------ halo exchange
 
 struct HaloArgs {

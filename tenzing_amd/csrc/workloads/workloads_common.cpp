@@ -1,5 +1,9 @@
 #include "workloads.hpp"
 
+#include <unistd.h>
+
+#include <fstream>
+
 #include "core/util.hpp"
 #include "hip/hip_runtime.hpp"
 
@@ -34,6 +38,18 @@ void DeviceBuffer::upload(const void *src, size_t bytes) {
 void DeviceBuffer::download(void *dst, size_t bytes) const {
   TZ_CHECK(bytes <= bytes_, "download overflow");
   if (bytes) TZ_HIP(hipMemcpy(dst, p_, bytes, hipMemcpyDeviceToHost));
+}
+
+std::string node_identity() {
+  char host[64] = {0};
+  gethostname(host, sizeof(host) - 1);
+  std::string id(host);
+  std::ifstream f("/proc/sys/kernel/random/boot_id");
+  std::string boot;
+  if (f) std::getline(f, boot);
+  id += "|" + boot;
+  id.resize(kNodeIdBytes, '\0');
+  return id;
 }
 
 void EmptyKernelOp::launch(void *stream, Executor &) const { kern::empty(stream); }

@@ -344,3 +344,12 @@ def test_resolve_graph_flags_a_dropped_sync(tz):
         assert tz.verify(cut, tz.resolve_graph(g, cut), 2) != []
         return
     pytest.skip("no rollout needed a cross-stream wait")
+
+
+def test_node_identity_is_fixed_size_and_stable(tz):
+    """IPC handles travel with this id; a peer maps them only when the ids match (same node)"""
+    import socket
+
+    a, b = tz._tz.node_identity(), tz._tz.node_identity()
+    assert a == b and len(a) == 96
+    assert a.split(b"|")[0] == socket.gethostname().encode()[:63]
