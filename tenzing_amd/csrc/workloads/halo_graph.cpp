@@ -245,6 +245,30 @@ void HaloExchange::add_relay_part(Graph &g, const std::vector<int> &remote, doub
   g.then_finish(u);
 }
 
+void HaloExchange::add_mixed_part(Graph &g, const std::vector<int> &remote) {
+  // A link that one engine cannot fill may carry more with two: when both faces of an axis go
+  // to the same peer (a dimension of 2 ranks), the + face goes by CU stores and the - face by
+  // the copy engines, concurrently if the search puts the two ops on different streams. Both
+  // engines signal the same arrival counters, so one wait and one unpack serve both.
+  auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
+  std::vector<int> byKernel, byCopy;
+  for (int i : remote) {
+    const Dir &d = dirs_[i];
+    const bool face = (d.dx != 0) + (d.dy != 0) + (d.dz != 0) == 1;
+    (face && d.dx + d.dy + d.dz < 0 ? byCopy : byKernel).push_back(i);
+  }
+  auto w = std::make_shared<HaloWait>(self, remote, "mx");
+  auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::UnpackRelease, remote, "mx");
+  for (auto &[dirs, st] : {std::pair{byKernel, HaloStageGroup::Put}, std::pair{byCopy, HaloStageGroup::CopyPut}}) {
+    if (dirs.empty()) continue;
+    auto p = std::make_shared<HaloStageGroup>(self, st, dirs, "mx");
+    g.start_then(p);
+    g.then(p, w);
+  }
+  g.then(w, u);
+  g.then_finish(u);
+}
+
 void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, int via) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   for (int i : dirs) {
@@ -477,6 +501,9 @@ void HaloExchange::add_exchange(Graph &g) {
     auto gr = std::make_shared<Graph>();
     add_ipc_part(*gr, remote, kViaCopy);
     alts.push_back(std::make_shared<StaticCompoundOp>("he_via_sdma", gr));
+    auto mx = std::make_shared<Graph>();
+    add_mixed_part(*mx, remote);
+    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_mixed", mx));
   }
   if (uses_relay()) {
     if (a_.relay == "force") alts.clear();

@@ -287,6 +287,9 @@ private:
                      const std::string &pre); // fuse mode over `dirs`
   void add_ipc_part(Graph &g, const std::vector<int> &remote, int via);
   void add_relay_part(Graph &g, const std::vector<int> &remote, double frac);
+  /// buffers mode: the two faces of every axis go to their peers by different engines at once
+  /// (positive side: kernel puts, negative side: copy-engine puts; edges and corners: kernel)
+  void add_mixed_part(Graph &g, const std::vector<int> &remote);
   void check_pipelined(int i) const;
   std::string setup_ipc(Ctrl *ctrl); // "" on success, else why IPC cannot be used
   void ipc_preflight(Ctrl *ctrl);    // one verified exchange; disables IPC collectively on failure

@@ -39,10 +39,17 @@ def main():
             for mode in [tz.ExecMode.Eager if m == "eager" else tz.ExecMode.Graph for m in modes]:
                 rt.set_mode(mode)
                 rt.set_graph_unroll(3 if mode == tz.ExecMode.Graph else 1)
+                need = os.environ.get("TZ_TEST_REQUIRE", "")  # an op-name prefix every run uses
+                draw = 0
                 for seed in range(int(os.environ.get("TZ_TEST_SEEDS", "3"))):
                     msg = ""
                     if ctrl.rank == 0:
-                        msg = tz.random_rollout(tz.State(g, tz.Platform(3)), seed).json(True)
+                        for _ in range(400):
+                            cand = tz.random_rollout(tz.State(g, tz.Platform(3)), draw)
+                            draw += 1
+                            if not need or any(o.name.startswith(need) for o in cand.ops()):
+                                break
+                        msg = cand.json(True)
                     seq = tz.OpIndex(g).sequence_from_json(ctrl.bcast(msg, 0).decode())
                     halo.init_grid()
                     say("init_grid", seed)
@@ -67,7 +74,8 @@ def main():
                                     copyput=any(o.name.startswith("he_copyput_")
                                                 for o in seq.ops()),
                                     relay=any(o.name.startswith("he_rl") for o in seq.ops()),
-                                    relay_sdma=any(o.name.endswith("_fwdcp") for o in seq.ops())))
+                                    relay_sdma=any(o.name.endswith("_fwdcp") for o in seq.ops()),
+                                    mixed=any(o.name == "he_copyput_mx" for o in seq.ops())))
             if os.environ.get("TZ_TEST_NO_MCTS"):
                 continue
             # a short collective search over ipc schedules

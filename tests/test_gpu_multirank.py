@@ -76,6 +76,23 @@ def test_ipc_halo_loopback(gpu, world, mode):
             assert used == (mode == "buffers"), [run["copyput"] for run in r["runs"]]
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_mixed_engines_loopback(gpu, world):
+    """buffers mode's mixed transport: the + face of every axis by CU stores, the - face by the
+    copy engines, into the same receive buffers and arrival counters; every ghost right, eager
+    and as hipGraphs, over repeated exchanges"""
+    extra = {"TZ_IPC_GRID": "0", "TZ_TEST_FUSES": "choice", "TZ_TEST_REQUIRE": "he_copyput_mx",
+             "TZ_TEST_SEEDS": "2", "TZ_TEST_NO_MCTS": "1"}
+    if world == 8:
+        extra.update(TZ_TEST_N="24", TZ_TEST_RELAY="off")
+    res = _launch("ipc_halo", world, extra_env=extra)
+    for r in res:
+        assert r["runs"], r
+        for run in r["runs"]:
+            assert run["mixed"] and run["copyput"], run
+            assert run["bad1"] == 0 and run["bad2"] == 0 and run["err"] == 0, run
+
+
 def test_relay_routing_loopback(gpu):
     """the 2x2x2 grid with every remote direction through relay routing (a share of each face
     via the corner peer, forwarded over its edge-diagonal link): every ghost right on all 8
