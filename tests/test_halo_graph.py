@@ -109,6 +109,15 @@ def test_ipc_transport_graph(tz, fuse, size, mode, monkeypatch):
             # relay routing (2x2x2, buffers mode): checked in test_relay_routing_graph
             seen.add("relay")
             continue
+        if "he_wait_mx" in names:
+            # buffers mode, mixed engines: + faces by kernel puts, - faces by copy-engine puts,
+            # both before the one wait, one unpack after it
+            seen.add("mx")
+            w = names.index("he_wait_mx")
+            assert names.index("he_put_mx") < w and names.index("he_copyput_mx") < w
+            assert names.index("he_unpack_mx") > w
+            assert not any(n.startswith(("he_pack_", "he_shift_")) for n in names)
+            continue
         # buffers mode also offers copy-engine puts (pack locally, SDMA copy, signal): a
         # ChoiceOp between the two, whose op names differ ("cp_")
         v = "cp_" if "he_wait_cp_remote" in names else ""
@@ -126,7 +135,10 @@ def test_ipc_transport_graph(tz, fuse, size, mode, monkeypatch):
         if fuse == "none":
             assert len(puts) == n_ipc
     seen.discard("relay")
-    assert seen == ({""} if mode == "grid" else {"", "cp_"})
+    if mode == "grid":
+        assert seen == {""}
+    else:  # 12 rollouts: at least two of the three put transports
+        assert len(seen) >= 2 and seen <= {"", "cp_", "mx"}, seen
 
 
 @pytest.mark.parametrize("transport", ["auto", "ipc"])
