@@ -46,7 +46,8 @@ def _start_deadline(seconds: float) -> None:
 
 def link_probe(tz, halo, ctrl, iters, rccl=False):
     """GB/s of ONE transfer over one xGMI link with each available transport (the +z face to
-    the +z neighbour, every rank at once, one transfer at a time), and the time the exchange's
+    the +z neighbour, every rank at once, one transfer at a time), of both z faces at once
+    (`pair_GBps`: kernel puts, copy engines, or one of each), and the time the exchange's
     busiest link (the peer receiving the most bytes) would take at the best of those rates. An
     exchange runs several transfers per link at once (several streams, copy engines), so it can
     beat that time; on loopback ranks (one GPU) the rates say nothing about xGMI."""
@@ -66,13 +67,26 @@ def link_probe(tz, halo, ctrl, iters, rccl=False):
             rates[via] = None
             if ctrl.rank == 0:
                 print(f"bench.py: link probe {via}: {e}", file=sys.stderr)
+    # both faces of the axis at once (one peer when the axis has 2 ranks): kernel puts, copy
+    # engines, or one of each concurrently -- what the busiest link carries in practice
+    pair = {}
+    if not halo.is_direct(halo.opposite(i)):
+        for how in ("put", "sdma", "mixed"):
+            try:
+                t = halo.link_probe(i, "pair_" + how, iters, ctrl)
+                pair[how] = 2.0 * face / t / 1e9
+            except Exception as e:  # noqa: BLE001  (collective: every rank skips together)
+                pair[how] = None
+                if ctrl.rank == 0:
+                    print(f"bench.py: link probe pair_{how}: {e}", file=sys.stderr)
     per_peer = {}
     for k in range(halo.ndirs()):
         if not halo.is_direct(k):
             per_peer[halo.neighbor(k)] = per_peer.get(halo.neighbor(k), 0.0) + 8.0 * halo.box_elems(k)
     busiest = max(per_peer.values()) if per_peer else 0.0
-    best = max([r for r in rates.values() if r], default=None)
-    return {"face_MB": face / 1e6, "GBps": rates, "busiest_link_MB": busiest / 1e6,
+    best = max([r for r in list(rates.values()) + list(pair.values()) if r], default=None)
+    return {"face_MB": face / 1e6, "GBps": rates, "pair_GBps": pair,
+            "busiest_link_MB": busiest / 1e6,
             "busiest_link_at_probe_rate_ms": (busiest / (best * 1e9) * 1e3) if best else None}
 
 

@@ -568,11 +568,45 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
   TZ_CHECK(ready() && ctrl && ctrl->size() == a_.size, "link probe needs a set-up exchange and its control plane");
   TZ_CHECK(dir >= 0 && dir < ndirs() && !direct_[dir], "direction " << dir << " is not remote");
   TZ_CHECK(iters >= 1, "iters must be positive");
-  const std::vector<int> d{dir};
-  hipStream_t s = nullptr;
+  // "pair_put" / "pair_sdma" / "pair_mixed": both faces of the axis at once (one peer when the
+  // dimension has 2 ranks), by kernel puts, copy engines, or one of each on two streams
+  const bool pair = via.rfind("pair_", 0) == 0;
+  const std::string how = pair ? via.substr(5) : via;
+  const std::vector<int> d = pair ? std::vector<int>{dir, opp_[dir]} : std::vector<int>{dir};
+  hipStream_t s = nullptr, s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  auto release = [&] {
+    if (s2) hipStreamDestroy(s2);
+    if (fork) hipEventDestroy(fork);
+    if (join) hipEventDestroy(join);
+    hipStreamDestroy(s);
+  };
+  if (how == "mixed") {
+    TZ_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    TZ_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    TZ_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  }
   auto once = [&] {
-    if (via == "put" || via == "sdma") {
+    if (pair && (how == "put" || how == "sdma" || how == "mixed")) {
+      TZ_CHECK(ipcReady_ && ipc_[d[0]] && ipc_[d[1]], "ipc transport not available");
+      if (how == "put") {
+        put_group(d, s);
+      } else if (how == "sdma") {
+        copy_put_group(d, s);
+      } else { // + face by CU stores on s, - face by the copy engines on s2, concurrently
+        TZ_HIP(hipEventRecord(fork, s));
+        TZ_HIP(hipStreamWaitEvent(s2, fork, 0));
+        put_group({d[0]}, s);
+        copy_put_group({d[1]}, s2);
+        TZ_HIP(hipEventRecord(join, s2));
+        TZ_HIP(hipStreamWaitEvent(s, join, 0));
+      }
+      wait_group(d, s);
+      if (!ipcGrid_) ipc_unpack_group(d, s);
+    } else if (pair) {
+      TZ_THROW("pair probes take put, sdma or mixed (got " << how << ")");
+    } else if (via == "put" || via == "sdma") {
       TZ_CHECK(ipcReady_ && ipc_[dir], "ipc transport not available");
       if (via == "put") put_group(d, s);
       else copy_put_group(d, s);
@@ -589,13 +623,15 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
   };
   // agree collectively that every rank can run the probe before any transfer is issued
   std::string err;
-  if ((via == "put" || via == "sdma") && !(ipcReady_ && ipc_[dir] && (via == "put" || (useCopy_ && !ipcGrid_))))
+  const bool ipcOk = ipcReady_ && ipc_[dir] && (!pair || ipc_[opp_[dir]]);
+  if ((how == "put" || how == "sdma" || how == "mixed") &&
+      !(ipcOk && (how == "put" || (useCopy_ && !ipcGrid_))))
     err = via + " unavailable";
   if (via == "rccl" && !(useRccl_ && pipe_[dir])) err = "rccl unavailable";
   double bad = err.empty() ? 0.0 : 1.0;
   ctrl->allreduce_max(&bad, 1);
   if (bad != 0) {
-    hipStreamDestroy(s);
+    release();
     TZ_THROW("link probe: " << (err.empty() ? via + " unavailable on another rank" : err));
   }
   // a local failure travels with the collectives (every rank makes the same calls), so all
@@ -606,7 +642,8 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
     if (v) *v = red[0];
     if (red[1] != 0.0) {
       hipStreamSynchronize(s);
-      hipStreamDestroy(s);
+      if (s2) hipStreamSynchronize(s2);
+      release();
       TZ_THROW("link probe (" << via << ") failed" << (e.empty() ? " on another rank" : ": " + e));
     }
   };
@@ -628,7 +665,7 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
     e = x.what();
   }
   agree(e, &t); // (also: peers may write into my buffers until every rank got here)
-  hipStreamDestroy(s);
+  release();
   return t;
 }
 

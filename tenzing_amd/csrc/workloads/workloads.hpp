@@ -270,7 +270,10 @@ public:
   /// neighbour there, `iters` times, through `via` ("put": kernel stores into the peer's
   /// memory, "sdma": copy engines, "rccl": pack + RCCL send/recv + unpack), one transfer at a
   /// time on one stream. Each transfer crosses one xGMI link per rank, so this measures what one
-  /// link carries with that transport. Returns seconds per transfer, max over ranks.
+  /// link carries with that transport. "pair_put" / "pair_sdma" / "pair_mixed" move both faces
+  /// of the axis at once (kernel puts, copy engines, or the + face by kernel and the - face by
+  /// copy engines on two streams): with 2 ranks along the axis both cross the same link.
+  /// Returns seconds per transfer, max over ranks.
   double link_probe(int dir, const std::string &via, int iters, Ctrl *ctrl);
   /// direct transport: move the interior slab facing each direction of `dirs` straight into
   /// the neighbour's ghost region on the opposite side (one launch)

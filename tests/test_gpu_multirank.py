@@ -132,6 +132,10 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     # kernel puts always; copy-engine puts need receive buffers; RCCL is refused in loopback
     assert p["GBps"]["put"] > 0 and "rccl" not in p["GBps"]
     assert (p["GBps"]["sdma"] is not None) == (mode == "buffers")
+    # both z faces at once (2 ranks: one peer): kernel puts always, copy engines and the
+    # kernel + copy-engine mix in buffers mode
+    assert p["pair_GBps"]["put"] > 0
+    assert (p["pair_GBps"]["sdma"] is not None) == (p["pair_GBps"]["mixed"] is not None) == (mode == "buffers")
     assert p["busiest_link_MB"] > p["face_MB"] > 0 and p["busiest_link_at_probe_rate_ms"] > 0
 
 
