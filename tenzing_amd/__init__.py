@@ -116,7 +116,7 @@ from ._tz import (  # noqa: E402,F401
     verify,
 )
 
-from .search import search  # noqa: E402,F401
+from .search import run, search  # noqa: E402,F401
 
 __version__ = _tz.version()
 

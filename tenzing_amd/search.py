@@ -9,6 +9,7 @@ C++ (tenzing-mcts/examples/halo_run_strategy.hpp:135-160, tenzing-dfs/examples/s
     res = tz.search(g, streams=2, iters=100)                  # MCTS on the GPU, hipGraph candidates
     res = tz.search(g, streams=2, solver="dfs", sim=True)     # exhaustive, cost model, no GPU
     best = res.sims[res.best()]
+    ms = tz.run(g, best.seq.json(True), streams=2)      # later: replay it, no search
 """
 from __future__ import annotations
 
@@ -71,3 +72,42 @@ def search(graph, streams: int = 2, solver: str = "mcts", iters: int = 100,
         res = _tz.mcts_explore(graph, plat, bench, ctrl, o)
     del bench, rt  # the runtime (and its streams) goes before the caller's tensors
     return res
+
+
+def run(graph, schedule, streams: int, iters: int = 100, warmup: int = 10, mode: str = "graph",
+        graph_unroll: int = 10, device: int | None = None, ctrl=None) -> float:
+    """Run a found schedule of ``graph`` without searching and return milliseconds per
+    iteration (max over ranks). ``schedule`` is a Sequence or its JSON (``seq.json(True)``, e.g.
+    read back from a file); it is first proven race-free on the graph it executes."""
+    import json as _json
+    import time
+
+    if not isinstance(schedule, _tz.Sequence):
+        text = schedule if isinstance(schedule, str) else _json.dumps(schedule)
+        schedule = _tz.OpIndex(graph).sequence_from_json(text)
+    bad = _tz.verify(schedule, _tz.resolve_graph(graph, schedule), streams)
+    if bad:
+        raise ValueError("schedule is not race-free on this graph: " + "; ".join(bad[:5]))
+    if ctrl is None:
+        from .parallel import init_ctrl
+
+        ctrl = init_ctrl()
+    if device is None:
+        from .parallel import select_device
+
+        device = select_device()
+    if device < 0:
+        raise RuntimeError("no GPU visible")
+    rt = _tz.HipRuntime(device=device, n_streams=streams,
+                        mode=_tz.ExecMode.Graph if mode == "graph" else _tz.ExecMode.Eager,
+                        graph_unroll=graph_unroll)
+    rt.prepare(schedule)
+    rt.run(warmup)
+    rt.device_sync()
+    ctrl.barrier()
+    t0 = time.perf_counter()
+    rt.run(iters)
+    rt.device_sync()
+    dt = ctrl.allreduce_max([time.perf_counter() - t0])[0]
+    del rt
+    return dt / max(iters, 1) * 1e3

@@ -522,3 +522,23 @@ def test_graph_mode_many_prepares(tz, gpu):
             rt.device_sync()
             assert halo.check_grid() == 0, seq.desc()
         del rt
+
+
+def test_search_then_run_user_graph(tz, gpu):
+    """tz.search on a user graph of busy kernels, then tz.run of the best schedule read back
+    from JSON: the two-stream overlap holds in the replay"""
+    g = tz.Graph()
+    k = [tz.BusyKernelOp(f"k{i}", us) for i, us in enumerate((10, 60, 60, 10), 1)]
+    g.start_then(k[0])
+    g.then(k[0], k[1])
+    g.then(k[0], k[2])
+    g.then(k[1], k[3])
+    g.then(k[2], k[3])
+    g.then_finish(k[3])
+    res = tz.search(g, streams=2, solver="dfs", bench_iters=3, target_secs=0.002,
+                    ctrl=tz.SelfCtrl(), device=0)
+    best = res.sims[res.best()]
+    ms = tz.run(g, best.seq.json(True), streams=2, iters=200, ctrl=tz.SelfCtrl(), device=0)
+    # k2 and k3 overlap: well under the 140 us of running all four back to back
+    assert 0.07 < ms < 0.125, ms
+    assert abs(ms - best.res.pct10 * 1e3) < 0.3 * ms

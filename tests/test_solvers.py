@@ -225,3 +225,17 @@ def test_one_call_search_sim_and_dfs(tz, tmp_path):
     assert abs(r3.sims[r3.best()].res.pct10 - best) < 1e-12
     with pytest.raises(ValueError):
         tz.search(g, solver="bfs", sim=True, ctrl=tz.SelfCtrl())
+
+
+def test_run_refuses_racy_schedules(tz):
+    """tz.run proves a loaded schedule race-free before it touches the GPU"""
+    g = diamond(tz)
+    seq = tz.random_rollout(tz.State(g, tz.Platform(2, symmetric_streams=False)), 3)
+    doc = json.loads(seq.json(True))
+    waits = [k for k, op in enumerate(doc) if op.get("kind") in ("CudaStreamWaitEvent", "CudaEventSync")]
+    if waits:
+        bad = [op for k, op in enumerate(doc) if k != waits[0]]
+        with pytest.raises(ValueError, match="race-free"):
+            tz.run(g, bad, streams=2, ctrl=tz.SelfCtrl(), device=-1)
+    with pytest.raises(RuntimeError, match="no GPU"):
+        tz.run(g, doc, streams=2, ctrl=tz.SelfCtrl(), device=-1)
