@@ -317,6 +317,23 @@ def test_example_torch_overlap(gpu):
     assert bs["gemm"] != bs["h2d"], j
 
 
+def test_example_grad_allreduce_overlap(gpu):
+    """examples/grad_allreduce_overlap.py: backward GEMMs and per-bucket RCCL all-reduces (one
+    rank here), searched by MCTS through the communication ops"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "examples", "grad_allreduce_overlap.py"),
+                        "--iters", "10", "--layers", "3", "--n", "2048"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["ranks"] == 1 and j["candidates"] == 10 and j["best_ms"] > 0
+    assert {"bwd0", "allreduce0"} <= set(j["best_streams"])
+
+
 def test_cpp_library_example_on_gpu(tz, gpu):
     """the C++ library example on the device: its own HIP kernel op, MCTS over 2 streams, the
     winning schedule's results checked by the program (exit 1 on a wrong element)"""
