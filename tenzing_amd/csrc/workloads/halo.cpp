@@ -304,7 +304,8 @@ void HaloExchange::setup(Ctrl *ctrl) {
     // ipc "buffers" mode needs the receive buffer too (the peer packs straight into it); the
     // slack lets a relayed share start on a 128-B boundary behind the direct share
     if (pipe_[i] || (ipc_[i] && !ipcGrid_))
-      recv_[i] = DeviceBuffer((box_elems(opp_[i]) + (relay_ ? 16 : 0)) * sizeof(double));
+      recv_[i] = DeviceBuffer((box_elems(opp_[i]) + (relay_ ? 16 : 0)) * sizeof(double),
+                              /*peerWritten=*/ipc_[i] && !ipcGrid_);
   }
   if (relay_) {
     // the shares my origin relays through me: its face boxes have my boxes' shapes
@@ -316,7 +317,7 @@ void HaloExchange::setup(Ctrl *ctrl) {
         split_box(make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_), f, A, B);
         most = std::max(most, size_t(B.len) * B.n1 * B.n2 * B.n3);
       }
-      relayBuf_[i] = DeviceBuffer(most * sizeof(double));
+      relayBuf_[i] = DeviceBuffer(most * sizeof(double), /*peerWritten=*/true);
     }
   }
   if (useIpc_) {

@@ -403,7 +403,7 @@ void DistSpmv::setup(Ctrl *ctrl) {
   const size_t nl = size_t(local_rows());
   dSend_ = DeviceBuffer(std::max<size_t>(sendIdx_.size() * 4, 16));
   // (at least 64 KB: an IPC-exported buffer of its own rather than a sub-allocation)
-  dXr_ = DeviceBuffer(std::max<size_t>(remoteCols_.size() * 4, 65536));
+  dXr_ = DeviceBuffer(std::max<size_t>(remoteCols_.size() * 4, 65536), /*peerWritten=*/useIpc_);
   dYl_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));
   dYr_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));
   dY_ = DeviceBuffer(std::max<size_t>(nl * 4, 16));

@@ -41,6 +41,12 @@ class DeviceBuffer {
 public:
   DeviceBuffer() = default;
   explicit DeviceBuffer(size_t bytes);
+  /// `peerWritten`: another GPU stores into this buffer over xGMI (IPC receive buffers). It is
+  /// allocated fine-grained, so the reading kernels see those stores through the caches rather
+  /// than lines the local L2 kept from the previous exchange (coarse-grained memory is only
+  /// coherent with other agents at dispatch boundaries whose fences the device-side arrival
+  /// waits bypass). Env TZ_IPC_FINE=0 allocates it coarse-grained like any other buffer.
+  DeviceBuffer(size_t bytes, bool peerWritten);
   ~DeviceBuffer();
   DeviceBuffer(DeviceBuffer &&o) noexcept : p_(o.p_), bytes_(o.bytes_) {
     o.p_ = nullptr;

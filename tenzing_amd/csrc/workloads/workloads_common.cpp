@@ -2,6 +2,7 @@
 
 #include <unistd.h>
 
+#include <cstdlib>
 #include <fstream>
 
 #include "core/util.hpp"
@@ -13,6 +14,16 @@ namespace tz {
 
 DeviceBuffer::DeviceBuffer(size_t bytes) : bytes_(bytes) {
   if (bytes) TZ_HIP(hipMalloc(&p_, bytes));
+}
+
+DeviceBuffer::DeviceBuffer(size_t bytes, bool peerWritten) : bytes_(bytes) {
+  if (!bytes) return;
+  static const bool fine = [] {
+    const char *e = std::getenv("TZ_IPC_FINE");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (peerWritten && fine) TZ_HIP(hipExtMallocWithFlags(&p_, bytes, hipDeviceMallocFinegrained));
+  else TZ_HIP(hipMalloc(&p_, bytes));
 }
 
 DeviceBuffer::~DeviceBuffer() {
