@@ -99,7 +99,8 @@ def cmd_search(a) -> int:
     # or 1 is then a real choice, so the symmetric-stream pruning is off
     plat = tz.Platform(a.streams, symmetric_streams=not distinct)
     bo = tz.BenchOpts(n_iters=a.bench_iters, max_retries=a.max_retries, target_secs=a.target_secs,
-                      device_timer=a.device_timer, race_ratio=a.race_ratio)
+                      device_timer=a.device_timer, race_ratio=a.race_ratio,
+                      settle_ratio=a.settle_ratio)
     rt = None
     if a.replay:
         bench = tz.CsvBenchmarker(a.replay, g)
@@ -341,6 +342,8 @@ def _parser() -> argparse.ArgumentParser:
     s.add_argument("--target-secs", type=float, default=0.01)
     s.add_argument("--race-ratio", type=float, default=0.0,
                    help="stop measuring candidates clearly slower than this times the best so far")
+    s.add_argument("--settle-ratio", type=float, default=0.0,
+                   help="stop measuring a candidate once settle-min measurements agree within this ratio")
     s.add_argument("--device-timer", action="store_true",
                    help="time measurements with device events (GPU time) instead of host wall clock")
     s.add_argument("--mode", default="eager", choices=["eager", "graph"])

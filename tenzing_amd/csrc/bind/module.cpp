@@ -387,7 +387,7 @@ PYBIND11_MODULE(_tz, m) {
 
   // ------------------------------------------------------------------ benchmark
   py::class_<BenchOpts>(m, "BenchOpts")
-      .def(py::init([](int64_t n, int r, double t, bool rs, bool dev, double race) {
+      .def(py::init([](int64_t n, int r, double t, bool rs, bool dev, double race, double settle) {
         BenchOpts o;
         o.n_iters = n;
         o.max_retries = r;
@@ -395,12 +395,15 @@ PYBIND11_MODULE(_tz, m) {
         o.small_sample = rs ? RunsTestSmall::Reject : RunsTestSmall::Accept;
         o.device_timer = dev;
         o.race_ratio = race;
+        o.settle_ratio = settle;
         return o;
       }), py::arg("n_iters") = 1000, py::arg("max_retries") = 10, py::arg("target_secs") = 0.01,
          py::arg("reject_small_samples") = false, py::arg("device_timer") = false,
-         py::arg("race_ratio") = 0.0)
+         py::arg("race_ratio") = 0.0, py::arg("settle_ratio") = 0.0)
       .def_readwrite("race_ratio", &BenchOpts::race_ratio)
       .def_readwrite("race_min", &BenchOpts::race_min)
+      .def_readwrite("settle_ratio", &BenchOpts::settle_ratio)
+      .def_readwrite("settle_min", &BenchOpts::settle_min)
       .def_readwrite("n_iters", &BenchOpts::n_iters)
       .def_readwrite("max_retries", &BenchOpts::max_retries)
       .def_readwrite("target_secs", &BenchOpts::target_secs)
@@ -451,6 +454,7 @@ PYBIND11_MODULE(_tz, m) {
   py::class_<EmpiricalBenchmarker, Benchmarker>(m, "EmpiricalBenchmarker")
       .def(py::init<ExecutorRunner &, Ctrl &>(), py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
       .def_property_readonly("raced", &EmpiricalBenchmarker::raced)
+      .def_property_readonly("settled", &EmpiricalBenchmarker::settled)
       .def("reset_race", &EmpiricalBenchmarker::reset_race)
       .def("benchmark_many", &EmpiricalBenchmarker::benchmark_many, py::arg("seqs"), py::arg("opts"),
            py::arg("seed") = 0, py::call_guard<py::gil_scoped_release>(),

@@ -43,6 +43,7 @@ Json BenchOpts::json() const {
   j["targetSecs"] = target_secs;
   if (device_timer) j["deviceTimer"] = true;
   if (race_ratio > 0) j["raceRatio"] = race_ratio;
+  if (settle_ratio > 0) j["settleRatio"] = settle_ratio;
   return j;
 }
 
@@ -121,11 +122,13 @@ BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts
   std::vector<double> times;
   int retries = 0;
   int64_t hint = 1;
+  bool settled = false;
   for (int left = opts.max_retries; opts.max_retries == 0 || left > 0; --left) {
     Measurement m = measure(1, opts.target_secs, opts.device_timer); // warm-up, size the batch
     hint = m.n;
     times.clear();
     bool raced = false;
+    settled = false;
     for (int64_t i = 0; i < opts.n_iters; ++i) {
       m = measure(hint, opts.target_secs, opts.device_timer);
       hint = std::max(hint, m.n);
@@ -136,11 +139,21 @@ BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts
         raced = true; // clearly slower than the best so far: enough to rank it
         break;
       }
+      if (opts.settle_ratio > 0 && int64_t(times.size()) >= std::max(2, opts.settle_min) &&
+          i + 1 < opts.n_iters) {
+        const auto mm = std::minmax_element(times.begin(), times.end());
+        if (*mm.second - *mm.first <= opts.settle_ratio * *mm.first) {
+          settled = true; // the samples agree: further ones would not change its ranking
+          ++settled_;
+          break;
+        }
+      }
     }
     if (raced) {
       ++raced_;
       break;
     }
+    if (settled) break; // consistent samples: no randomness retry needed
     // per-measurement times are already maxed across ranks inside measure()
     if (compound_test(times, opts.small_sample) && left > 1) {
       ++retries;
@@ -152,7 +165,8 @@ BenchResult EmpiricalBenchmarker::benchmark(const Sequence &seq, const BenchOpts
   BenchResult r = BenchResult::from_times(times);
   r.samples_per_measurement = hint;
   r.retries = retries;
-  if (int64_t(times.size()) == opts.n_iters && (best_ == 0.0 || r.pct10 < best_)) best_ = r.pct10;
+  if ((settled || int64_t(times.size()) == opts.n_iters) && (best_ == 0.0 || r.pct10 < best_))
+    best_ = r.pct10;
   return r;
 }
 

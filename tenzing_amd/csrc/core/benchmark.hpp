@@ -43,6 +43,11 @@ struct BenchOpts {
   // bad). 0 = off. Every rank sees the same max-over-ranks times, so all stop together.
   double race_ratio = 0.0;
   int race_min = 2;
+  // settling: once `settle_min` measurements of a candidate all lie within settle_ratio of
+  // each other ((max - min) / min), stop: more samples would not move its percentiles by more
+  // than that. 0 = off. The decision uses max-over-ranks times, so all ranks stop together.
+  double settle_ratio = 0.0;
+  int settle_min = 4;
   Json json() const;
 };
 
@@ -91,6 +96,8 @@ public:
                                           uint64_t seed = 0);
   /// candidates cut short by racing so far
   int64_t raced() const { return raced_; }
+  /// candidates whose measurements agreed early (settle_ratio) so far
+  int64_t settled() const { return settled_; }
   /// forget the best time racing compares against
   void reset_race() { best_ = 0.0; }
 
@@ -105,6 +112,7 @@ private:
   Ctrl &ctrl_;
   double best_ = 0.0; // best complete pct10 seen (racing); identical on every rank
   int64_t raced_ = 0;
+  int64_t settled_ = 0;
   // batch sizing closes half the gap to the target per run (round-1 rule, env
   // TZ_HALF_GAP_SIZING=1 for A/B runs; must be the same on every rank)
   bool halfGapSizing_ = false;

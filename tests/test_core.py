@@ -353,3 +353,25 @@ def test_node_identity_is_fixed_size_and_stable(tz):
     a, b = tz._tz.node_identity(), tz._tz.node_identity()
     assert a == b and len(a) == 96
     assert a.split(b"|")[0] == socket.gethostname().encode()[:63]
+
+
+def test_settling_stops_consistent_candidates_early(tz):
+    """BenchOpts.settle_ratio: once settle_min measurements agree within the ratio, the
+    candidate is done (no need for all n_iters); off by default"""
+    import time
+
+    g = tz.Graph()
+    c = tz.StaticChoiceOp("pick", [tz.SleepOp("a", 100.0), tz.SleepOp("b", 300.0)])
+    g.start_then(c)
+    g.then_finish(c)
+    for settle, expect in ((0.5, 2), (0.0, 0)):
+        b = tz.EmpiricalBenchmarker(tz.HostExecutor(1), tz.SelfCtrl())
+        o = tz.DfsOpts()
+        o.bench = tz.BenchOpts(n_iters=40, max_retries=1, target_secs=0.002, settle_ratio=settle)
+        t0 = time.time()
+        r = tz.dfs_explore(g, tz.Platform(1), b, tz.SelfCtrl(), o)
+        wall = time.time() - t0
+        assert len(r.sims) == 2 and b.settled == expect
+        if settle:
+            assert wall < 0.5  # 2 candidates x ~4 measurements of ~2 ms (not 40)
+    assert tz.BenchOpts(settle_ratio=0.1).settle_ratio == 0.1
