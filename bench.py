@@ -131,6 +131,9 @@ def main() -> int:
     ap.add_argument("--race-ratio", type=float, default=1.25,
                     help="stop measuring a candidate once race-min measurements are all slower "
                          "than this times the best so far (0 = measure every candidate fully)")
+    ap.add_argument("--settle-ratio", type=float, default=0.0,
+                    help="stop measuring a candidate once its first 4 measurements agree within "
+                         "this ratio (0 = off)")
     ap.add_argument("--strategy", default="FastMin")
     ap.add_argument("--search-mode", default="graph", choices=["eager", "graph"],
                     help="benchmark candidates eagerly or compiled to hipGraphs (default: graph, "
@@ -191,7 +194,7 @@ def main() -> int:
     opts.strategy = args.strategy
     opts.seed = args.seed
     opts.bench = tz.BenchOpts(n_iters=args.bench_iters, max_retries=3, target_secs=args.target_secs,
-                              race_ratio=args.race_ratio)
+                              race_ratio=args.race_ratio, settle_ratio=args.settle_ratio)
     platform = tz.Platform(n_streams=args.streams)
     # candidates that cannot be compiled to a hipGraph are skipped by the search (every rank
     # agrees: preparation is collective); if none could be measured, search eagerly instead
