@@ -149,6 +149,9 @@ def main() -> int:
                     help="re-measure the K best distinct candidates interleaved, compiled as "
                          "hipGraphs, and keep the fastest (0: trust the search's ranking)")
     ap.add_argument("--csv", default="", help="write the search results CSV here (rank 0)")
+    ap.add_argument("--save-best", default="",
+                    help="write the best schedule and this workload's options (rank 0) in the "
+                         "format `python -m tenzing_amd run` and `tz-search --run` take")
     ap.add_argument("--link-probe-iters", type=int, default=20,
                     help="several ranks: after the timing, measure what one xGMI link carries "
                          "per transport (one face to one peer at a time; 0 = skip)")
@@ -383,6 +386,18 @@ def main() -> int:
             "link_probe": probe,
         }
         print(json.dumps(out), flush=True)
+        if args.save_best:
+            doc = {"tenzing_amd": tz.__version__, "ranks": world,
+                   "mode": "graph" if use_graph else "eager", "pct10_ms": ms,
+                   "args": {"workload": "halo", "streams": args.streams, "halo_n": args.n,
+                            "nq": cfg.nq, "ghost": cfg.ghost, "neighbors": args.neighbors,
+                            "order": args.order, "fuse": args.fuse, "transport": args.transport,
+                            "relay": args.relay,
+                            "relay_fracs": ",".join(str(f) for f in cfg.relay_fracs),
+                            "stencil": bool(args.stencil), "rank_grid": args.rank_grid},
+                   "schedule": json.loads(best.json(True))}
+            with open(args.save_best, "w") as f:
+                json.dump(doc, f, indent=1)
     return 0 if bad == 0 else 3
 
 

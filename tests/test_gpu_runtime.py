@@ -559,3 +559,26 @@ def test_search_then_run_user_graph(tz, gpu):
     # k2 and k3 overlap: well under the 140 us of running all four back to back
     assert 0.07 < ms < 0.125, ms
     assert abs(ms - best.res.pct10 * 1e3) < 0.3 * ms
+
+
+def test_bench_save_best_then_run(tz, gpu, tmp_path):
+    """the driver bench's best schedule, saved, runs again through `python -m tenzing_amd run`
+    (the same workload rebuilt from the saved options, verified, checked, timed)"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = tmp_path / "bench_best.json"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--cells", "64",
+                        "--mcts-iters", "6", "--steps", "5", "--warmup", "2", "--rerank", "1",
+                        "--save-best", str(path)], cwd=root, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    doc = json.loads(path.read_text())
+    assert doc["ranks"] == 1 and doc["args"]["halo_n"] == 64 and doc["args"]["neighbors"] == 26
+    r = subprocess.run([sys.executable, "-m", "tenzing_amd", "run", str(path), "--iters", "50",
+                        "--warmup", "5"], cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["correct"] and j["halo_bad_cells"] == 0 and j["ms_per_iter"] > 0
