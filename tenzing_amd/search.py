@@ -19,6 +19,7 @@ from . import _tz
 def search(graph, streams: int = 2, solver: str = "mcts", iters: int = 100,
            strategy: str = "FastMin", mode: str = "graph", graph_unroll: int = 8,
            bench_iters: int = 10, target_secs: float = 0.002, race_ratio: float = 0.0,
+           settle_ratio: float = 0.0,
            max_seqs: int = -1, sim: bool = False, replay: str = "", ctrl=None,
            device: int | None = None, seed: int = 0, time_budget_s: float = 0.0,
            watchdog_s: float = 0.0, symmetric_streams: bool = True):
@@ -40,7 +41,7 @@ def search(graph, streams: int = 2, solver: str = "mcts", iters: int = 100,
         ctrl = init_ctrl()
     plat = _tz.Platform(streams, symmetric_streams=symmetric_streams)
     bo = _tz.BenchOpts(n_iters=bench_iters, max_retries=3, target_secs=target_secs,
-                       race_ratio=race_ratio)
+                       race_ratio=race_ratio, settle_ratio=settle_ratio)
     rt = None
     if replay:
         bench = _tz.CsvBenchmarker(replay, graph)
