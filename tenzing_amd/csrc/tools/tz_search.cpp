@@ -61,7 +61,7 @@ void usage() {
          "  [--relay auto|off|force] [--relay-fracs F1,F2]\n"
          "  [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
-         "  [--checkpoint PATH] [--resume PATH] [--watchdog S] [--race-ratio R]\n"
+         "  [--checkpoint PATH] [--resume PATH] [--watchdog S] [--race-ratio R] [--settle-ratio R]\n"
          "  [--save-best PATH]      write the best schedule + workload options (JSON)\n"
          "  [--run PATH [--run-iters N] [--run-warmup N]]\n"
          "                          run a saved schedule (this CLI's or python -m tenzing_amd's)\n"
@@ -272,6 +272,7 @@ int main(int argc, char **argv) {
     bo.n_iters = int64_t(a.num("bench-iters", 50));
     bo.target_secs = a.num("target-secs", 0.01);
     bo.race_ratio = a.num("race-ratio", 0.0);
+    bo.settle_ratio = a.num("settle-ratio", 0.0);
 
     if (a.flag("run")) {
       // a saved schedule: rebuilt by op name, proven race-free on the graph it executes,
