@@ -47,7 +47,8 @@ def _start_deadline(seconds: float) -> None:
 def link_probe(tz, halo, ctrl, iters, rccl=False):
     """GB/s of ONE transfer over one xGMI link with each available transport (the +z face to
     the +z neighbour, every rank at once, one transfer at a time), of both z faces at once
-    (`pair_GBps`: kernel puts, copy engines, or one of each), and the time the exchange's
+    (`pair_GBps`: kernel puts, copy engines, or one of each), kernel puts over the x and y face
+    links as well (`put_GBps_by_axis`, where those faces are remote), and the time the exchange's
     busiest link (the peer receiving the most bytes) would take at the best of those rates. An
     exchange runs several transfers per link at once (several streams, copy engines), so it can
     beat that time; on loopback ranks (one GPU) the rates say nothing about xGMI."""
@@ -79,13 +80,25 @@ def link_probe(tz, halo, ctrl, iters, rccl=False):
                 pair[how] = None
                 if ctrl.rank == 0:
                     print(f"bench.py: link probe pair_{how}: {e}", file=sys.stderr)
+    # the other axes' face links too (kernel puts): are the links of one node alike?
+    by_axis = {"z": rates.get("put")}
+    for name, d in (("x", (1, 0, 0)), ("y", (0, 1, 0))):
+        k = dirs.index(d)
+        if halo.is_direct(k):
+            continue
+        try:
+            by_axis[name] = 8.0 * halo.box_elems(k) / halo.link_probe(k, "put", iters, ctrl) / 1e9
+        except Exception as e:  # noqa: BLE001  (collective: every rank skips together)
+            by_axis[name] = None
+            if ctrl.rank == 0:
+                print(f"bench.py: link probe put {name}: {e}", file=sys.stderr)
     per_peer = {}
     for k in range(halo.ndirs()):
         if not halo.is_direct(k):
             per_peer[halo.neighbor(k)] = per_peer.get(halo.neighbor(k), 0.0) + 8.0 * halo.box_elems(k)
     busiest = max(per_peer.values()) if per_peer else 0.0
     best = max([r for r in list(rates.values()) + list(pair.values()) if r], default=None)
-    return {"face_MB": face / 1e6, "GBps": rates, "pair_GBps": pair,
+    return {"face_MB": face / 1e6, "GBps": rates, "pair_GBps": pair, "put_GBps_by_axis": by_axis,
             "busiest_link_MB": busiest / 1e6,
             "busiest_link_at_probe_rate_ms": (busiest / (best * 1e9) * 1e3) if best else None}
 

@@ -135,6 +135,8 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     # both z faces at once (2 ranks: one peer): kernel puts always, copy engines and the
     # kernel + copy-engine mix in buffers mode
     assert p["pair_GBps"]["put"] > 0
+    # 2 ranks: 1x1x2, only the z faces are remote
+    assert set(p["put_GBps_by_axis"]) == {"z"}
     assert (p["pair_GBps"]["sdma"] is not None) == (p["pair_GBps"]["mixed"] is not None) == (mode == "buffers")
     assert p["busiest_link_MB"] > p["face_MB"] > 0 and p["busiest_link_at_probe_rate_ms"] > 0
 
