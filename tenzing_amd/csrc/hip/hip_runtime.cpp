@@ -113,11 +113,11 @@ HipRuntime::~HipRuntime() {
   stop_ = true;
   if (watchdog_.joinable()) watchdog_.join();
   destroy_graph();
-  for (void *e : events_) hipEventDestroy(E(e));
-  for (void *e : internal_) hipEventDestroy(E(e));
+  for (void *e : events_) (void)hipEventDestroy(E(e));
+  for (void *e : internal_) (void)hipEventDestroy(E(e));
   for (void *e : timerEv_)
-    if (e) hipEventDestroy(E(e));
-  for (void *s : streams_) hipStreamDestroy(S(s));
+    if (e) (void)hipEventDestroy(E(e));
+  for (void *s : streams_) (void)hipStreamDestroy(S(s));
 }
 
 std::string HipRuntime::device_name() const {
@@ -201,10 +201,10 @@ void HipRuntime::device_sync() { TZ_HIP(hipDeviceSynchronize()); }
 
 void HipRuntime::destroy_exec(void *exec) {
   if (!exec) return;
-  hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec));
+  (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec));
   auto it = graphOf_.find(exec);
   if (it != graphOf_.end()) {
-    hipGraphDestroy(static_cast<hipGraph_t>(it->second));
+    (void)hipGraphDestroy(static_cast<hipGraph_t>(it->second));
     graphOf_.erase(it);
   }
 }
@@ -304,7 +304,7 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
           TZ_HIP(hipStreamGetCaptureInfo_v2(st, &cs, nullptr, nullptr, &d, &nd));
           tails.assign(d, d + nd);
         } catch (...) {
-          hipStreamEndCapture(st, &captured);
+          (void)hipStreamEndCapture(st, &captured);
           throw;
         }
         TZ_HIP(hipStreamEndCapture(st, &captured));
@@ -338,7 +338,7 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
     }
     return exec;
   } catch (...) {
-    if (graph) hipGraphDestroy(graph);
+    if (graph) (void)hipGraphDestroy(graph);
     throw;
   }
 }
@@ -474,7 +474,7 @@ std::vector<HipRuntime::Span> HipRuntime::trace(const Sequence &seq, int iterati
   } catch (const std::exception &e) {
     err = e.what();
   }
-  for (hipEvent_t e : evs) hipEventDestroy(e);
+  for (hipEvent_t e : evs) (void)hipEventDestroy(e);
   seq_ = keep;
   internalUsed_ = 0;
   if (!err.empty()) throw Error(err);
