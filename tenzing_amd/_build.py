@@ -116,13 +116,17 @@ def _ninja_file(debug: bool) -> str:
     # plus a user-side example that defines its own kernel op against it
     lib = BUILD / "libtenzing_amd.a"
     lines.append(f"build {lib}: ar {allobjs}")
-    ex_src = ROOT / "examples" / "cpp" / "custom_kernel_op.hip"
-    ex_obj = f"{BUILD}/examples/custom_kernel_op.o"
-    ex_exe = PKG / "bin" / "tz-example-custom-op"
-    lines.append(f"build {ex_obj}: hipdev {ex_src}")
-    lines.append(f"build {ex_exe}: link_exe {ex_obj} {lib}")
+    # and a multi-rank program with RCCL comm ops in its graph
+    exes = []
+    for src, exe_name in (("custom_kernel_op", "tz-example-custom-op"),
+                          ("ring_overlap", "tz-example-ring")):
+        ex_obj = f"{BUILD}/examples/{src}.o"
+        ex_exe = PKG / "bin" / exe_name
+        lines.append(f"build {ex_obj}: hipdev {ROOT / 'examples' / 'cpp' / (src + '.hip')}")
+        lines.append(f"build {ex_exe}: link_exe {ex_obj} {lib}")
+        exes.append(str(ex_exe))
     lines.append(f"default {ext_path()} {PKG / 'bin' / 'tz-search'} {PKG / 'bin' / 'tz-unit'} "
-                 f"{lib} {ex_exe}")
+                 f"{lib} {' '.join(exes)}")
     return "\n".join(lines) + "\n"
 
 

@@ -349,6 +349,25 @@ def test_cpp_library_example_on_gpu(tz, gpu):
     assert j["best_us"] < 0.8 * j["worst_us"], j
 
 
+def test_cpp_ring_example_on_gpu(tz, gpu):
+    """the C++ multi-rank example (examples/cpp/ring_overlap.hip) on one rank: RCCL send/recv and
+    all-reduce ops in a user graph, searched as hipGraph candidates; the program checks the
+    winning schedule's results (exit 1 on a wrong element) and the search overlaps the interior
+    kernel with the communication chain"""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tenzing_amd", "bin", "tz-example-ring")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["ranks"] == 1 and j["bad"] == 0 and j["candidates"] == 20
+    assert j["interior_stream"] != j["xfer_stream"], j
+    assert j["best_us"] < j["worst_us"], j
+
+
 @pytest.mark.parametrize("order", ["qxyz", "xyzq"])
 def test_halo_stencil_mode_correct(tz, gpu, order):
     """exchange + 7-point stencil: for random schedules of both alternatives (interior beside
