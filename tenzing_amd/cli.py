@@ -127,6 +127,7 @@ def cmd_search(a) -> int:
         o = tz.MctsOpts()
         o.n_iters = a.iters
         o.time_budget_s = a.time_budget
+        o.max_tree_nodes = a.max_tree_nodes
         o.strategy = a.strategy
         o.seed = a.seed
         o.expand_rollout = not a.no_expand_rollout
@@ -335,6 +336,8 @@ def _parser() -> argparse.ArgumentParser:
     s.add_argument("--strategy", default="FastMin")
     s.add_argument("--iters", type=int, default=300)
     s.add_argument("--time-budget", type=float, default=0.0)
+    s.add_argument("--max-tree-nodes", type=int, default=0,
+                   help="MCTS: stop once the tree holds this many nodes (0 = unlimited)")
     s.add_argument("--max-seqs", type=int, default=15000)
     s.add_argument("--streams", type=int, default=2)
     s.add_argument("--bench-iters", type=int, default=50)

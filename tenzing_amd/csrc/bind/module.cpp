@@ -506,6 +506,7 @@ PYBIND11_MODULE(_tz, m) {
       .def(py::init<>())
       .def_readwrite("n_iters", &MctsOpts::n_iters)
       .def_readwrite("time_budget_s", &MctsOpts::time_budget_s)
+      .def_readwrite("max_tree_nodes", &MctsOpts::max_tree_nodes)
       .def_readwrite("expand_rollout", &MctsOpts::expand_rollout)
       .def_readwrite("remove_redundant_syncs", &MctsOpts::remove_redundant_syncs)
       .def_readwrite("reuse_measurements", &MctsOpts::reuse_measurements)

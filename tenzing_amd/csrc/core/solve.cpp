@@ -293,6 +293,7 @@ Json MctsOpts::json() const {
   Json j, o;
   o["nIters"] = n_iters;
   o["timeBudgetS"] = time_budget_s;
+  if (max_tree_nodes > 0) o["maxTreeNodes"] = max_tree_nodes;
   o["expandRollout"] = expand_rollout;
   o["removeRedundantSyncs"] = remove_redundant_syncs;
   o["reuseMeasurements"] = reuse_measurements;
@@ -311,12 +312,14 @@ struct Tree {
   std::unique_ptr<Strategy> strat;
   std::mt19937_64 rng;
   double c;
+  size_t nodes = 1; // nodes created so far (the root included)
 
   void ensure_children(MctsNode &node, const State &st) {
     if (node.expanded) return;
     node.expanded = true;
     node.terminal = st.complete();
     for (auto &d : st.get_decisions()) {
+      ++nodes;
       auto ch = std::make_unique<MctsNode>();
       ch->parent = &node;
       ch->decision = d;
@@ -531,6 +534,10 @@ SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &ben
       } else if (opts.time_budget_s > 0 && wtime() - t0 > opts.time_budget_s) {
         stop = 3;
         result.stop_reason = "time_budget";
+      } else if (opts.max_tree_nodes > 0 && tree.nodes >= size_t(opts.max_tree_nodes)) {
+        // reference Stop::Reason::large_tree (mcts.hpp:131): bounds the host memory of the tree
+        stop = 5;
+        result.stop_reason = "large_tree";
       }
       if (opts.trap_signals && signal_pending()) {
         stop = 4;

@@ -88,6 +88,7 @@ std::vector<std::string> strategy_names();
 struct MctsOpts {
   int64_t n_iters = 300;        // 0 = until the tree is fully visited / budget exhausted
   double time_budget_s = 0;     // 0 = unlimited
+  int64_t max_tree_nodes = 0;   // stop once the tree holds this many nodes (0 = unlimited)
   bool expand_rollout = true;   // keep rollout paths in the tree (reference Opts::expandRollout)
   bool remove_redundant_syncs = true;
   bool reuse_measurements = true; // benchmark each equivalent final schedule once

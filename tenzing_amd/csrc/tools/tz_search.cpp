@@ -51,7 +51,7 @@ int env_int(const char *a, const char *b, int d) {
 void usage() {
   std::cerr
       << "usage: tz-search [--workload halo|spmv|halo+spmv|diamond] [--solver mcts|dfs]\n"
-         "  [--strategy NAME] [--iters N] [--time-budget S] [--streams N] [--bench-iters N]\n"
+         "  [--strategy NAME] [--iters N] [--time-budget S] [--max-tree-nodes N] [--streams N] [--bench-iters N]\n"
          "  [--target-secs S] [--mode eager|graph] [--sim] [--seed N] [--no-expand-rollout]\n"
          "  [--halo-n N] [--nq N] [--ghost N] [--neighbors 6|26] [--order xyzq|qxyz]\n"
          "  [--fuse none|pack|all|groups|choice] [--graph-unroll K]\n"
@@ -329,6 +329,7 @@ int main(int argc, char **argv) {
       MctsOpts o;
       o.n_iters = int64_t(a.num("iters", 300));
       o.time_budget_s = a.num("time-budget", 0);
+      o.max_tree_nodes = int64_t(a.num("max-tree-nodes", 0));
       o.strategy = a.get("strategy", "FastMin");
       o.seed = uint64_t(a.num("seed", 0));
       o.expand_rollout = !a.flag("no-expand-rollout");

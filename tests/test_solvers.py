@@ -161,6 +161,24 @@ def test_time_budget_stop(tz):
     assert r.stop_reason in ("time_budget", "full_tree")
 
 
+def test_large_tree_stop(tz):
+    """reference Stop::Reason::large_tree (mcts.hpp:131): the search ends once the tree holds
+    max_tree_nodes nodes, after the iteration that crossed the bound"""
+    g = diamond(tz)
+    o = tz.MctsOpts()
+    o.n_iters = 0
+    o.max_tree_nodes = 40
+    o.bench = tz.BenchOpts(n_iters=2)
+    r = tz.mcts_explore(g, tz.Platform(4), tz.SimBenchmarker(4), tz.SelfCtrl(), o)
+    assert r.stop_reason == "large_tree"
+    assert 40 <= r.tree_size
+    assert len(r.sims) >= 1
+    o.max_tree_nodes = 0
+    o.n_iters = 3
+    assert tz.mcts_explore(g, tz.Platform(4), tz.SimBenchmarker(4), tz.SelfCtrl(), o).stop_reason \
+        in ("iterations", "full_tree")
+
+
 def test_failed_candidates_are_skipped(tz):
     """a candidate whose benchmark fails (e.g. cannot be compiled to a hipGraph) is pruned from
     the tree instead of ending the search; DFS skips it too"""
