@@ -25,7 +25,7 @@ BUILD = ROOT / "build"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("TZ_OFFLOAD_ARCH", "gfx950")
 
-CORE = ["json", "numeric", "ops", "graph", "state", "serdes", "ctrl", "benchmark", "solve"]
+CORE = ["json", "numeric", "ops", "graph", "state", "serdes", "ctrl", "ctrl_mpi", "benchmark", "solve"]
 HIP_HOST = ["hip_runtime", "rccl_comm", "comm_ops", "rocsparse_spmv"]
 WORKLOADS = ["halo", "halo_ipc", "halo_graph", "halo_stencil", "spmv", "workloads_common"]
 KERNELS = ["halo_kernels", "spmv_kernels", "stencil_kernels"]
@@ -61,7 +61,7 @@ def _ninja_file(debug: bool) -> str:
         f"hipflags = {common} {hipdefs}",
         f"devflags = {common} --offload-arch={ARCH} -munsafe-fp-atomics -ffp-contract=fast",
         f"pyflags = -I{pybind11.get_include()} -I{py_inc}",
-        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lrocsparse -lrocprofiler-sdk-roctx -lpthread",
+        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lrocsparse -lrocprofiler-sdk-roctx -lpthread -ldl",
         "rule cxx",
         "  command = $cxx $cflags $extra -MMD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",
@@ -154,7 +154,7 @@ def _sanitizer_ninja(kind: str) -> str:
         "  deps = gcc",
         "  description = CXX[" + kind + "] $out",
         "rule link",
-        f"  command = $cxx {flags} -o $out $in -lpthread",
+        f"  command = $cxx {flags} -o $out $in -lpthread -ldl",
         "  description = LINK $out",
     ]
     objs = []

@@ -500,6 +500,11 @@ PYBIND11_MODULE(_tz, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("rendezvous_file", &TcpCtrl::rendezvous_file, py::arg("path"), py::arg("host") = "127.0.0.1",
            py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>());
+  py::class_<MpiCtrl, Ctrl, std::shared_ptr<MpiCtrl>>(m, "MpiCtrl")
+      .def(py::init<const std::string &>(), py::arg("lib") = "", py::call_guard<py::gil_scoped_release>())
+      .def_static("launched", &MpiCtrl::launched)
+      .def_static("launcher_local_rank", &MpiCtrl::launcher_local_rank)
+      .def_property_readonly("library", &MpiCtrl::library);
 
   // ------------------------------------------------------------------ solvers
   py::class_<MctsOpts>(m, "MctsOpts")

@@ -3,10 +3,11 @@
 //
 // Parity: the reference uses MPI for these (MPI_Bcast of the schedule JSON, src/sequence.cpp:
 // 88-125; MPI_Barrier/MPI_Allreduce(MAX) in src/benchmarker.cpp:45-145; Stop-flag MPI_Bcast in
-// tenzing-mcts mcts.hpp:149-150 and tenzing-dfs dfs.hpp:67-68). There is no MPI on the MI355X
-// image and the GPU data plane is RCCL, so the control plane is a native TCP star (rank 0 hub,
-// TCP_NODELAY, length-prefixed frames) bootstrapped from the launcher's rendezvous. It is not
-// on the device path: candidate schedules move their payloads over RCCL/xGMI.
+// tenzing-mcts mcts.hpp:149-150 and tenzing-dfs dfs.hpp:67-68). The GPU data plane is RCCL, so
+// the default control plane is a native TCP star (rank 0 hub, TCP_NODELAY, length-prefixed
+// frames) bootstrapped from the launcher's rendezvous (torchrun). Programs started by an MPI
+// launcher, as the reference's are, can use MpiCtrl instead (host MPI, opened at run time). Neither
+// is on the device path: candidate schedules move their payloads over RCCL/xGMI.
 #pragma once
 
 #include <cstdint>
@@ -73,6 +74,33 @@ private:
   int rank_, size_;
   int listenFd_ = -1;
   std::vector<int> peers_; // rank 0: fd per rank (index 0 unused); others: peers_[0] = root
+};
+
+/// Control plane over MPI_COMM_WORLD for ranks started by mpirun / mpiexec / srun (the
+/// reference's launch model). libmpi (MPICH ABI) is opened at run time: $TZ_MPI_LIB, the
+/// loader's libmpi.so.12 / libmpi.so, then /opt/conda/lib. MPI_Init_thread runs unless MPI is
+/// already initialized, and MPI_Finalize then runs at process exit.
+class MpiCtrl : public Ctrl {
+public:
+  explicit MpiCtrl(const std::string &lib = "");
+  /// this process was started by an MPI launcher (PMI / PMIx / MVAPICH environment)
+  static bool launched();
+  /// the node-local rank the launcher exported, -1 if none
+  static int launcher_local_rank();
+  /// path of the MPI library in use
+  std::string library() const;
+
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  void barrier() override;
+  void bcast(std::string &data, int root) override;
+  void allreduce_max(double *v, size_t n) override;
+  void allreduce_sum(double *v, size_t n) override;
+  std::vector<std::string> allgather(const std::string &mine) override;
+  using Ctrl::allreduce_max;
+
+private:
+  int rank_ = 0, size_ = 1;
 };
 
 } // namespace tz

@@ -1,0 +1,188 @@
+// MPI control plane: the reference's own launch model (mpirun / srun, one rank per GPU, the
+// control collectives over MPI_COMM_WORLD: src/sequence.cpp:88-125, src/benchmarker.cpp:45-145,
+// tenzing-mcts mcts.hpp:149-150).
+//
+// libmpi is opened at run time, so the build needs no MPI and a process that never asks for the
+// MPI backend never loads it. The ABI is MPICH's (MPICH, Cray MPICH, MVAPICH, Intel MPI: handles
+// are ints, the constants below are fixed by that ABI); this image ships MPICH 3.3 under
+// /opt/conda. MPI is host-only here: it carries the search's small control messages, never
+// device buffers (the data plane is RCCL / IPC puts).
+#include "ctrl.hpp"
+#include "util.hpp"
+
+#include <dlfcn.h>
+
+#include <cstdlib>
+#include <mutex>
+
+namespace tz {
+
+namespace {
+
+// MPICH ABI (mpi.h of MPICH 3.x/4.x)
+using MPI_Comm = int;
+using MPI_Datatype = int;
+using MPI_Op = int;
+constexpr MPI_Comm kCommWorld = 0x44000000;
+constexpr MPI_Datatype kByte = 0x4c00010d;
+constexpr MPI_Datatype kInt = 0x4c000405;
+constexpr MPI_Datatype kDouble = 0x4c00080b;
+constexpr MPI_Op kMax = 0x58000001;
+constexpr MPI_Op kSum = 0x58000003;
+constexpr int kThreadFunneled = 1;
+void *const kInPlace = reinterpret_cast<void *>(-1);
+
+struct Api {
+  void *lib = nullptr;
+  std::string path;
+  int (*Initialized)(int *) = nullptr;
+  int (*Finalized)(int *) = nullptr;
+  int (*Init_thread)(int *, char ***, int, int *) = nullptr;
+  int (*Finalize)() = nullptr;
+  int (*Comm_rank)(MPI_Comm, int *) = nullptr;
+  int (*Comm_size)(MPI_Comm, int *) = nullptr;
+  int (*Barrier)(MPI_Comm) = nullptr;
+  int (*Bcast)(void *, int, MPI_Datatype, int, MPI_Comm) = nullptr;
+  int (*Allreduce)(const void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm) = nullptr;
+  int (*Allgather)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, MPI_Comm) = nullptr;
+  int (*Allgatherv)(const void *, int, MPI_Datatype, void *, const int *, const int *, MPI_Datatype,
+                    MPI_Comm) = nullptr;
+  bool initializedHere = false;
+};
+
+template <class F> void sym(Api &a, F &f, const char *name) {
+  f = reinterpret_cast<F>(dlsym(a.lib, name));
+  TZ_CHECK(f, "MPI library " << a.path << " has no " << name);
+}
+
+std::mutex g_mu;
+Api *g_api = nullptr; // process-wide: MPI is initialized at most once per process
+
+void finalize_at_exit() {
+  // an MPI launcher counts a rank that exits without MPI_Finalize as failed
+  if (g_api && g_api->initializedHere) {
+    int fin = 0;
+    g_api->Finalized(&fin);
+    if (!fin) g_api->Finalize();
+  }
+}
+
+Api &api(const std::string &want) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_api) return *g_api;
+  auto *a = new Api();
+  std::vector<std::string> tries;
+  if (!want.empty()) tries.push_back(want);
+  if (const char *e = std::getenv("TZ_MPI_LIB")) tries.push_back(e);
+  for (const char *p : {"libmpi.so.12", "libmpi.so", "/opt/conda/lib/libmpi.so.12", "/opt/conda/lib/libmpi.so"})
+    tries.push_back(p);
+  std::string errs;
+  for (const auto &p : tries) {
+    // global: MPICH may open its own plugins that resolve against it
+    a->lib = dlopen(p.c_str(), RTLD_NOW | RTLD_GLOBAL);
+    if (a->lib) {
+      a->path = p;
+      break;
+    }
+    const char *e = dlerror();
+    errs += "\n  " + p + ": " + (e ? e : "not found");
+  }
+  if (!a->lib) {
+    delete a;
+    TZ_THROW("MPI control plane: no MPI library could be opened (set TZ_MPI_LIB):" << errs);
+  }
+  sym(*a, a->Initialized, "MPI_Initialized");
+  sym(*a, a->Finalized, "MPI_Finalized");
+  sym(*a, a->Init_thread, "MPI_Init_thread");
+  sym(*a, a->Finalize, "MPI_Finalize");
+  sym(*a, a->Comm_rank, "MPI_Comm_rank");
+  sym(*a, a->Comm_size, "MPI_Comm_size");
+  sym(*a, a->Barrier, "MPI_Barrier");
+  sym(*a, a->Bcast, "MPI_Bcast");
+  sym(*a, a->Allreduce, "MPI_Allreduce");
+  sym(*a, a->Allgather, "MPI_Allgather");
+  sym(*a, a->Allgatherv, "MPI_Allgatherv");
+  int init = 0, fin = 0;
+  a->Initialized(&init);
+  a->Finalized(&fin);
+  TZ_CHECK(!fin, "MPI control plane: MPI was already finalized in this process");
+  if (!init) {
+    // the search drives MPI from one thread; other threads (watchdog) never call it
+    int provided = 0;
+    TZ_CHECK(a->Init_thread(nullptr, nullptr, kThreadFunneled, &provided) == 0, "MPI_Init_thread failed");
+    a->initializedHere = true;
+    std::atexit(finalize_at_exit);
+  }
+  g_api = a;
+  return *a;
+}
+
+#define TZ_MPI(call)                                                                               \
+  do {                                                                                             \
+    const int rc_ = (call);                                                                        \
+    TZ_CHECK(rc_ == 0, #call << " failed (MPI error " << rc_ << ")");                              \
+  } while (0)
+
+} // namespace
+
+bool MpiCtrl::launched() {
+  // MPICH hydra / PMI-1 and PMI-2, PMIx (Slurm, OpenPMIx), MVAPICH, Slurm srun
+  for (const char *v : {"PMI_SIZE", "PMI_RANK", "PMIX_RANK", "MV2_COMM_WORLD_SIZE", "MPI_LOCALNRANKS"})
+    if (std::getenv(v)) return true;
+  return false;
+}
+
+int MpiCtrl::launcher_local_rank() {
+  for (const char *v : {"MPI_LOCALRANKID", "MV2_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID",
+                        "OMPI_COMM_WORLD_LOCAL_RANK", "PALS_LOCAL_RANKID"})
+    if (const char *e = std::getenv(v)) return std::atoi(e);
+  return -1;
+}
+
+MpiCtrl::MpiCtrl(const std::string &lib) {
+  Api &a = api(lib);
+  TZ_MPI(a.Comm_rank(kCommWorld, &rank_));
+  TZ_MPI(a.Comm_size(kCommWorld, &size_));
+}
+
+std::string MpiCtrl::library() const { return g_api ? g_api->path : ""; }
+
+void MpiCtrl::barrier() { TZ_MPI(g_api->Barrier(kCommWorld)); }
+
+void MpiCtrl::bcast(std::string &data, int root) {
+  long long n = rank_ == root ? (long long)data.size() : 0;
+  TZ_MPI(g_api->Bcast(&n, int(sizeof(n)), kByte, root, kCommWorld));
+  TZ_CHECK(n >= 0 && n < (1ll << 31), "MPI bcast: message of " << n << " bytes");
+  if (rank_ != root) data.assign(size_t(n), '\0');
+  if (n) TZ_MPI(g_api->Bcast(&data[0], int(n), kByte, root, kCommWorld));
+}
+
+void MpiCtrl::allreduce_max(double *v, size_t n) {
+  if (n) TZ_MPI(g_api->Allreduce(kInPlace, v, int(n), kDouble, kMax, kCommWorld));
+}
+
+void MpiCtrl::allreduce_sum(double *v, size_t n) {
+  if (n) TZ_MPI(g_api->Allreduce(kInPlace, v, int(n), kDouble, kSum, kCommWorld));
+}
+
+std::vector<std::string> MpiCtrl::allgather(const std::string &mine) {
+  TZ_CHECK(mine.size() < (size_t(1) << 31), "MPI allgather: message too large");
+  int len = int(mine.size());
+  std::vector<int> lens(size_t(size_), 0);
+  std::vector<int> offs(size_t(size_), 0);
+  TZ_MPI(g_api->Allgather(&len, 1, kInt, lens.data(), 1, kInt, kCommWorld));
+  long long total = 0;
+  for (int r = 0; r < size_; ++r) {
+    offs[size_t(r)] = int(total);
+    total += lens[size_t(r)];
+  }
+  TZ_CHECK(total < (1ll << 31), "MPI allgather: " << total << " bytes in total");
+  std::string all(size_t(total), '\0');
+  TZ_MPI(g_api->Allgatherv(mine.data(), len, kByte, total ? &all[0] : nullptr, lens.data(), offs.data(),
+                           kByte, kCommWorld));
+  std::vector<std::string> out(static_cast<size_t>(size_));
+  for (int r = 0; r < size_; ++r) out[size_t(r)] = all.substr(size_t(offs[size_t(r)]), size_t(lens[size_t(r)]));
+  return out;
+}
+
+} // namespace tz

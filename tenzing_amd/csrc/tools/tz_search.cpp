@@ -4,9 +4,11 @@
 //
 //   tz-search --workload halo --solver mcts --strategy FastMin --iters 100 --streams 4
 //   torchrun --nproc-per-node 8 ... tz-search (one process per GPU; RANK/WORLD_SIZE/LOCAL_RANK)
+//   mpirun -n 8 tz-search ...                 (the reference's launch; control plane over MPI)
 //
-// Multi-rank control-plane rendezvous goes through a file (--rdzv-file, default under /tmp keyed
-// by MASTER_PORT); the data plane is RCCL.
+// Under torchrun the control-plane rendezvous goes through a file (--rdzv-file, default under
+// /tmp keyed by MASTER_PORT); under an MPI launcher it is MPI_COMM_WORLD (--ctrl mpi, picked
+// automatically). The data plane is RCCL / IPC puts either way.
 #include "core/solve.hpp"
 #include "hip/hip_runtime.hpp"
 #include "workloads/workloads.hpp"
@@ -59,7 +61,7 @@ void usage() {
          "  [--spmv-form choice|split|accum] [--spmv-transport auto|rccl|ipc]\n"
          "  [--spmv-library adaptive|lrb|rowsplit|''] [--cu-partition] [--stencil] [--max-seqs N]\n"
          "  [--relay auto|off|force] [--relay-fracs F1,F2]\n"
-         "  [--rdzv-file PATH]\n"
+         "  [--ctrl auto|tcp|mpi|self] [--mpi-lib PATH] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--watchdog S] [--race-ratio R] [--settle-ratio R]\n"
          "  [--save-best PATH]      write the best schedule + workload options (JSON)\n"
@@ -134,21 +136,39 @@ int main(int argc, char **argv) {
       if (!a.flag("mode") && saved.contains("mode")) a.kv["mode"] = saved.at("mode").as_string();
       TZ_CHECK(!a.flag("sim"), "--run needs a GPU");
     }
-    const int rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", 0);
-    const int size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1);
-    const int local = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", rank);
+    // control plane: --ctrl mpi for ranks started by mpirun / srun (the reference's launch
+    // model), tcp for torchrun-style RANK / WORLD_SIZE; auto picks mpi when an MPI launcher
+    // started this process and no WORLD_SIZE is set
+    std::string ctrlKind = a.get("ctrl", "auto");
+    TZ_CHECK(ctrlKind == "auto" || ctrlKind == "tcp" || ctrlKind == "mpi" || ctrlKind == "self",
+             "--ctrl must be auto, tcp, mpi or self");
+    if (ctrlKind == "auto")
+      ctrlKind = !std::getenv("WORLD_SIZE") && MpiCtrl::launched() ? "mpi" : "tcp";
+    std::shared_ptr<Ctrl> ctrl;
+    int rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", 0);
+    int size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1);
+    int local = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", rank);
+    if (ctrlKind == "mpi") {
+      auto m = std::make_shared<MpiCtrl>(a.get("mpi-lib", ""));
+      rank = m->rank();
+      size = m->size();
+      local = MpiCtrl::launcher_local_rank() >= 0 ? MpiCtrl::launcher_local_rank() : rank;
+      ctrl = m;
+    } else if (ctrlKind == "self") {
+      rank = 0;
+      size = 1;
+    }
     log_rank() = rank;
     const bool sim = a.flag("sim");
     const int streams = int(a.num("streams", 2));
     const std::string workload = a.get("workload", "halo");
 
-    std::shared_ptr<Ctrl> ctrl;
-    if (size > 1) {
+    if (!ctrl && size > 1) {
       auto t = std::make_shared<TcpCtrl>(rank, size);
       const std::string port = std::getenv("MASTER_PORT") ? std::getenv("MASTER_PORT") : "default";
       t->rendezvous_file(a.get("rdzv-file", "/tmp/tz_rdzv_" + port), a.get("master-addr", "127.0.0.1"));
       ctrl = t;
-    } else {
+    } else if (!ctrl) {
       ctrl = std::make_shared<SelfCtrl>();
     }
     if (rank == 0) std::cerr << reproduce_json(a.raw).dump() << "\n";

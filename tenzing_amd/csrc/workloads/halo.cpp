@@ -192,10 +192,11 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
 }
 
 HaloExchange::~HaloExchange() {
-  for (void *e : copyEvents_) hipEventDestroy(static_cast<hipEvent_t>(e));
-  for (void *s : copyStreams_) hipStreamDestroy(static_cast<hipStream_t>(s));
-  for (void *p : opened_) hipIpcCloseMemHandle(p);
-  if (flags_) hipFree(flags_);
+  // teardown: nothing useful to do with an error here
+  for (void *e : copyEvents_) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
+  for (void *s : copyStreams_) (void)hipStreamDestroy(static_cast<hipStream_t>(s));
+  for (void *p : opened_) (void)hipIpcCloseMemHandle(p);
+  if (flags_) (void)hipFree(flags_);
 }
 
 int HaloExchange::coord_to_rank(int x, int y, int z) const {

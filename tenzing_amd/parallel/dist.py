@@ -7,6 +7,10 @@ an ephemeral port and broadcasts the port; every rank then joins the native star
 (``tenzing_amd._tz.TcpCtrl``). RCCL communicators for the data plane are created later by the
 workloads, with their unique ids broadcast over that control plane.
 
+Processes started by an MPI launcher instead (``mpirun -n 8 python bench.py``, the reference's
+launch model) use ``MpiCtrl``: the control collectives then run over MPI_COMM_WORLD (host MPI,
+opened at run time), and the node-local rank the launcher exports picks the GPU.
+
 Reference: MPI_Init + MPI_COMM_WORLD everywhere (tenzing-mcts/examples/halo_min_time.cu:11,
 spmv_run_strategy.cuh:81-90 rank -> device = rank % ndev).
 """
@@ -27,7 +31,17 @@ class DistEnv:
     master_port: int = 29500
 
 
+def _mpi_launched() -> bool:
+    return "WORLD_SIZE" not in os.environ and _tz.MpiCtrl.launched()
+
+
 def env() -> DistEnv:
+    if _mpi_launched():
+        e = os.environ
+        rank = int(e.get("PMI_RANK", e.get("PMIX_RANK", e.get("MV2_COMM_WORLD_RANK", 0))))
+        world = int(e.get("PMI_SIZE", e.get("MV2_COMM_WORLD_SIZE", 1)))
+        local = _tz.MpiCtrl.launcher_local_rank()
+        return DistEnv(rank, world, local if local >= 0 else rank)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", rank))
@@ -36,8 +50,17 @@ def env() -> DistEnv:
 
 
 def init_ctrl(rank: int | None = None, world: int | None = None, master_addr: str | None = None,
-              timeout_s: float = 300.0) -> "_tz.Ctrl":
-    """Create the native control plane for this process (SelfCtrl for a single process)."""
+              timeout_s: float = 300.0, backend: str = "auto") -> "_tz.Ctrl":
+    """Create the native control plane for this process (SelfCtrl for a single process).
+
+    backend: "tcp" (torchrun-style RANK / WORLD_SIZE rendezvous), "mpi" (MPI_COMM_WORLD) or
+    "auto" (mpi when an MPI launcher started this process and WORLD_SIZE is unset)."""
+    if backend not in ("auto", "tcp", "mpi"):
+        raise ValueError(f"backend must be auto, tcp or mpi (got {backend!r})")
+    if backend == "mpi" or (backend == "auto" and _mpi_launched()):
+        ctrl = _tz.MpiCtrl()
+        _tz.set_log_rank(ctrl.rank)
+        return ctrl
     e = env()
     rank = e.rank if rank is None else rank
     world = e.world if world is None else world
