@@ -576,11 +576,11 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
   hipStream_t s = nullptr, s2 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  auto release = [&] {
-    if (s2) hipStreamDestroy(s2);
-    if (fork) hipEventDestroy(fork);
-    if (join) hipEventDestroy(join);
-    hipStreamDestroy(s);
+  auto release = [&] { // also on error paths: the first failure is the one reported
+    if (s2) (void)hipStreamDestroy(s2);
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+    (void)hipStreamDestroy(s);
   };
   if (how == "mixed") {
     TZ_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
@@ -641,8 +641,8 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
     ctrl->allreduce_max(red, 2);
     if (v) *v = red[0];
     if (red[1] != 0.0) {
-      hipStreamSynchronize(s);
-      if (s2) hipStreamSynchronize(s2);
+      (void)hipStreamSynchronize(s);
+      if (s2) (void)hipStreamSynchronize(s2);
       release();
       TZ_THROW("link probe (" << via << ") failed" << (e.empty() ? " on another rank" : ": " + e));
     }

@@ -27,12 +27,12 @@ DeviceBuffer::DeviceBuffer(size_t bytes, bool peerWritten) : bytes_(bytes) {
 }
 
 DeviceBuffer::~DeviceBuffer() {
-  if (p_) hipFree(p_);
+  if (p_) (void)hipFree(p_); // teardown: nothing useful to do with an error
 }
 
 DeviceBuffer &DeviceBuffer::operator=(DeviceBuffer &&o) noexcept {
   if (this != &o) {
-    if (p_) hipFree(p_);
+    if (p_) (void)hipFree(p_);
     p_ = o.p_;
     bytes_ = o.bytes_;
     o.p_ = nullptr;

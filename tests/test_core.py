@@ -3,6 +3,7 @@
 test/test_gpu_graph.cu) and adds synchronizer / serdes / equivalence properties."""
 import json
 import os
+import shutil
 import subprocess
 
 import pytest
@@ -48,6 +49,22 @@ def test_native_unit_suite_under_sanitizers(kind):
     assert r.returncode == 0, r.stderr[-4000:]
     assert "0 failures" in r.stderr
     assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
+
+
+@pytest.mark.skipif(shutil.which("cmake") is None, reason="no cmake")
+def test_cmake_build_of_the_core(tmp_path):
+    """the CMake project (for C++ programs that embed the engine, as the reference's drivers link
+    its `tenzing` library) configures, builds the host-only core and its unit suite passes"""
+    b = tmp_path / "b"
+    gen = ["-G", "Ninja"] if shutil.which("ninja") else []
+    r = subprocess.run(["cmake", "-S", ROOT, "-B", str(b), *gen, "-DTZ_BUILD_EXAMPLES=OFF"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    r = subprocess.run(["cmake", "--build", str(b), "--target", "tz-unit", "-j", "8"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    r = subprocess.run([str(b / "tz-unit")], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "0 failures" in r.stderr, r.stderr[-3000:]
 
 
 def test_noop_graph(tz):
