@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--extra", action="store_true", help="also unroll / XCD order / block caps")
+    ap.add_argument("--blocks", action="store_true",
+                    help="also 1-2 items in flight per lane (2-4x the workgroups; the HBM probe, "
+                         "scripts/hbm_roof.hip, copies fastest with ~128 workgroups per CU)")
     a = ap.parse_args()
     torch.zeros(1, device="cuda")
     h, _ = build_halo(HaloConfig(n=a.n, neighbors=26, order="qxyz", transport="direct"),
@@ -30,20 +33,37 @@ def main():
     st = torch.cuda.current_stream()
     dirs = list(range(h.ndirs()))
     unroll, ntp, ntu, mb, ntm = k.get_box_tuning()
-    # name: (nt loads, nt stores, unroll, xcd remap, max blocks per box)
+    mu0, mi0 = k.get_move_unroll(), k.get_move_items()
+    # name: (nt loads, nt stores, items in flight per lane, XCD remap, max blocks per box
+    #        [, items per lane the grid is sized for; default = in flight])
     variants = {"r1_default": (True, False, 4, 0, 4096), "nt_both": (True, True, 4, 0, 4096),
-                "plain": (False, False, 4, 0, 4096), "default": (False, True, 4, 0, 4096)}
+                "plain": (False, False, 4, 0, 4096), "u4": (False, True, 4, 0, 4096)}
     if a.extra:
-        variants.update({"default_u8": (False, True, 8, 0, 4096),
-                         "default_remap1": (False, True, 4, 1, 4096),
-                         "default_remap2": (False, True, 4, 2, 4096),
-                         "default_mb1024": (False, True, 4, 0, 1024),
-                         "default_mb16384": (False, True, 4, 0, 16384)})
+        variants.update({"u4_remap1": (False, True, 4, 1, 4096),
+                         "u4_remap2": (False, True, 4, 2, 4096),
+                         "u4_mb1024": (False, True, 4, 0, 1024),
+                         "u4_mb16384": (False, True, 4, 0, 16384)})
+    if a.blocks:
+        # fewer items per lane: 2x / 4x the workgroups for the same boxes
+        variants.update({"u2": (False, True, 2, 0, 65535),
+                         "u1": (False, True, 1, 0, 65535),
+                         "u2_mb4096": (False, True, 2, 0, 4096),
+                         "u2_remap1": (False, True, 2, 1, 65535),
+                         "u1_remap1": (False, True, 1, 1, 65535),
+                         "u2_plain": (False, False, 2, 0, 65535),
+                         "u2_nt_both": (True, True, 2, 0, 65535),
+                         "u1_i2": (False, True, 1, 0, 65535, 2),
+                         "u1_i3": (False, True, 1, 0, 65535, 3),
+                         "u2_i4": (False, True, 2, 0, 65535, 4),
+                         "u2_i6": (False, True, 2, 0, 65535, 6),
+                         "u4_i8": (False, True, 4, 0, 65535, 8)})
     res = {v: [] for v in variants}
     prev_remap = k.get_xcd_remap()
     for r in range(a.rounds):
-        for name, (ntload, ntstore, u, remap, mbv) in variants.items():
-            k.set_box_tuning(u, ntp, ntu, mbv, ntload)
+        for name, (ntload, ntstore, u, remap, mbv, *items) in variants.items():
+            k.set_box_tuning(unroll, ntp, ntu, mbv, ntload)
+            k.set_move_unroll(u)
+            k.set_move_items(items[0] if items else u)
             k.set_nt_move_store(ntstore)
             k.set_xcd_remap(remap)
             for _ in range(5):
@@ -56,6 +76,8 @@ def main():
             e1.synchronize()
             res[name].append(e0.elapsed_time(e1) * 1e3 / a.reps)
     k.set_box_tuning(unroll, ntp, ntu, mb, ntm)
+    k.set_move_unroll(mu0)
+    k.set_move_items(mi0)
     k.set_nt_move_store(True)
     k.set_xcd_remap(prev_remap)
     h.init_grid()

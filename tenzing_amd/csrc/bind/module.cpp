@@ -969,6 +969,16 @@ PYBIND11_MODULE(_tz, m) {
   k.def("set_nt_move_store", [](bool on) { kern::box_tuning().nt_move_store = on; }, py::arg("on"));
   k.def("get_nt_move_store", []() { return kern::box_tuning().nt_move_store; });
   k.def("get_xcd_remap", []() { return kern::box_tuning().xcd_remap; });
+  k.def("set_move_unroll", [](int u) {
+    TZ_CHECK(u == 1 || u == 2 || u == 4, "move_unroll must be 1, 2 or 4");
+    kern::box_tuning().move_unroll = u;
+  }, py::arg("unroll"));
+  k.def("get_move_unroll", []() { return kern::box_tuning().move_unroll; });
+  k.def("set_move_items", [](int n) {
+    TZ_CHECK(n >= 1 && n <= 64, "move_items must be 1..64");
+    kern::box_tuning().move_items = n;
+  }, py::arg("items"));
+  k.def("get_move_items", []() { return kern::box_tuning().move_items; });
   k.def("get_box_tuning", []() {
     const auto &t = kern::box_tuning();
     return py::make_tuple(t.unroll, t.nt_pack, t.nt_unpack, t.max_blocks, t.nt_move);

@@ -41,6 +41,11 @@ BoxTuning &box_tuning() {
     if (const char *e = std::getenv("TZ_PUT_MAX_BLOCKS")) v.put_max_blocks = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("TZ_NT_MOVE_STORE")) v.nt_move_store = std::atoi(e) != 0;
     if (const char *e = std::getenv("TZ_NT_MOVE_LOAD")) v.nt_move = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TZ_MOVE_UNROLL")) {
+      const int u = std::atoi(e);
+      if (u == 1 || u == 2 || u == 4) v.move_unroll = u;
+      else std::fprintf(stderr, "[tz] warning: TZ_MOVE_UNROLL=%s is not 1, 2 or 4; using %d\n", e, v.move_unroll);
+    }
     if (const char *e = std::getenv("TZ_NT_PACK")) v.nt_pack = std::atoi(e) != 0;
     if (const char *e = std::getenv("TZ_NT_UNPACK")) v.nt_unpack = std::atoi(e) != 0;
     if (const char *e = std::getenv("TZ_XCD_REMAP")) {
@@ -141,10 +146,11 @@ DevDesc make_dev(const BoxDesc &b) {
   return d;
 }
 
-// `cap`: blocks per box at most (0: BoxTuning::max_blocks)
-uint32_t blocks_for(const DevDesc &d, int cap = 0) {
+// `cap`: blocks per box at most (0: BoxTuning::max_blocks); `unroll`: items per lane (0:
+// BoxTuning::unroll)
+uint32_t blocks_for(const DevDesc &d, int cap = 0, int unroll = 0) {
   const BoxTuning &t = box_tuning();
-  const uint64_t per = uint64_t(kThreads) * uint64_t(t.unroll);
+  const uint64_t per = uint64_t(kThreads) * uint64_t(unroll > 0 ? unroll : t.unroll);
   uint64_t b = (uint64_t(d.items) + per - 1) / per;
   const uint64_t m = uint64_t(std::max(1, cap > 0 ? cap : t.max_blocks));
   return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(b, m)));
@@ -556,7 +562,15 @@ namespace {
 // the device batch of a move launch (shared by the plain and the signalling variant);
 // `keep` maps batch entries back to input boxes
 DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vector<int> &keep,
-                         int cap = 0);
+                         int cap = 0, int unroll = 0);
+
+template <int U>
+void launch_move(const dim3 &g, hipStream_t s, const DevBatch &b, const DevRemap &r, bool ntl, bool nts) {
+  if (ntl && nts) hipLaunchKernelGGL((box_move_many_k<U, true, true>), g, dim3(kThreads), 0, s, b, r);
+  else if (ntl) hipLaunchKernelGGL((box_move_many_k<U, true, false>), g, dim3(kThreads), 0, s, b, r);
+  else if (nts) hipLaunchKernelGGL((box_move_many_k<U, false, true>), g, dim3(kThreads), 0, s, b, r);
+  else hipLaunchKernelGGL((box_move_many_k<U, false, false>), g, dim3(kThreads), 0, s, b, r);
+}
 } // namespace
 
 void box_move_many(const MoveDesc *moves, int n, void *stream) {
@@ -564,7 +578,10 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
   if (n > kMaxBoxes) throw std::runtime_error("box_move_many: too many boxes");
   uint32_t total = 0;
   std::vector<int> keep;
-  DevBatch b = make_move_batch(moves, n, total, keep);
+  const int U = box_tuning().move_unroll;
+  if (U != 1 && U != 2 && U != 4) throw std::runtime_error("box_move_many: move_unroll must be 1, 2 or 4");
+  const int items = std::max(U, box_tuning().move_items);
+  DevBatch b = make_move_batch(moves, n, total, keep, 0, items);
   if (b.n == 0) return;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int mode = box_tuning().xcd_remap;
@@ -586,14 +603,9 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
   r.per_xcd = mode == 1 ? (total + 7) / 8 : 0;
   const dim3 g(r.per_xcd ? r.per_xcd * 8 : total);
   const BoxTuning &t = box_tuning();
-  if (t.nt_move && t.nt_move_store)
-    hipLaunchKernelGGL((box_move_many_k<4, true, true>), g, dim3(kThreads), 0, s, b, r);
-  else if (t.nt_move)
-    hipLaunchKernelGGL((box_move_many_k<4, true, false>), g, dim3(kThreads), 0, s, b, r);
-  else if (t.nt_move_store)
-    hipLaunchKernelGGL((box_move_many_k<4, false, true>), g, dim3(kThreads), 0, s, b, r);
-  else
-    hipLaunchKernelGGL((box_move_many_k<4, false, false>), g, dim3(kThreads), 0, s, b, r);
+  if (U == 1) launch_move<1>(g, s, b, r, t.nt_move, t.nt_move_store);
+  else if (U == 2) launch_move<2>(g, s, b, r, t.nt_move, t.nt_move_store);
+  else launch_move<4>(g, s, b, r, t.nt_move, t.nt_move_store);
   TZ_HIP_LAUNCH_CHECK();
 }
 
@@ -685,7 +697,7 @@ void ipc_signal(unsigned long long *const *signal, int n, void *stream) {
 
 namespace {
 DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vector<int> &keep,
-                         int cap) {
+                         int cap, int unroll) {
   DevBatch b{};
   b.n = 0;
   total = 0;
@@ -716,7 +728,7 @@ DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vec
     }
     b.d[b.n] = d;
     b.block_start[b.n] = total;
-    total += blocks_for(d, cap);
+    total += blocks_for(d, cap, unroll);
     keep.push_back(i);
     ++b.n;
   }

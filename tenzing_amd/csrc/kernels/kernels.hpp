@@ -45,6 +45,13 @@ struct BoxTuning {
   // loads plus stores: 57.7 us). Env TZ_NT_MOVE_LOAD / TZ_NT_MOVE_STORE override.
   bool nt_move = false;
   bool nt_move_store = true;
+  // box_move (direct transfers): items in flight per lane (1, 2 or 4; env TZ_MOVE_UNROLL) and
+  // items per lane the grid is sized for (>= in flight; the lane loops over them). One in
+  // flight, two per lane (twice the workgroups of 4 x 4) moves the 26 directions at 512^3 x 3
+  // in 43.5 us against 44.1 us, the best of 10 shapes (scripts/move_ab.py --blocks,
+  // profiles/r2_move_shape/)
+  int move_unroll = 1;
+  int move_items = 2;
   int xcd_remap = 0; // box_move block order: 0 round-robin, 1 one contiguous range per XCD,
                      // 2 every box split into 8 contiguous per-XCD shares
 };
