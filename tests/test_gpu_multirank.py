@@ -141,6 +141,29 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     assert p["busiest_link_MB"] > p["face_MB"] > 0 and p["busiest_link_at_probe_rate_ms"] > 0
 
 
+def test_bench_two_ranks_under_mpiexec(gpu):
+    """the same bench flow started the reference's way, by an MPI launcher: the control plane is
+    MPI_COMM_WORLD (MpiCtrl), so the schedule broadcasts, max-reductions and the IPC handle
+    exchange all go over MPI, while the transfers stay on the GPU"""
+    import shutil
+
+    mpiexec = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
+    if not os.path.exists(mpiexec):
+        pytest.skip("no MPI launcher")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [mpiexec, "-n", "2", sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "6", "--warmup", "2", "--cells", "64", "--mcts-iters", "6",
+           "--bench-iters", "3", "--deadline-s", "240", "--link-probe-iters", "0"]
+    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the one result line
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["verified_bad_cells"] == 0 and j["verified_bad_cells_after_timing"] == 0
+    assert j["config"]["rank_grid"] == [1, 1, 2] and j["mcts_candidates"] == 6
+
+
 @pytest.mark.parametrize("world,case", [(2, "spmv"), (4, "spmv"), (8, "spmv"), (2, "fused")])
 def test_spmv_ipc_loopback(gpu, world, case):
     """distributed SpMV (and SpMV + halo in one graph, BASELINE config 5) on several ranks of
