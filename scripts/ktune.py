@@ -24,15 +24,23 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--unrolls", default="",
+                    help="comma list: sweep items per lane (grid sizing) at the default nt "
+                         "settings instead of the round-1 grid (1-2: more workgroups, one item "
+                         "in flight; the direct move gained 1.2 %% that way, profiles/r2_move_shape/)")
     a = ap.parse_args()
     torch.zeros(1, device="cuda")
-    h, _ = build_halo(HaloConfig(n=a.n, neighbors=26, order=a.order), tz.SelfCtrl(), device=0)
+    h, _ = build_halo(HaloConfig(n=a.n, neighbors=26, order=a.order, transport="copy"),
+                      tz.SelfCtrl(), device=0)
     s = torch.cuda.current_stream()
     st = s.cuda_stream
     K = tz._tz.kernels
     # (unroll, nt_pack, nt_unpack, max_blocks); first round (r1) showed unroll 8 and block caps
     # neutral, nt pack loads -27 %, nt unpack stores +5 %
+    prev = K.get_box_tuning()
     configs = list(itertools.product([4, 8], [False, True], [False, True], [4096]))
+    if a.unrolls:
+        configs = [(int(u), True, ntu, 65535) for u in a.unrolls.split(",") for ntu in (False, True)]
     res = {c: {"pack": [], "shift": [], "unpack": [], "iter": []} for c in configs}
     for _ in range(a.rounds):
         for c in configs:
@@ -59,7 +67,7 @@ def main():
         print(json.dumps({"unroll": c[0], "nt_pack": c[1], "nt_unpack": c[2], "max_blocks": c[3],
                           **{k: round(statistics.median(v), 2) for k, v in r.items()},
                           "iter_min": round(min(r["iter"]), 2)}), flush=True)
-    K.set_box_tuning(4, True, False, 4096)
+    K.set_box_tuning(*prev)
 
 
 if __name__ == "__main__":

@@ -953,12 +953,14 @@ PYBIND11_MODULE(_tz, m) {
     kern::box_move_many(ms.data(), int(ms.size()), P(s));
   }, py::arg("moves"), py::arg("stream") = 0);
   k.def("set_box_tuning", [](int unroll, bool ntPack, bool ntUnpack, int maxBlocks, bool ntMove) {
+    TZ_CHECK(unroll >= 1 && unroll <= 64, "unroll must be 1..64");
+    TZ_CHECK(maxBlocks >= 1, "max_blocks must be positive");
     kern::box_tuning().unroll = unroll;
     kern::box_tuning().nt_pack = ntPack;
     kern::box_tuning().nt_unpack = ntUnpack;
     kern::box_tuning().max_blocks = maxBlocks;
     kern::box_tuning().nt_move = ntMove;
-  }, py::arg("unroll") = 4, py::arg("nt_pack") = true, py::arg("nt_unpack") = true,
+  }, py::arg("unroll") = 3, py::arg("nt_pack") = true, py::arg("nt_unpack") = true,
      py::arg("max_blocks") = 4096, py::arg("nt_move") = false);
   k.def("set_xcd_remap", &kern::set_xcd_remap, py::arg("mode"));
   k.def("set_put_max_blocks", [](int b) {

@@ -389,6 +389,9 @@ void dispatch_one(dim3 g, hipStream_t s, double *grid, const DevDesc &d) {
   if (box_tuning().unroll >= 8) {
     if (nt) launch_one<UNPACK, 8, true>(g, s, grid, d);
     else launch_one<UNPACK, 8, false>(g, s, grid, d);
+  } else if (box_tuning().unroll < 4) { // one item in flight, `unroll` items per lane
+    if (nt) launch_one<UNPACK, 1, true>(g, s, grid, d);
+    else launch_one<UNPACK, 1, false>(g, s, grid, d);
   } else {
     if (nt) launch_one<UNPACK, 4, true>(g, s, grid, d);
     else launch_one<UNPACK, 4, false>(g, s, grid, d);
@@ -401,6 +404,9 @@ void dispatch_many(dim3 g, hipStream_t s, double *grid, const DevBatch &b) {
   if (box_tuning().unroll >= 8) {
     if (nt) launch_many<UNPACK, 8, true>(g, s, grid, b);
     else launch_many<UNPACK, 8, false>(g, s, grid, b);
+  } else if (box_tuning().unroll < 4) { // one item in flight, `unroll` items per lane
+    if (nt) launch_many<UNPACK, 1, true>(g, s, grid, b);
+    else launch_many<UNPACK, 1, false>(g, s, grid, b);
   } else {
     if (nt) launch_many<UNPACK, 4, true>(g, s, grid, b);
     else launch_many<UNPACK, 4, false>(g, s, grid, b);

@@ -25,7 +25,10 @@ constexpr int kMaxBoxes = 32;
 
 /// launch tuning of the box kernels (process-wide; measured defaults)
 struct BoxTuning {
-  int unroll = 4;         // items in flight per lane: 4 or 8 (8: no gain, scripts/ktune.py)
+  // pack / unpack: items per lane the grid is sized for; 4 or 8 keep that many loads in flight,
+  // 1-3 keep one in flight. 3 packs and unpacks 2 % faster than 4 in pipeline context
+  // (scripts/ktune.py --unrolls, profiles/r2_move_shape/ktune_unrolls*.jsonl); 8 is slower
+  int unroll = 3;
   bool nt_pack = true;    // non-temporal grid loads in pack: -27 % pack time in pipeline context
   // non-temporal ghost stores in unpack: the ghosts are not read again within the exchange.
   // Round 1 measured +5 % on the one-rank pack -> copy -> unpack chain; the receive-buffer
