@@ -878,23 +878,6 @@ PYBIND11_MODULE(_tz, m) {
                    reinterpret_cast<float *>(y), lanes, acc, P(s));
   }, py::arg("n_rows"), py::arg("row_ptr"), py::arg("col_ind"), py::arg("val"), py::arg("x"), py::arg("y"),
      py::arg("lanes") = 0, py::arg("accumulate") = false, py::arg("stream") = 0);
-  k.def("build_panel_csr", [](const std::vector<int32_t> &rp, const std::vector<int32_t> &ci,
-                              const std::vector<float> &v, int nCols, int width) {
-    TZ_CHECK(!rp.empty() && size_t(rp.back()) == ci.size() && ci.size() == v.size(), "bad CSR arrays");
-    auto m = kern::build_panel_csr(int(rp.size()) - 1, nCols, rp.data(), ci.data(), v.data(), width);
-    return py::make_tuple(m.nPanels, m.rowPtr, m.col, m.val);
-  }, py::arg("row_ptr"), py::arg("col_ind"), py::arg("val"), py::arg("n_cols"),
-     py::arg("width") = kern::kPanelWidth,
-     "column-panel CSR (n_panels, row_ptr, col (u16), val) for csr_spmv_panel");
-  k.def("csr_spmv_panel", [](int n, int nCols, int nPanels, int width, uintptr_t rp, uintptr_t ci, uintptr_t v,
-                             uintptr_t x, uintptr_t y, bool acc, uintptr_t s) {
-    kern::csr_spmv_panel(n, nCols, nPanels, width, reinterpret_cast<const int32_t *>(rp),
-                         reinterpret_cast<const uint16_t *>(ci), reinterpret_cast<const float *>(v),
-                         reinterpret_cast<const float *>(x), reinterpret_cast<float *>(y), acc, P(s));
-  }, py::arg("n_rows"), py::arg("n_cols"), py::arg("n_panels"), py::arg("width"), py::arg("row_ptr"),
-     py::arg("col"), py::arg("val"), py::arg("x"), py::arg("y"), py::arg("accumulate") = false,
-     py::arg("stream") = 0);
-  k.attr("PANEL_WIDTH") = kern::kPanelWidth;
   py::class_<RocsparseCsr, std::shared_ptr<RocsparseCsr>>(
       k, "RocsparseCsr", "rocSPARSE CSR SpMV (library comparison variant): y = A x on raw pointers")
       .def(py::init([](int64_t m, int64_t n, int64_t nnz, uintptr_t rp, uintptr_t ci, uintptr_t v,

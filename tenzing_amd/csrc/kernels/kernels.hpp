@@ -5,7 +5,6 @@
 #pragma once
 
 #include <cstdint>
-#include <vector>
 
 namespace tz {
 namespace kern {
@@ -124,24 +123,6 @@ void copy_many(const CopyDesc *d, int n, void *stream);
 /// reduction). When `accumulate`, y[r] += ... instead.
 void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,
               const float *x, float *y, int lanesPerRow, bool accumulate, void *stream);
-/// Column-panel CSR for csr_spmv_panel: the entries of panel p (columns [p*width, (p+1)*width))
-/// come before those of panel p+1, each panel in CSR order with panel-local 16-bit column
-/// indices; rowPtr holds nPanels * (nRows + 1) absolute offsets.
-constexpr int kPanelWidth = 40960; // f32 columns per panel: all 160 KB of a gfx950 workgroup's LDS
-struct PanelCsr {
-  int nRows = 0, nCols = 0, nPanels = 0, width = kPanelWidth;
-  std::vector<int32_t> rowPtr;
-  std::vector<uint16_t> col;
-  std::vector<float> val;
-};
-PanelCsr build_panel_csr(int nRows, int nCols, const int32_t *rowPtr, const int32_t *colInd,
-                         const float *val, int width = kPanelWidth);
-/// y = A x (y += A x when `accumulate`) with x staged through LDS one column panel at a time:
-/// every workgroup owns a row range, copies each x panel into LDS with 16-B loads and gathers
-/// from LDS instead of issuing one L2 request per nonzero.
-void csr_spmv_panel(int nRows, int nCols, int nPanels, int width, const int32_t *pRowPtr,
-                    const uint16_t *pCol, const float *pVal, const float *x, float *y,
-                    bool accumulate, void *stream);
 /// dst[i] = src[idx[i]]
 void gather_f32(int n, const float *src, const int32_t *idx, float *dst, void *stream);
 /// one peer's part of an IPC put of the SpMV x halo: dst[i] = src[idx[off + i]], i < n, then

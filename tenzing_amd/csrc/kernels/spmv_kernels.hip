@@ -100,66 +100,6 @@ __global__ __launch_bounds__(kThreads) void csr_spmv_stream_k(int nRows,
   if (row < nr && sub == 0) y[r0 + row] = accumulate ? y[r0 + row] + sum : sum;
 }
 
-// LDS column panels: a 1024-thread workgroup owns up to 4096 consecutive rows (one thread per
-// row, up to kPanelRpt rows per thread) and walks the column panels in order. Per panel it copies
-// x's panel into LDS (16-B loads, every lane), then each row thread gathers its panel entries
-// from LDS. At the reference's band width every row touches the whole x, so one L2 request per
-// nonzero (one 128-B line for 4 useful bytes) becomes one 16-B load per 4 columns per
-// workgroup plus LDS reads; 16-bit panel-local column indices also cut the matrix stream.
-constexpr int kPanelThreads = 1024, kPanelRpt = 4;
-constexpr int kPanelStage = kPanelWidth / 4 / kPanelThreads; // 16-B loads per lane per panel
-static_assert(kPanelStage * 4 * kPanelThreads == kPanelWidth, "panel width: whole 16-B loads per lane");
-typedef float f4_t __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(kPanelThreads) void csr_spmv_panel_k(
-    int nRows, int nCols, int nPanels, int width, int rowsPerBlock, const int32_t *__restrict__ pRowPtr,
-    const uint16_t *__restrict__ pCol, const float *__restrict__ pVal, const float *__restrict__ x,
-    float *__restrict__ y, int accumulate) {
-  __shared__ float xs[kPanelWidth];
-  const int r0 = blockIdx.x * rowsPerBlock;
-  const int r1 = min(nRows, r0 + rowsPerBlock);
-  float acc[kPanelRpt];
-#pragma unroll
-  for (int k = 0; k < kPanelRpt; ++k) acc[k] = 0.f;
-  for (int p = 0; p < nPanels; ++p) {
-    const int c0 = p * width, w = min(width, nCols - c0);
-    if (p) __syncthreads(); // every row thread is done with the previous panel
-    const float *xp = x + c0;
-    const int w4 = (reinterpret_cast<uintptr_t>(xp) & 15) == 0 ? w / 4 : 0;
-    // the whole panel in flight at once: every lane issues all its 16-B loads before the
-    // first LDS write
-    f4_t v[kPanelStage];
-#pragma unroll
-    for (int u = 0; u < kPanelStage; ++u) {
-      const int i = int(threadIdx.x) + u * kPanelThreads;
-      if (i < w4) v[u] = reinterpret_cast<const f4_t *>(xp)[i];
-    }
-#pragma unroll
-    for (int u = 0; u < kPanelStage; ++u) {
-      const int i = int(threadIdx.x) + u * kPanelThreads;
-      if (i < w4) reinterpret_cast<f4_t *>(xs)[i] = v[u];
-    }
-    for (int i = w4 * 4 + threadIdx.x; i < w; i += kPanelThreads) xs[i] = xp[i];
-    __syncthreads();
-    const int32_t *rp = pRowPtr + int64_t(p) * (nRows + 1);
-#pragma unroll
-    for (int k = 0; k < kPanelRpt; ++k) {
-      const int row = r0 + int(threadIdx.x) + k * kPanelThreads;
-      if (row < r1) {
-        const int a = rp[row], b = rp[row + 1];
-        float s = 0.f;
-        for (int j = a; j < b; ++j) s = fmaf(pVal[j], xs[pCol[j]], s);
-        acc[k] += s;
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kPanelRpt; ++k) {
-    const int row = r0 + int(threadIdx.x) + k * kPanelThreads;
-    if (row < r1) y[row] = accumulate ? y[row] + acc[k] : acc[k];
-  }
-}
-
 __global__ __launch_bounds__(kThreads) void gather_k(int n, const float *__restrict__ src,
                                                      const int32_t *__restrict__ idx,
                                                      float *__restrict__ dst) {
@@ -295,73 +235,6 @@ int grid_for(int64_t n, int perThread = 1) {
 }
 
 } // namespace
-
-PanelCsr build_panel_csr(int nRows, int nCols, const int32_t *rowPtr, const int32_t *colInd,
-                         const float *val, int width) {
-  if (nRows < 0 || nCols < 0) throw std::invalid_argument("build_panel_csr: negative size");
-  if (width < 1 || width > kPanelWidth || width > 65536)
-    throw std::invalid_argument("build_panel_csr: panel width must be 1.." + std::to_string(kPanelWidth));
-  PanelCsr m;
-  m.nRows = nRows;
-  m.nCols = nCols;
-  m.width = width;
-  m.nPanels = std::max(1, (nCols + width - 1) / width);
-  const int64_t nnz = nRows ? rowPtr[nRows] : 0;
-  m.rowPtr.assign(size_t(m.nPanels) * size_t(nRows + 1), 0);
-  m.col.resize(size_t(nnz));
-  m.val.resize(size_t(nnz));
-  // counts per (panel, row), then prefix sums in panel-major order
-  std::vector<int64_t> cnt(size_t(m.nPanels) * size_t(nRows), 0);
-  for (int r = 0; r < nRows; ++r)
-    for (int32_t j = rowPtr[r]; j < rowPtr[r + 1]; ++j) {
-      if (colInd[j] < 0 || colInd[j] >= nCols) throw std::invalid_argument("build_panel_csr: column out of range");
-      ++cnt[size_t(colInd[j] / width) * size_t(nRows) + size_t(r)];
-    }
-  int64_t off = 0;
-  for (int p = 0; p < m.nPanels; ++p) {
-    int32_t *rp = m.rowPtr.data() + size_t(p) * size_t(nRows + 1);
-    for (int r = 0; r < nRows; ++r) {
-      rp[r] = int32_t(off);
-      off += cnt[size_t(p) * size_t(nRows) + size_t(r)];
-    }
-    rp[nRows] = int32_t(off);
-  }
-  // scatter: a row's entries keep their CSR order inside each panel
-  std::vector<int64_t> fill(size_t(m.nPanels) * size_t(nRows));
-  for (int p = 0; p < m.nPanels; ++p)
-    for (int r = 0; r < nRows; ++r)
-      fill[size_t(p) * size_t(nRows) + size_t(r)] = m.rowPtr[size_t(p) * size_t(nRows + 1) + size_t(r)];
-  for (int r = 0; r < nRows; ++r)
-    for (int32_t j = rowPtr[r]; j < rowPtr[r + 1]; ++j) {
-      const int p = colInd[j] / width;
-      const int64_t k = fill[size_t(p) * size_t(nRows) + size_t(r)]++;
-      m.col[size_t(k)] = uint16_t(colInd[j] - p * width);
-      m.val[size_t(k)] = val[j];
-    }
-  return m;
-}
-
-void csr_spmv_panel(int nRows, int nCols, int nPanels, int width, const int32_t *pRowPtr,
-                    const uint16_t *pCol, const float *pVal, const float *x, float *y,
-                    bool accumulate, void *stream) {
-  if (nRows <= 0) return;
-  if (width < 1 || width > kPanelWidth || nPanels < 1 || int64_t(nPanels) * width < nCols)
-    throw std::invalid_argument("csr_spmv_panel: panels do not cover the columns");
-  static int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    return n;
-  }();
-  // one workgroup per CU when the rows allow (the x panels are re-read per workgroup), at most
-  // kPanelRpt rows per thread
-  const int rows = std::min<int>(kPanelThreads * kPanelRpt, std::max(1, (nRows + cus - 1) / cus));
-  const dim3 g(unsigned((nRows + rows - 1) / rows));
-  hipLaunchKernelGGL(csr_spmv_panel_k, g, dim3(kPanelThreads), 0, static_cast<hipStream_t>(stream), nRows,
-                     nCols, nPanels, width, rows, pRowPtr, pCol, pVal, x, y, accumulate ? 1 : 0);
-  TZ_HIP_LAUNCH_CHECK();
-}
 
 void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,
               const float *x, float *y, int lanesPerRow, bool accumulate, void *stream) {

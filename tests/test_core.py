@@ -395,30 +395,3 @@ def test_settling_stops_consistent_candidates_early(tz):
         else:
             assert b.settled == 0
     assert tz.BenchOpts(settle_ratio=0.1).settle_ratio == 0.1
-
-
-def test_panel_csr_layout(tz):
-    """column-panel CSR of csr_spmv_panel: panel-major entries, panel-local 16-bit columns, every
-    row's entries in CSR order within a panel; the product over panels equals the CSR product"""
-    import numpy as np
-
-    n = 700
-    rp, ci, val = tz._tz.random_band_matrix(n, 300, 10 * n, 3)
-    for width in (64, 250, 700, tz._tz.kernels.PANEL_WIDTH):
-        npan, prp, pcol, pval = tz._tz.kernels.build_panel_csr(rp, ci, val, n, width)
-        assert npan == max(1, -(-n // width)) and len(prp) == npan * (n + 1)
-        assert len(pcol) == len(ci) and max(pcol) < width
-        x = np.random.default_rng(0).standard_normal(n)
-        y = np.zeros(n)
-        for p in range(npan):
-            r = prp[p * (n + 1):(p + 1) * (n + 1)]
-            for i in range(n):
-                for j in range(r[i], r[i + 1]):
-                    y[i] += pval[j] * x[p * width + pcol[j]]
-        ref = np.zeros(n)
-        for i in range(n):
-            for j in range(rp[i], rp[i + 1]):
-                ref[i] += val[j] * x[ci[j]]
-        assert np.allclose(y, ref)
-    with pytest.raises(Exception, match="panel width"):
-        tz._tz.kernels.build_panel_csr(rp, ci, val, n, 0)

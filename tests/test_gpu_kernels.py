@@ -135,33 +135,6 @@ def test_csr_spmv_matches_torch(tz, gpu, lanes, per_row):
     assert torch.allclose(y.double().cpu(), 2 * ref, rtol=1e-4, atol=2e-4)
 
 
-@pytest.mark.parametrize("n,width", [(5000, 40960), (5000, 1024), (5000, 777), (70000, 40960)])
-def test_csr_spmv_panel_matches_torch(tz, gpu, n, width):
-    """x staged through LDS one column panel at a time (one panel, several panels, a width not
-    a multiple of 4 so panels start unaligned, and more rows than one workgroup per CU holds)"""
-    rp, ci, val = tz._tz.random_band_matrix(n, min(n, 3000), 10 * n, 11)
-    K = tz._tz.kernels
-    npan, prp, pcol, pval = K.build_panel_csr(rp, ci, val, n, width)
-    prp_t = torch.tensor(prp, dtype=torch.int32, device="cuda")
-    pcol_t = torch.tensor(pcol, dtype=torch.int32).to(torch.uint16).cuda() if hasattr(torch, "uint16") \
-        else torch.tensor(pcol, dtype=torch.int32).to(torch.int16).cuda()
-    pval_t = torch.tensor(pval, dtype=torch.float32, device="cuda")
-    x = torch.randn(n, dtype=torch.float32, device="cuda")
-    y = torch.zeros(n, dtype=torch.float32, device="cuda")
-    K.csr_spmv_panel(n, n, npan, width, prp_t.data_ptr(), pcol_t.data_ptr(), pval_t.data_ptr(),
-                     x.data_ptr(), y.data_ptr(), False, _stream())
-    rp_t = torch.tensor(rp, dtype=torch.int64)
-    A = torch.sparse_csr_tensor(rp_t, torch.tensor(ci, dtype=torch.int64),
-                                torch.tensor(val, dtype=torch.float32), size=(n, n)).to_dense()
-    ref = A.double() @ x.double().cpu()
-    torch.cuda.synchronize()
-    assert torch.allclose(y.double().cpu(), ref, rtol=1e-4, atol=1e-4)
-    K.csr_spmv_panel(n, n, npan, width, prp_t.data_ptr(), pcol_t.data_ptr(), pval_t.data_ptr(),
-                     x.data_ptr(), y.data_ptr(), True, _stream())
-    torch.cuda.synchronize()
-    assert torch.allclose(y.double().cpu(), 2 * ref, rtol=1e-4, atol=2e-4)
-
-
 def test_vector_kernels(tz, gpu):
     n = 100_003
     a = torch.randn(n, device="cuda")
