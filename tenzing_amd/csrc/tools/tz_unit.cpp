@@ -336,6 +336,21 @@ TEST(mcts_finds_good_schedule) {
   }
 }
 
+TEST(mcts_large_tree_stops) {
+  // reference Stop::Reason::large_tree (tenzing-mcts mcts.hpp:131)
+  auto g = diamond(10, 100, 100, 10);
+  SimBenchmarker sb(4, SimParams());
+  SelfCtrl ctrl;
+  MctsOpts o;
+  o.n_iters = 0;
+  o.max_tree_nodes = 50;
+  o.bench.n_iters = 2;
+  SearchResult r = mcts_explore(*g, Platform::make_n_streams(4), sb, ctrl, o);
+  CHECK(r.stop_reason == "large_tree");
+  CHECK(r.tree_size >= 50);
+  CHECK(!r.sims.empty());
+}
+
 TEST(mcts_full_tree_stops) {
   auto g = std::make_shared<Graph>();
   auto a = std::make_shared<NoOp>("a"), b = std::make_shared<NoOp>("b");
