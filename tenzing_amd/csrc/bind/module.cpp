@@ -503,6 +503,7 @@ PYBIND11_MODULE(_tz, m) {
   py::class_<MpiCtrl, Ctrl, std::shared_ptr<MpiCtrl>>(m, "MpiCtrl")
       .def(py::init<const std::string &>(), py::arg("lib") = "", py::call_guard<py::gil_scoped_release>())
       .def_static("launched", &MpiCtrl::launched)
+      .def_static("launcher_size", &MpiCtrl::launcher_size)
       .def_static("launcher_local_rank", &MpiCtrl::launcher_local_rank)
       .def_property_readonly("library", &MpiCtrl::library);
 

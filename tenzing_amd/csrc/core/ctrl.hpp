@@ -83,7 +83,9 @@ private:
 class MpiCtrl : public Ctrl {
 public:
   explicit MpiCtrl(const std::string &lib = "");
-  /// this process was started by an MPI launcher (PMI / PMIx / MVAPICH environment)
+  /// ranks the MPI launcher started (PMI / PMIx / MVAPICH / Open MPI environment), 1 if none
+  static int launcher_size();
+  /// this process is one of several ranks started by an MPI launcher
   static bool launched();
   /// the node-local rank the launcher exported, -1 if none
   static int launcher_local_rank();

@@ -125,11 +125,20 @@ Api &api(const std::string &want) {
 
 } // namespace
 
+int MpiCtrl::launcher_size() {
+  // MPICH hydra / PMI-1 and PMI-2, MVAPICH, Open MPI; Slurm srun (PMIx) exports only the rank
+  // through PMIx, so its task count counts only next to a PMI rank
+  for (const char *v : {"PMI_SIZE", "MV2_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_SIZE"})
+    if (const char *e = std::getenv(v)) return std::atoi(e);
+  if (std::getenv("PMIX_RANK") || std::getenv("PMI_RANK"))
+    if (const char *e = std::getenv("SLURM_NTASKS")) return std::atoi(e);
+  return 1;
+}
+
 bool MpiCtrl::launched() {
-  // MPICH hydra / PMI-1 and PMI-2, PMIx (Slurm, OpenPMIx), MVAPICH, Slurm srun
-  for (const char *v : {"PMI_SIZE", "PMI_RANK", "PMIX_RANK", "MV2_COMM_WORLD_SIZE", "MPI_LOCALNRANKS"})
-    if (std::getenv(v)) return true;
-  return false;
+  // one rank needs no control plane at all: a single process under a PMI environment (a batch
+  // system that wraps every job) keeps the plain single-process path
+  return launcher_size() > 1;
 }
 
 int MpiCtrl::launcher_local_rank() {

@@ -38,8 +38,9 @@ def _mpi_launched() -> bool:
 def env() -> DistEnv:
     if _mpi_launched():
         e = os.environ
-        rank = int(e.get("PMI_RANK", e.get("PMIX_RANK", e.get("MV2_COMM_WORLD_RANK", 0))))
-        world = int(e.get("PMI_SIZE", e.get("MV2_COMM_WORLD_SIZE", 1)))
+        rank = int(e.get("PMI_RANK", e.get("PMIX_RANK", e.get("MV2_COMM_WORLD_RANK",
+                                                              e.get("OMPI_COMM_WORLD_RANK", 0)))))
+        world = _tz.MpiCtrl.launcher_size()
         local = _tz.MpiCtrl.launcher_local_rank()
         return DistEnv(rank, world, local if local >= 0 else rank)
     rank = int(os.environ.get("RANK", 0))
