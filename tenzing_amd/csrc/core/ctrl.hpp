@@ -83,7 +83,7 @@ private:
 class MpiCtrl : public Ctrl {
 public:
   explicit MpiCtrl(const std::string &lib = "");
-  /// ranks the MPI launcher started (PMI / PMIx / MVAPICH / Open MPI environment), 1 if none
+  /// ranks an MPICH-family launcher started (PMI / PMIx / MVAPICH environment), 1 if none
   static int launcher_size();
   /// this process is one of several ranks started by an MPI launcher
   static bool launched();

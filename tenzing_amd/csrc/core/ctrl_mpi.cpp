@@ -126,9 +126,10 @@ Api &api(const std::string &want) {
 } // namespace
 
 int MpiCtrl::launcher_size() {
-  // MPICH hydra / PMI-1 and PMI-2, MVAPICH, Open MPI; Slurm srun (PMIx) exports only the rank
-  // through PMIx, so its task count counts only next to a PMI rank
-  for (const char *v : {"PMI_SIZE", "MV2_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_SIZE"})
+  // MPICH hydra / PMI-1 and PMI-2, MVAPICH; Slurm srun (PMIx) exports only the rank through
+  // PMIx, so its task count counts only next to a PMI rank. Open MPI's launcher is not an MPICH
+  // one: its ranks keep the TCP control plane (tz-search reads OMPI_COMM_WORLD_RANK / _SIZE)
+  for (const char *v : {"PMI_SIZE", "MV2_COMM_WORLD_SIZE"})
     if (const char *e = std::getenv(v)) return std::atoi(e);
   if (std::getenv("PMIX_RANK") || std::getenv("PMI_RANK"))
     if (const char *e = std::getenv("SLURM_NTASKS")) return std::atoi(e);

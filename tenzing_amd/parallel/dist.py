@@ -38,8 +38,7 @@ def _mpi_launched() -> bool:
 def env() -> DistEnv:
     if _mpi_launched():
         e = os.environ
-        rank = int(e.get("PMI_RANK", e.get("PMIX_RANK", e.get("MV2_COMM_WORLD_RANK",
-                                                              e.get("OMPI_COMM_WORLD_RANK", 0)))))
+        rank = int(e.get("PMI_RANK", e.get("PMIX_RANK", e.get("MV2_COMM_WORLD_RANK", 0))))
         world = _tz.MpiCtrl.launcher_size()
         local = _tz.MpiCtrl.launcher_local_rank()
         return DistEnv(rank, world, local if local >= 0 else rank)

@@ -12,7 +12,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MPIEXEC = shutil.which("mpiexec") or ("/opt/conda/bin/mpiexec"
                                       if os.path.exists("/opt/conda/bin/mpiexec") else None)
-pytestmark = pytest.mark.skipif(MPIEXEC is None, reason="no MPI launcher in this image")
+needs_mpi = pytest.mark.skipif(MPIEXEC is None, reason="no MPI launcher in this image")
 
 BODY = r"""
 import json, sys
@@ -48,6 +48,7 @@ def _mpiexec(n, argv, timeout=180):
                           timeout=timeout, env=e, cwd="/tmp")
 
 
+@needs_mpi
 def test_mpi_ctrl_collectives_and_search():
     p = _mpiexec(3, [sys.executable, "-c", BODY.format(root=ROOT)])
     assert p.returncode == 0, p.stdout + p.stderr
@@ -62,6 +63,7 @@ def test_mpi_ctrl_collectives_and_search():
     assert rs[0]["n"] == 8 and rs[1]["n"] == 0  # only rank 0 holds results
 
 
+@needs_mpi
 def test_native_cli_under_mpiexec():
     """tz-search picks the MPI control plane when an MPI launcher started it (--ctrl auto)"""
     exe = os.path.join(ROOT, "tenzing_amd", "bin", "tz-search")
@@ -73,3 +75,24 @@ def test_native_cli_under_mpiexec():
     assert summary and summary[0]["ranks"] == 2 and summary[0]["candidates"] == 6
     # the results CSV comes from rank 0 only
     assert sum(ln.startswith("0|") for ln in p.stdout.splitlines()) == 1
+
+
+@pytest.mark.parametrize("env,launched", [
+    ({}, False),
+    ({"PMI_RANK": "0", "PMI_SIZE": "1"}, False),       # one rank under a PMI batch wrapper
+    ({"PMIX_RANK": "0", "SLURM_NTASKS": "1"}, False),
+    ({"PMI_RANK": "1", "PMI_SIZE": "4"}, True),
+    ({"OMPI_COMM_WORLD_RANK": "0", "OMPI_COMM_WORLD_SIZE": "2"}, False),  # not MPICH ABI
+    ({"PMIX_RANK": "3", "SLURM_NTASKS": "8"}, True),
+])
+def test_mpi_launch_detection(env, launched):
+    """MPI is picked only for several launcher ranks; a single process keeps the plain path
+    (no MPI library is opened)"""
+    code = ("import sys; sys.path.insert(0, %r); import tenzing_amd as tz; "
+            "print(tz._tz.MpiCtrl.launched(), tz._tz.MpiCtrl.launcher_size())" % ROOT)
+    e = {k: v for k, v in os.environ.items()
+         if not k.startswith(("PMI", "OMPI_", "MV2_", "SLURM_", "MPI_LOCAL"))}
+    e.update(env)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=e,
+                         timeout=120).stdout.split()
+    assert out[0] == str(launched)
