@@ -134,6 +134,15 @@ def cmd_search(a) -> int:
         o.dump_tree = a.dump_tree
         o.bench = bo
         o.trap_signals = True
+        if a.seed_schedule and ctrl.rank == 0:
+            # a `--save-best` document, or a bare schedule (JSON array of ops)
+            seeds = []
+            for path in a.seed_schedule:
+                with open(path) as f:
+                    doc = json.load(f)
+                sched = doc["schedule"] if isinstance(doc, dict) else doc
+                seeds.append(tz.OpIndex(g).sequence_from_json(json.dumps(sched)))
+            o.seed_schedules = seeds
         if a.checkpoint:
             o.checkpoint_path = a.checkpoint
             o.checkpoint_every = 10
@@ -336,6 +345,9 @@ def _parser() -> argparse.ArgumentParser:
     s.add_argument("--strategy", default="FastMin")
     s.add_argument("--iters", type=int, default=300)
     s.add_argument("--time-budget", type=float, default=0.0)
+    s.add_argument("--seed-schedule", action="append", default=[],
+                   help="MCTS: measure this schedule (a --save-best document or a JSON array of "
+                        "ops of this workload) before searching; repeatable")
     s.add_argument("--max-tree-nodes", type=int, default=0,
                    help="MCTS: stop once the tree holds this many nodes (0 = unlimited)")
     s.add_argument("--max-seqs", type=int, default=15000)

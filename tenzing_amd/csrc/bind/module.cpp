@@ -513,6 +513,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("n_iters", &MctsOpts::n_iters)
       .def_readwrite("time_budget_s", &MctsOpts::time_budget_s)
       .def_readwrite("max_tree_nodes", &MctsOpts::max_tree_nodes)
+      .def_readwrite("seed_schedules", &MctsOpts::seed_schedules)
       .def_readwrite("expand_rollout", &MctsOpts::expand_rollout)
       .def_readwrite("remove_redundant_syncs", &MctsOpts::remove_redundant_syncs)
       .def_readwrite("reuse_measurements", &MctsOpts::reuse_measurements)
@@ -541,7 +542,8 @@ PYBIND11_MODULE(_tz, m) {
   py::class_<SimResult>(m, "SimResult")
       .def_readonly("seq", &SimResult::seq)
       .def_readonly("res", &SimResult::res)
-      .def_readonly("cached", &SimResult::cached);
+      .def_readonly("cached", &SimResult::cached)
+      .def_readonly("seeded", &SimResult::seeded);
   py::class_<SearchResult>(m, "SearchResult")
       .def_readonly("sims", &SearchResult::sims)
       .def_readonly("wall_s", &SearchResult::wall_s)

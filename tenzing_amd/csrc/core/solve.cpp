@@ -501,6 +501,42 @@ SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &ben
                                             << " results");
   }
 
+  // seed schedules: every rank measures them first (collectively, like any candidate)
+  const int64_t nSeeds = ctrl.bcast_int(root ? int64_t(opts.seed_schedules.size()) : 0, 0);
+  for (int64_t k = 0; k < nSeeds; ++k) {
+    std::string msg;
+    if (root) {
+      const Sequence &s = opts.seed_schedules[size_t(k)];
+      if (opts.verify) {
+        auto v = verify(s, *resolve_graph(*gp, s), plat.n_streams);
+        TZ_CHECK(v.empty(), "seed schedule " << k << " has a race: " << v[0].desc());
+      }
+      msg = s.json(true).dump();
+    }
+    ctrl.bcast(msg, 0);
+    Sequence s = root ? opts.seed_schedules[size_t(k)] : index.sequence_from_json(Json::parse(msg));
+    SimResult sr;
+    sr.seq = s;
+    sr.seeded = true;
+    try {
+      ScopedTimer t(result.counters, "BENCHMARK");
+      sr.res = bench.benchmark(s, opts.bench);
+    } catch (const std::exception &e) {
+      if (!opts.skip_failed || !skippable(e, ctrl)) throw;
+      if (root) {
+        ++result.failed;
+        TZ_LOG(Warn, "seed schedule " << k << " skipped: " << e.what());
+      }
+      continue;
+    }
+    if (root) {
+      cache.emplace(s.canonical_key(), result.sims.size());
+      result.sims.push_back(sr);
+      if (onResult) onResult(result.sims.size() - 1, sr);
+      TZ_LOG(Info, "seed schedule " << k << " pct10=" << sr.res.pct10);
+    }
+  }
+
   std::function<void(int)> dump = [&result](int) { result.dump_csv(std::cout); };
   if (root && opts.trap_signals) register_handler(dump);
 

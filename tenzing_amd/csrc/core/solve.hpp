@@ -30,6 +30,7 @@ struct SimResult {
   Sequence seq;
   BenchResult res;
   bool cached = false;
+  bool seeded = false; // one of MctsOpts::seed_schedules, not found by the search
 };
 
 struct SearchResult {
@@ -104,6 +105,9 @@ struct MctsOpts {
   int64_t checkpoint_every = 0;
   bool trap_signals = false;     // dump partial CSV on SIGINT/SIGTERM/SIGABRT (CLI)
   std::string resume_path;      // resume a checkpointed tree
+  // schedules of this graph to measure before the search (the program's current schedule, a
+  // previous search's best): they count as results, so the search never reports worse
+  std::vector<Sequence> seed_schedules;
   Json json() const;
 };
 

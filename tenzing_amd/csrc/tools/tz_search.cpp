@@ -63,7 +63,8 @@ void usage() {
          "  [--relay auto|off|force] [--relay-fracs F1,F2]\n"
          "  [--ctrl auto|tcp|mpi|self] [--mpi-lib PATH] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
-         "  [--checkpoint PATH] [--resume PATH] [--watchdog S] [--race-ratio R] [--settle-ratio R]\n"
+         "  [--checkpoint PATH] [--resume PATH] [--seed-schedule PATH] [--watchdog S]\n"
+         "  [--race-ratio R] [--settle-ratio R]\n"
          "  [--save-best PATH]      write the best schedule + workload options (JSON)\n"
          "  [--run PATH [--run-iters N] [--run-warmup N]]\n"
          "                          run a saved schedule (this CLI's or python -m tenzing_amd's)\n"
@@ -357,6 +358,15 @@ int main(int argc, char **argv) {
       o.checkpoint_path = a.get("checkpoint", "");
       o.checkpoint_every = o.checkpoint_path.empty() ? 0 : 10;
       o.resume_path = a.get("resume", "");
+      if (a.flag("seed-schedule") && rank == 0) {
+        // a --save-best document or a bare schedule (JSON array of ops of this workload)
+        std::ifstream f(a.get("seed-schedule", ""));
+        TZ_CHECK(f, "cannot open " << a.get("seed-schedule", ""));
+        std::stringstream ss;
+        ss << f.rdbuf();
+        const Json doc = Json::parse(ss.str());
+        o.seed_schedules.push_back(OpIndex(*g).sequence_from_json(doc.is_object() ? doc.at("schedule") : doc));
+      }
       o.bench = bo;
       o.trap_signals = true;
       res = mcts_explore(*g, plat, *bench, *ctrl, o);

@@ -173,3 +173,26 @@ def test_native_save_best_loads_in_python(tmp_path):
     assert doc["args"]["fuse"] == "choice" and doc["args"]["stencil"] is False
     w, g, wl, seq = cli.load_schedule(doc, tz.SelfCtrl(), -1, False)
     assert w.workload == "fused" and w.streams == 3 and len(seq) == len(doc["schedule"])
+
+
+def test_seed_schedule_flag_both_clis(tmp_path):
+    """search --save-best, then a new search seeded with that schedule measures it first (both
+    CLIs read either CLI's document)"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    best = tmp_path / "best.json"
+    r = subprocess.run([sys.executable, "-m", "tenzing_amd", "search", "--workload", "diamond", "--sim",
+                 "--iters", "5", "--save-best", str(best)], cwd=root, capture_output=True, text=True,
+                timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run([sys.executable, "-m", "tenzing_amd", "search", "--workload", "diamond", "--sim",
+                 "--iters", "4", "--seed-schedule", str(best)], cwd=root, capture_output=True,
+                text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["candidates"] == 5
+    exe = os.path.join(root, "tenzing_amd", "bin", "tz-search")
+    if os.path.exists(exe):
+        r = subprocess.run([exe, "--workload", "diamond", "--sim", "--iters", "4", "--seed-schedule",
+                     str(best)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = [ln for ln in r.stderr.splitlines() if ln.startswith('{"best')][-1]
+        assert json.loads(line)["candidates"] == 5

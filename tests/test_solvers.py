@@ -257,3 +257,35 @@ def test_run_refuses_racy_schedules(tz):
             tz.run(g, bad, streams=2, ctrl=tz.SelfCtrl(), device=-1)
     with pytest.raises(RuntimeError, match="no GPU"):
         tz.run(g, doc, streams=2, ctrl=tz.SelfCtrl(), device=-1)
+
+
+def test_seed_schedules_are_measured_first(tz):
+    """MctsOpts.seed_schedules: known schedules (the program's current one, a previous best) are
+    benchmarked before the search and count as results; a racy seed is refused"""
+    def _opts(n):
+        o = tz.MctsOpts()
+        o.n_iters = n
+        o.bench = tz.BenchOpts(n_iters=2)
+        return o
+
+    g = diamond(tz)
+    first = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), _opts(6))
+    seed = first.sims[first.best()].seq
+    o = _opts(5)
+    o.seed_schedules = [tz.OpIndex(g).sequence_from_json(seed.json(True))]
+    r = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), o)
+    assert r.sims[0].seeded and not any(s.seeded for s in r.sims[1:])
+    assert r.sims[0].seq.canonical_key() == seed.canonical_key()
+    assert r.sims[r.best()].res.pct10 <= r.sims[0].res.pct10
+    # a schedule with a missing sync is refused before anything runs
+    ng = g.clone()
+    ng.normalize()
+    ops = {n: ng.op(ng.find(n)) for n in ("k1", "k2", "k3", "k4")}
+    bad = tz.Sequence()
+    bad.append(tz.Start())
+    for n, st in (("k1", 0), ("k2", 1), ("k3", 0), ("k4", 0)):
+        bad.append(tz.BoundGpuOp(ops[n], st))
+    bad.append(tz.Finish())
+    o.seed_schedules = [bad]
+    with pytest.raises(Exception, match="race"):
+        tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), o)
