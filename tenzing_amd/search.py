@@ -22,7 +22,7 @@ def search(graph, streams: int = 2, solver: str = "mcts", iters: int = 100,
            settle_ratio: float = 0.0,
            max_seqs: int = -1, sim: bool = False, replay: str = "", ctrl=None,
            device: int | None = None, seed: int = 0, time_budget_s: float = 0.0,
-           watchdog_s: float = 0.0, symmetric_streams: bool = True):
+           watchdog_s: float = 0.0, symmetric_streams: bool = True, seeds=()):
     """Search the schedules of ``graph`` on ``streams`` streams and return the SearchResult.
 
     solver: "mcts" (``iters`` iterations, ``strategy``) or "dfs" (up to ``max_seqs``
@@ -30,7 +30,8 @@ def search(graph, streams: int = 2, solver: str = "mcts", iters: int = 100,
     with ``graph_unroll`` iterations per launch; "eager"), with the discrete-event model
     (``sim``) or from a results CSV (``replay``). ``ctrl``: the control plane (default: this
     process alone, or every rank when launched by torchrun); ``device``: the GPU (default: the
-    local rank's)."""
+    local rank's). ``seeds``: schedules (Sequence or its JSON) measured before an MCTS search;
+    they count as results (``seeded``), so the best is never worse than them."""
     if solver not in ("mcts", "dfs"):
         raise ValueError("solver must be 'mcts' or 'dfs'")
     if mode not in ("graph", "eager"):
@@ -70,6 +71,10 @@ def search(graph, streams: int = 2, solver: str = "mcts", iters: int = 100,
         o.seed = seed
         o.time_budget_s = time_budget_s
         o.bench = bo
+        if seeds:
+            idx = _tz.OpIndex(graph)
+            o.seed_schedules = [s if isinstance(s, _tz.Sequence) else idx.sequence_from_json(s)
+                                for s in seeds]
         res = _tz.mcts_explore(graph, plat, bench, ctrl, o)
     del bench, rt  # the runtime (and its streams) goes before the caller's tensors
     return res

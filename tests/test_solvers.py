@@ -289,3 +289,6 @@ def test_seed_schedules_are_measured_first(tz):
     o.seed_schedules = [bad]
     with pytest.raises(Exception, match="race"):
         tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), o)
+    # the one-call API takes a Sequence or its JSON
+    r = tz.search(g, streams=2, iters=3, sim=True, seeds=[seed.json(True)], ctrl=tz.SelfCtrl())
+    assert r.sims[0].seeded and len(r.sims) == 4
