@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--orders", default="qxyz,xyzq")
+    ap.add_argument("--zcs", default="32,64", help="z-chunk lengths to sweep (16, 32, 64)")
+    ap.add_argument("--pfs", default="1,2")
+    ap.add_argument("--dbs", default="1,0")
     a = ap.parse_args()
     n, nq, g = a.n, 3, 3
     st = torch.cuda.current_stream().cuda_stream
@@ -39,8 +42,8 @@ def main():
         O = torch.empty_like(G)
         base = g * sz + g * sy + x0
         nbytes = 2 * 8 * n ** 3 * nq
-        configs = [(True, ty, zc, pf, db) for ty in (8, 16) for zc in (32, 64) for pf in (1, 2)
-                   for db in (True, False)]
+        configs = [(True, ty, int(zc), int(pf), db == "1") for ty in (8, 16)
+                   for zc in a.zcs.split(",") for pf in a.pfs.split(",") for db in a.dbs.split(",")]
         configs += [(False, 8, 32, 1, False)]
         # roof: torch's contiguous copy of the whole padded grid (read + write every element)
         for _ in range(3):

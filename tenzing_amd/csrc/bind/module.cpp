@@ -916,11 +916,14 @@ PYBIND11_MODULE(_tz, m) {
      py::arg("nouter"), py::arg("sy"), py::arg("sz"), py::arg("so"), py::arg("xs"),
      py::arg("c0") = 0.4, py::arg("c1") = 0.1, py::arg("lds") = true, py::arg("stream") = 0);
   k.def("set_stencil_tuning", [](int ty, int zc, int pf, bool db) {
+    TZ_CHECK(ty == 8 || ty == 16, "stencil ty must be 8 or 16");
+    TZ_CHECK(zc == 16 || zc == 32 || zc == 64, "stencil zc must be 16, 32 or 64");
+    TZ_CHECK(pf == 1 || pf == 2, "stencil pf must be 1 or 2");
     kern::stencil_tuning().ty = ty;
     kern::stencil_tuning().zc = zc;
     kern::stencil_tuning().pf = pf;
     kern::stencil_tuning().db = db;
-  }, py::arg("ty") = 16, py::arg("zc") = 64, py::arg("pf") = 1, py::arg("db") = true);
+  }, py::arg("ty") = 16, py::arg("zc") = 16, py::arg("pf") = 1, py::arg("db") = true);
   k.def("gather_f32", [](int n, uintptr_t src, uintptr_t idx, uintptr_t dst, uintptr_t s) {
     kern::gather_f32(n, reinterpret_cast<const float *>(src), reinterpret_cast<const int32_t *>(idx),
                      reinterpret_cast<float *>(dst), P(s));

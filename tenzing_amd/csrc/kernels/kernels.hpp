@@ -164,8 +164,10 @@ struct StencilBox {
 };
 /// stencil launch shape: rows per workgroup tile (4, 8, 16) and planes per z chunk (32, 64)
 struct StencilTuning {
-  int ty = 16; // 64 x 16 tiles, 64-plane chunks: 4.2 TB/s at 512^3 x 3 (scripts/stencil_bench.py)
-  int zc = 64;
+  int ty = 16; // 64 x 16 tiles (scripts/stencil_bench.py)
+  // 16-plane chunks: 4x the workgroups of 64-plane chunks for two extra planes read per chunk;
+  // 1580 vs 1620 us at 512^3 x 3 (profiles/r2_move_shape/stencil_zc.jsonl)
+  int zc = 16;
   int pf = 1;  // planes in flight beyond z + 1 (1 or 2)
   bool db = true; // double-buffered LDS tile (one barrier per plane instead of two)
 };

@@ -281,6 +281,9 @@ void launch_zc(const StencilBox &b, hipStream_t s) {
   if (t.zc == 64) {
     if (t.pf >= 2) launch_stencil<LDS, VX, TY, 64, 2>(b, s);
     else launch_stencil<LDS, VX, TY, 64, 1>(b, s);
+  } else if (t.zc == 16) {
+    if (t.pf >= 2) launch_stencil<LDS, VX, TY, 16, 2>(b, s);
+    else launch_stencil<LDS, VX, TY, 16, 1>(b, s);
   } else {
     if (t.pf >= 2) launch_stencil<LDS, VX, TY, 32, 2>(b, s);
     else launch_stencil<LDS, VX, TY, 32, 1>(b, s);

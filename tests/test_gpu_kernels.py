@@ -157,7 +157,7 @@ def test_vector_kernels(tz, gpu):
     assert torch.equal(io, 3.0 + 0.5 * torch.arange(1000, dtype=torch.float64, device="cuda"))
 
 
-@pytest.fixture(params=[(16, 64, 1), (8, 32, 2), (16, 32, 2)], ids=lambda t: "ty%d-zc%d-pf%d" % t)
+@pytest.fixture(params=[(16, 16, 1), (16, 64, 1), (8, 32, 2), (16, 16, 2)], ids=lambda t: "ty%d-zc%d-pf%d" % t)
 def stencil_tuning(tz, request):
     """kernel tilings (rows per tile, planes per chunk, planes in flight); restores the default"""
     tz._tz.kernels.set_stencil_tuning(*request.param)
