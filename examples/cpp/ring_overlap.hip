@@ -13,9 +13,11 @@
 //
 //   tenzing_amd/bin/tz-example-ring                                    # 1 rank (self exchange)
 //   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 --no-python tenzing_amd/bin/tz-example-ring
+//   mpirun -n 8 tenzing_amd/bin/tz-example-ring                        # as the reference's drivers
 //
-// Ranks come from RANK / WORLD_SIZE / LOCAL_RANK; rank 0 publishes its control-plane port in
-// /tmp/tz_ring_<MASTER_PORT>. Built by `python -m tenzing_amd._build` against
+// Under torchrun, ranks come from RANK / WORLD_SIZE / LOCAL_RANK and rank 0 publishes its
+// control-plane port in /tmp/tz_ring_<MASTER_PORT>; under an MPI launcher the control plane is
+// MPI_COMM_WORLD. Built by `python -m tenzing_amd._build` against
 // build/libtenzing_amd.a.
 #include "core/solve.hpp"
 #include "hip/comm_ops.hpp"
@@ -89,12 +91,16 @@ private:
 } // namespace
 
 int main() {
-  const int rank = env_int("RANK", 0), size = env_int("WORLD_SIZE", 1);
-  const int local = env_int("LOCAL_RANK", rank);
-  tz::log_rank() = rank;
+  int rank = env_int("RANK", 0), size = env_int("WORLD_SIZE", 1);
+  int local = env_int("LOCAL_RANK", rank);
   try {
     std::shared_ptr<tz::Ctrl> ctrl;
-    if (size > 1) {
+    if (!std::getenv("WORLD_SIZE") && tz::MpiCtrl::launched()) {
+      ctrl = std::make_shared<tz::MpiCtrl>();
+      rank = ctrl->rank();
+      size = ctrl->size();
+      local = tz::MpiCtrl::launcher_local_rank() >= 0 ? tz::MpiCtrl::launcher_local_rank() : rank;
+    } else if (size > 1) {
       auto t = std::make_shared<tz::TcpCtrl>(rank, size);
       const char *port = std::getenv("MASTER_PORT");
       t->rendezvous_file(std::string("/tmp/tz_ring_") + (port ? port : "default"),
@@ -103,6 +109,7 @@ int main() {
     } else {
       ctrl = std::make_shared<tz::SelfCtrl>();
     }
+    tz::log_rank() = rank;
     const int ndev = tz::hip_device_count();
     TZ_CHECK(ndev > 0, "no GPU visible");
     const int device = local % ndev;
