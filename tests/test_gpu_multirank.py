@@ -164,6 +164,27 @@ def test_bench_two_ranks_under_mpiexec(gpu):
     assert j["config"]["rank_grid"] == [1, 1, 2] and j["mcts_candidates"] == 6
 
 
+def test_native_cli_two_ranks_under_mpiexec(gpu):
+    """tz-search started by mpiexec (no torchrun): MPI control plane, IPC puts between the two
+    loopback ranks, a collective search and the final check of the best schedule"""
+    import shutil
+
+    mpiexec = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
+    exe = os.path.join(ROOT, "tenzing_amd", "bin", "tz-search")
+    if not os.path.exists(mpiexec) or not os.path.exists(exe):
+        pytest.skip("no MPI launcher or tz-search")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([mpiexec, "-n", "2", exe, "--workload", "halo", "--halo-n", "48",
+                        "--neighbors", "26", "--transport", "ipc", "--iters", "6", "--streams", "2",
+                        "--bench-iters", "3", "--target-secs", "0.001"],
+                       cwd="/tmp", capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    line = [x for x in r.stderr.splitlines() if x.startswith('{"best')][-1]
+    j = json.loads(line)
+    assert j["ranks"] == 2 and j["candidates"] == 6
+
+
 @pytest.mark.parametrize("world,case", [(2, "spmv"), (4, "spmv"), (8, "spmv"), (2, "fused")])
 def test_spmv_ipc_loopback(gpu, world, case):
     """distributed SpMV (and SpMV + halo in one graph, BASELINE config 5) on several ranks of
