@@ -881,11 +881,6 @@ PYBIND11_MODULE(_tz, m) {
                    reinterpret_cast<float *>(y), lanes, acc, P(s));
   }, py::arg("n_rows"), py::arg("row_ptr"), py::arg("col_ind"), py::arg("val"), py::arg("x"), py::arg("y"),
      py::arg("lanes") = 0, py::arg("accumulate") = false, py::arg("stream") = 0);
-  k.def("set_spmv_rows", [](int r) {
-    TZ_CHECK(r == 1 || r == 2 || r == 4, "rows per lane group must be 1, 2 or 4");
-    kern::spmv_rows_per_group() = r;
-  }, py::arg("rows"));
-  k.def("get_spmv_rows", []() { return kern::spmv_rows_per_group(); });
   py::class_<RocsparseCsr, std::shared_ptr<RocsparseCsr>>(
       k, "RocsparseCsr", "rocSPARSE CSR SpMV (library comparison variant): y = A x on raw pointers")
       .def(py::init([](int64_t m, int64_t n, int64_t nnz, uintptr_t rp, uintptr_t ci, uintptr_t v,

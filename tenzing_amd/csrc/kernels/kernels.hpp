@@ -123,9 +123,6 @@ void copy_many(const CopyDesc *d, int n, void *stream);
 /// reduction). When `accumulate`, y[r] += ... instead.
 void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,
               const float *x, float *y, int lanesPerRow, bool accumulate, void *stream);
-/// rows per W-lane group of the lanes-per-row CSR kernels (1, 2 or 4; env TZ_SPMV_ROWS): with
-/// more than one, each group keeps the loads of that many rows in flight
-int &spmv_rows_per_group();
 /// dst[i] = src[idx[i]]
 void gather_f32(int n, const float *src, const int32_t *idx, float *dst, void *stream);
 /// one peer's part of an IPC put of the SpMV x halo: dst[i] = src[idx[off + i]], i < n, then

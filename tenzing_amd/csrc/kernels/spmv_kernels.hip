@@ -16,7 +16,6 @@
 #include "kernels.hpp"
 
 #include <algorithm>
-#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -50,54 +49,6 @@ __global__ __launch_bounds__(kThreads) void csr_spmv_k(int nRows, const int32_t 
 #pragma unroll
   for (int off = W / 2; off > 0; off >>= 1) sum += __shfl_xor(sum, off, W);
   if (lane == 0) y[row] = accumulate ? y[row] + sum : sum;
-}
-
-// R rows per W-lane group (rows g, g + G, ..., G = number of groups): the group issues the
-// column/value loads and the x gathers of all R rows before it reduces any of them, so each
-// wave keeps R times the loads in flight. The plain kernel above is latency bound at the
-// reference's sizes (three dependent loads per row, only ~2 waves of rows per CU slot).
-template <int W, int R>
-__global__ __launch_bounds__(kThreads) void csr_spmv_multi_k(int nRows, const int32_t *__restrict__ rowPtr,
-                                                             const int32_t *__restrict__ colInd,
-                                                             const float *__restrict__ val,
-                                                             const float *__restrict__ x,
-                                                             float *__restrict__ y, int accumulate) {
-  const int gtid = blockIdx.x * kThreads + threadIdx.x;
-  const int group = gtid / W, lane = gtid & (W - 1);
-  const int ngroups = int(gridDim.x) * (kThreads / W);
-  int b[R], e[R];
-  int len = 0;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int row = group + r * ngroups;
-    b[r] = row < nRows ? rowPtr[row] : 0;
-    e[r] = row < nRows ? rowPtr[row + 1] : 0;
-    len = max(len, e[r] - b[r]);
-  }
-  float sum[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) sum[r] = 0.f;
-  for (int k = lane; k < len; k += W) {
-    int c[R];
-    float v[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int j = b[r] + k;
-      const bool ok = j < e[r];
-      c[r] = ok ? colInd[j] : -1;
-      v[r] = ok ? val[j] : 0.f;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (c[r] >= 0) sum[r] = fmaf(v[r], x[c[r]], sum[r]);
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-#pragma unroll
-    for (int off = W / 2; off > 0; off >>= 1) sum[r] += __shfl_xor(sum[r], off, W);
-    const int row = group + r * ngroups;
-    if (lane == 0 && row < nRows) y[row] = accumulate ? y[row] + sum[r] : sum[r];
-  }
 }
 
 // CSR-stream: a block owns kStreamRows consecutive rows; its nnz range [rowPtr[r0],
@@ -285,15 +236,6 @@ int grid_for(int64_t n, int perThread = 1) {
 
 } // namespace
 
-int &spmv_rows_per_group() {
-  static int r = [] {
-    const char *e = std::getenv("TZ_SPMV_ROWS");
-    const int v = e ? std::atoi(e) : 1;
-    return v == 2 || v == 4 ? v : 1;
-  }();
-  return r;
-}
-
 void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,
               const float *x, float *y, int lanesPerRow, bool accumulate, void *stream) {
   if (nRows <= 0) return;
@@ -307,21 +249,6 @@ void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const flo
   }
   int W = lanesPerRow;
   if (W <= 0) W = 8;
-  const int R = spmv_rows_per_group();
-  if (R > 1 && (W == 4 || W == 8 || W == 16)) {
-    const int64_t groups = (int64_t(nRows) + R - 1) / R;
-    const dim3 g(unsigned((groups * W + kThreads - 1) / kThreads)), b(kThreads);
-    const int acc = accumulate ? 1 : 0;
-#define TZ_MULTI(WW, RR) hipLaunchKernelGGL((csr_spmv_multi_k<WW, RR>), g, b, 0, s, nRows, rowPtr, colInd, val, x, y, acc)
-    if (R == 2) {
-      if (W == 4) TZ_MULTI(4, 2); else if (W == 8) TZ_MULTI(8, 2); else TZ_MULTI(16, 2);
-    } else {
-      if (W == 4) TZ_MULTI(4, 4); else if (W == 8) TZ_MULTI(8, 4); else TZ_MULTI(16, 4);
-    }
-#undef TZ_MULTI
-    TZ_HIP_LAUNCH_CHECK();
-    return;
-  }
   const int64_t threads = int64_t(nRows) * W;
   const dim3 g(unsigned((threads + kThreads - 1) / kThreads)), b(kThreads);
   const int acc = accumulate ? 1 : 0;
