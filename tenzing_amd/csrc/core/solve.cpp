@@ -504,17 +504,25 @@ SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &ben
   // seed schedules: every rank measures them first (collectively, like any candidate)
   const int64_t nSeeds = ctrl.bcast_int(root ? int64_t(opts.seed_schedules.size()) : 0, 0);
   for (int64_t k = 0; k < nSeeds; ++k) {
-    std::string msg;
+    // rank 0 checks the seed; a refusal travels with the broadcast so every rank throws together
+    Json m;
     if (root) {
       const Sequence &s = opts.seed_schedules[size_t(k)];
-      if (opts.verify) {
-        auto v = verify(s, *resolve_graph(*gp, s), plat.n_streams);
-        TZ_CHECK(v.empty(), "seed schedule " << k << " has a race: " << v[0].desc());
+      try {
+        if (opts.verify) {
+          auto v = verify(s, *resolve_graph(*gp, s), plat.n_streams);
+          TZ_CHECK(v.empty(), "seed schedule " << k << " has a race: " << v[0].desc());
+        }
+        m["seq"] = s.json(true);
+      } catch (const std::exception &e) {
+        m["err"] = std::string(e.what());
       }
-      msg = s.json(true).dump();
     }
+    std::string msg = root ? m.dump() : "";
     ctrl.bcast(msg, 0);
-    Sequence s = root ? opts.seed_schedules[size_t(k)] : index.sequence_from_json(Json::parse(msg));
+    m = Json::parse(msg);
+    if (m.contains("err")) TZ_THROW(m.at("err").as_string());
+    Sequence s = root ? opts.seed_schedules[size_t(k)] : index.sequence_from_json(m.at("seq"));
     SimResult sr;
     sr.seq = s;
     sr.seeded = true;

@@ -150,6 +150,35 @@ def body_halo_graph_consistency():
                 coords=list(h.coords()), grid=list(h.rank_grid()))
 
 
+def body_bad_seed():
+    """a racy seed schedule on rank 0: every rank must raise, none may hang in a collective"""
+    import tenzing_amd as tz
+    from tenzing_amd.parallel import init_ctrl
+
+    c = init_ctrl(timeout_s=60)
+    g = _diamond()
+    o = tz.MctsOpts()
+    o.n_iters = 3
+    o.bench = tz.BenchOpts(n_iters=2)
+    if c.rank == 0:
+        ng = g.clone()
+        ng.normalize()
+        ops = {n: ng.op(ng.find(n)) for n in ("k1", "k2", "k3", "k4")}
+        bad = tz.Sequence()
+        bad.append(tz.Start())
+        for n, st in (("k1", 0), ("k2", 1), ("k3", 0), ("k4", 0)):
+            bad.append(tz.BoundGpuOp(ops[n], st))
+        bad.append(tz.Finish())
+        o.seed_schedules = [bad]
+    try:
+        tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), c, o)
+        err = ""
+    except Exception as e:  # noqa: BLE001
+        err = str(e)
+    c.barrier()  # both ranks got here: nobody hangs
+    return dict(rank=c.rank, err=err)
+
+
 # ---------------------------------------------------------------- tests
 
 def test_ctrl_collectives(tmp_path):
@@ -275,3 +304,8 @@ def body_racing_two_ranks():
 def test_racing_is_collective(tmp_path):
     rs = _run("body_racing_two_ranks", 2, tmp_path)
     assert rs[0]["n"] == 3 and rs[0]["raced"] == rs[1]["raced"] == 2
+
+
+def test_bad_seed_schedule_fails_on_every_rank(tmp_path):
+    rs = _run("body_bad_seed", 2, tmp_path)
+    assert all("race" in r["err"] for r in rs), rs
