@@ -553,6 +553,11 @@ PYBIND11_MODULE(_tz, m) {
       .def_readonly("failed", &SearchResult::failed)
       .def("best", &SearchResult::best)
       .def("counters", [](const SearchResult &r) { return counters_dict(r.counters); })
+      .def("counter_counts", [](const SearchResult &r) {
+        py::dict d;
+        for (const auto &kv : r.counters.counts) d[py::str(kv.first)] = kv.second;
+        return d;
+      }, "how often each counter was hit (phases; SEED_IN_TREE: seeds placed in the tree)")
       .def("dump_csv", [](const SearchResult &r) {
         std::ostringstream ss;
         r.dump_csv(ss);

@@ -418,6 +418,115 @@ struct Tree {
   }
 };
 
+// every op name inside `op`: itself, a compound's sub-graph, a choice's alternatives
+void op_names(const OpPtr &op, std::unordered_set<std::string> &out) {
+  out.insert(op->name());
+  if (op->op_class() == OpClass::Compound) {
+    auto g = static_cast<const CompoundOp &>(*op).graph();
+    for (int v : g->vertices()) op_names(g->op(v), out);
+  } else if (op->op_class() == OpClass::Choice) {
+    for (const auto &c : static_cast<const ChoiceOp &>(*op).choices()) op_names(c, out);
+  }
+}
+
+// The tree path of a seed schedule, so that its measurement steers the search like any
+// rollout's. Descends from the root taking, at every state, the decision that agrees with the
+// seed: an Expand; a Choose whose alternative holds ops of the seed; an Assign of a pending op to
+// the stream the seed uses for it (seed streams relabeled consistently); then, by the seed's
+// next entry: for a sync, the offered sync of the same kind on the same stream, or none (the
+// state does not need it); for a graph op its Execute, else a sync the state requires (one the
+// seed dropped as redundant). The path is accepted when the descent's schedule, after the
+// seed's redundant-sync removal, is equivalent to the seed. Returns the terminal leaf or nullptr.
+MctsNode *seed_path(Tree &tree, const State &rootState, const Sequence &seed, bool removeRedundant,
+                    int nStreams) {
+  std::unordered_map<std::string, int> streamOf; // the seed's stream of each bound GPU op
+  std::unordered_set<std::string> names;
+  for (const auto &e : seed.entries) {
+    const OpClass c = e.op->op_class();
+    if (c == OpClass::Sync) continue;
+    names.insert(e.op->name());
+    if (c == OpClass::BoundGpu) streamOf[e.op->name()] = static_cast<const BoundGpuOp &>(*e.op).stream();
+  }
+  auto sync_stream = [](const BoundOp &op) {
+    const Json j = op.json();
+    return j.contains("stream") ? int(j.at("stream").as_int()) : -1;
+  };
+  std::unordered_map<int, int> relabel; // seed stream -> state stream
+  State st = rootState;
+  MctsNode *cur = &tree.root;
+  size_t pos = 0;
+  while (pos < seed.size() && seed[pos]->op_class() == OpClass::Start) ++pos;
+  for (int guard = 0; !st.complete(); ++guard) {
+    if (guard > 1000000) return nullptr;
+    tree.ensure_children(*cur, st);
+    const auto &ch = cur->children;
+    int pick = -1;
+    bool advance = false;
+    for (size_t i = 0; i < ch.size() && pick < 0; ++i)
+      if (ch[i]->decision.kind == Decision::Kind::Expand) pick = int(i);
+    for (size_t i = 0; i < ch.size() && pick < 0; ++i) {
+      const Decision &d = ch[i]->decision;
+      if (d.kind != Decision::Kind::Choose) continue;
+      const auto alts = static_cast<const ChoiceOp &>(*st.graph().op(d.node)).choices();
+      std::unordered_set<std::string> in;
+      op_names(alts[size_t(d.choice)], in);
+      for (const auto &n : in)
+        if (names.count(n)) {
+          pick = int(i);
+          break;
+        }
+    }
+    for (size_t i = 0; i < ch.size() && pick < 0; ++i) {
+      const Decision &d = ch[i]->decision;
+      if (d.kind != Decision::Kind::Assign) continue;
+      auto it = streamOf.find(st.graph().op(d.node)->name());
+      if (it == streamOf.end()) continue;
+      auto m = relabel.find(it->second);
+      bool taken = false;
+      for (const auto &kv : relabel) taken = taken || kv.second == d.stream;
+      if ((m != relabel.end() && m->second == d.stream) || (m == relabel.end() && !taken)) {
+        relabel[it->second] = d.stream;
+        pick = int(i);
+      }
+    }
+    if (pick < 0 && pos < seed.size() && seed[pos]->op_class() == OpClass::Sync) {
+      const BoundOp &want = *seed[pos];
+      const int ws = sync_stream(want);
+      auto m = relabel.find(ws);
+      for (size_t i = 0; i < ch.size() && pick < 0; ++i) {
+        const Decision &d = ch[i]->decision;
+        if (d.kind != Decision::Kind::Execute || d.op->op_class() != OpClass::Sync || d.op->kind() != want.kind())
+          continue;
+        if (ws < 0 || (m != relabel.end() && m->second == sync_stream(*d.op))) pick = int(i);
+      }
+      ++pos; // taken, or a sync this state does not need
+      if (pick < 0) continue;
+    }
+    if (pick < 0 && pos < seed.size()) {
+      for (size_t i = 0; i < ch.size() && pick < 0; ++i) {
+        const Decision &d = ch[i]->decision;
+        if (d.kind == Decision::Kind::Execute && d.op->op_class() != OpClass::Sync &&
+            d.op->name() == seed[pos]->name()) {
+          pick = int(i);
+          advance = true;
+        }
+      }
+    }
+    for (size_t i = 0; i < ch.size() && pick < 0; ++i) {
+      const Decision &d = ch[i]->decision;
+      if (d.kind == Decision::Kind::Execute && d.op->op_class() == OpClass::Sync) pick = int(i);
+    }
+    if (pick < 0) return nullptr;
+    if (advance) ++pos;
+    st.apply_inplace(ch[size_t(pick)]->decision);
+    cur = ch[size_t(pick)].get();
+  }
+  tree.ensure_children(*cur, st); // terminal: expanded without children
+  Sequence s = st.sequence();
+  if (removeRedundant) remove_redundant_syncs(s, st.graph(), nStreams);
+  return s.canonical_key() == seed.canonical_key() ? cur : nullptr;
+}
+
 void graphviz_rec(const MctsNode &node, const Strategy &strat, std::ostream &os, size_t &count,
                   size_t maxNodes, const std::string &id) {
   std::string color = node.fully_visited ? "green" : "black";
@@ -541,7 +650,14 @@ SearchResult mcts_explore(const Graph &g, const Platform &plat, Benchmarker &ben
       cache.emplace(s.canonical_key(), result.sims.size());
       result.sims.push_back(sr);
       if (onResult) onResult(result.sims.size() - 1, sr);
-      TZ_LOG(Info, "seed schedule " << k << " pct10=" << sr.res.pct10);
+      // its result steers the search from where the seed sits in the tree
+      MctsNode *leaf = seed_path(tree, rootState, s, opts.remove_redundant_syncs, plat.n_streams);
+      if (leaf) {
+        tree.backprop(leaf, sr.res);
+        result.counters.add("SEED_IN_TREE", 0.0);
+      }
+      TZ_LOG(Info, "seed schedule " << k << " pct10=" << sr.res.pct10
+                                    << (leaf ? " (in the tree)" : " (no tree path)"));
     }
   }
 

@@ -292,3 +292,44 @@ def test_seed_schedules_are_measured_first(tz):
     # the one-call API takes a Sequence or its JSON
     r = tz.search(g, streams=2, iters=3, sim=True, seeds=[seed.json(True)], ctrl=tz.SelfCtrl())
     assert r.sims[0].seeded and len(r.sims) == 4
+
+
+def _choice_compound_graph(tz):
+    sub = tz.Graph()
+    x = tz.SimGpuOp("x", 5)
+    ch = tz.StaticChoiceOp("y", [tz.SimGpuOp("y_slow", 50), tz.SimGpuOp("y_fast", 5)])
+    sub.start_then(x)
+    sub.then(x, ch)
+    sub.then_finish(ch)
+    g = tz.Graph()
+    comp = tz.StaticCompoundOp("comp", sub)
+    w = tz.SimGpuOp("w", 30)
+    g.start_then(comp)
+    g.start_then(w)
+    g.then_finish(comp)
+    g.then_finish(w)
+    return g
+
+
+@pytest.mark.parametrize("which,streams", [("diamond", 2), ("diamond", 3), ("diamond", 4),
+                                           ("choice", 2), ("choice", 3)])
+def test_seed_schedules_join_the_tree(tz, which, streams):
+    """a seed's measurement is backpropagated along the tree path that produces it (through
+    stream assignments, compound expansion and choices), for any schedule of the graph"""
+    g = diamond(tz) if which == "diamond" else _choice_compound_graph(tz)
+    ng = g.clone()
+    ng.normalize()
+    seeds = []
+    for k in range(12):
+        s = tz.random_rollout(tz.State(g, tz.Platform(streams)), k)
+        s, _ = tz.remove_redundant_syncs(s, tz.resolve_graph(g, s), streams)
+        seeds.append(s)
+    o = tz.MctsOpts()
+    o.n_iters = 2
+    o.bench = tz.BenchOpts(n_iters=2)
+    o.seed_schedules = seeds
+    r = tz.mcts_explore(g, tz.Platform(streams), tz.SimBenchmarker(streams), tz.SelfCtrl(), o)
+    assert sum(s.seeded for s in r.sims) == len(seeds)
+    # every distinct seed found its path (equal seeds share one result and one path)
+    distinct = len({s.canonical_key() for s in seeds})
+    assert r.counter_counts()["SEED_IN_TREE"] >= distinct
