@@ -351,6 +351,30 @@ TEST(mcts_large_tree_stops) {
   CHECK(!r.sims.empty());
 }
 
+TEST(mcts_seed_schedules_join_the_tree) {
+  auto g = diamond(10, 100, 100, 10);
+  auto gp = std::make_shared<Graph>(*g);
+  gp->normalize();
+  std::mt19937_64 rng(7);
+  MctsOpts o;
+  o.n_iters = 2;
+  o.bench.n_iters = 2;
+  std::set<std::string> keys;
+  for (int k = 0; k < 10; ++k) {
+    Sequence s = random_rollout(State(gp, Platform::make_n_streams(3)), rng);
+    remove_redundant_syncs(s, *resolve_graph(*gp, s), 3);
+    keys.insert(s.canonical_key());
+    o.seed_schedules.push_back(s);
+  }
+  SimBenchmarker sb(3, SimParams());
+  SelfCtrl ctrl;
+  SearchResult r = mcts_explore(*g, Platform::make_n_streams(3), sb, ctrl, o);
+  size_t seeded = 0;
+  for (const auto &s : r.sims) seeded += s.seeded;
+  CHECK(seeded == o.seed_schedules.size());
+  CHECK(r.counters.counts.count("SEED_IN_TREE") && r.counters.counts.at("SEED_IN_TREE") >= keys.size());
+}
+
 TEST(mcts_full_tree_stops) {
   auto g = std::make_shared<Graph>();
   auto a = std::make_shared<NoOp>("a"), b = std::make_shared<NoOp>("b");
