@@ -54,6 +54,7 @@ void SearchResult::dump_jsonl(std::ostream &os) const {
     j["i"] = int64_t(i);
     j["result"] = sims[i].res.json();
     j["cached"] = sims[i].cached;
+    if (sims[i].seeded) j["seeded"] = true;
     j["seq"] = sims[i].seq.json();
     os << j.dump() << "\n";
   }

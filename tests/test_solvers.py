@@ -275,6 +275,8 @@ def test_seed_schedules_are_measured_first(tz):
     o.seed_schedules = [tz.OpIndex(g).sequence_from_json(seed.json(True))]
     r = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), tz.SelfCtrl(), o)
     assert r.sims[0].seeded and not any(s.seeded for s in r.sims[1:])
+    rows = [json.loads(ln) for ln in r.dump_jsonl().splitlines()]
+    assert rows[0].get("seeded") is True and "seeded" not in rows[1]
     assert r.sims[0].seq.canonical_key() == seed.canonical_key()
     assert r.sims[r.best()].res.pct10 <= r.sims[0].res.pct10
     # a schedule with a missing sync is refused before anything runs
