@@ -1,9 +1,9 @@
 """Do parallel branches of a hipGraph still overlap when its nodes are child graphs?
 
 Two independent busy kernels (one workgroup each, ~200 us) on two streams, compiled into a
-hipGraph by the runtime with every op captured straight into the graph (TZ_GRAPH_CHILD=0) or as
-child graphs (TZ_GRAPH_CHILD=1; the env is read once per process, so run this script once per
-setting). Prints one JSON line: per-iteration time and the serial time of one kernel."""
+hipGraph by the runtime in one whole-schedule capture (TZ_GRAPH_CAPTURE=schedule, the default) or
+as child graphs (TZ_GRAPH_CAPTURE=child; the env is read once per process, so run this script once
+per setting). Prints one JSON line: per-iteration time and the serial time of one kernel."""
 import json
 import os
 import sys
@@ -37,7 +37,7 @@ def main():
     rt.run(n)
     rt.device_sync()
     dt = (time.perf_counter() - t0) / n
-    print(json.dumps({"child": os.environ.get("TZ_GRAPH_CHILD", "rccl"), "mode": str(rt.effective_mode),
+    print(json.dumps({"capture": os.environ.get("TZ_GRAPH_CAPTURE", "schedule"), "nodes": rt.graph_nodes, "mode": str(rt.effective_mode),
                       "iter_us": dt * 1e6, "one_kernel_us": us}))
 
 

@@ -196,6 +196,14 @@ PYBIND11_MODULE(_tz, m) {
     return std::string(buf);
   });
   m.def("rccl_version", &RcclComm::version);
+  m.def("hip_runtime_version", [] {
+    int v = 0;
+    return hipRuntimeGetVersion(&v) == hipSuccess ? v : -1;
+  }, "HIP_VERSION of the libamdhip64 this process actually uses (major*1e7 + minor*1e5 + patch)");
+  m.def("hip_driver_version", [] {
+    int v = 0;
+    return hipDriverGetVersion(&v) == hipSuccess ? v : -1;
+  });
   m.def("rccl_unique_id", [] { return py::bytes(RcclComm::unique_id()); },
         "a fresh ncclUniqueId as bytes");
   m.def("strategy_names", &strategy_names);
@@ -518,6 +526,9 @@ PYBIND11_MODULE(_tz, m) {
       .def("listen", &TcpCtrl::listen, py::arg("port") = 0, py::arg("bind_addr") = "0.0.0.0")
       .def("connect", &TcpCtrl::connect, py::arg("host"), py::arg("port"), py::arg("timeout_s") = 300.0,
            py::call_guard<py::gil_scoped_release>())
+      .def("rendezvous", &TcpCtrl::rendezvous, py::arg("host"), py::arg("port"),
+           py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>(),
+           "rank 0 listens on `port`, the others connect (handshake-checked): no store, no torch")
       .def("rendezvous_file", &TcpCtrl::rendezvous_file, py::arg("path"), py::arg("host") = "127.0.0.1",
            py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>());
   py::class_<MpiCtrl, Ctrl, std::shared_ptr<MpiCtrl>>(m, "MpiCtrl")

@@ -8,7 +8,9 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <sys/select.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <thread>
 #include <unistd.h>
 
@@ -119,24 +121,65 @@ int TcpCtrl::listen(int port, const std::string &bindAddr) {
   return ntohs(addr.sin_port);
 }
 
+namespace {
+constexpr uint32_t kHello = 0x545a4331; // "TZC1": a peer rank's first frame
+constexpr uint32_t kWelcome = 0x545a4f4b; // "TZOK": rank 0's release
+struct Hello {
+  uint32_t magic;
+  int32_t size, rank;
+};
+} // namespace
+
 void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
   if (size_ == 1) return;
   if (rank_ == 0) {
     TZ_CHECK(listenFd_ >= 0, "rank 0 must listen() before connect()");
-    for (int i = 1; i < size_; ++i) {
+    const double t0 = wtime();
+    for (int joined = 1; joined < size_;) {
+      // bounded: a rank that never comes must not leave rank 0 blocked in accept() forever
+      timeval tv{};
+      const double left = timeoutS - (wtime() - t0);
+      TZ_CHECK(left > 0, "ctrl rendezvous: " << (size_ - joined) << " of " << size_ - 1
+                                              << " ranks did not connect within " << timeoutS << " s");
+      tv.tv_sec = long(left);
+      tv.tv_usec = long((left - double(tv.tv_sec)) * 1e6);
+      fd_set rd;
+      FD_ZERO(&rd);
+      FD_SET(listenFd_, &rd);
+      const int sel = ::select(listenFd_ + 1, &rd, nullptr, nullptr, &tv);
+      if (sel < 0 && errno == EINTR) continue;
+      TZ_CHECK(sel >= 0, "select: " << std::strerror(errno));
+      if (sel == 0) continue; // timed out: the check above reports it
       int fd = ::accept(listenFd_, nullptr, nullptr);
       TZ_CHECK(fd >= 0, "accept: " << std::strerror(errno));
       nodelay(fd);
-      int32_t r = -1;
-      recv_all(fd, &r, sizeof(r));
-      TZ_CHECK(r > 0 && r < size_ && peers_[r] < 0, "bad or duplicate peer rank " << r);
-      peers_[r] = fd;
+      // a connection that does not speak the handshake within a second is dropped
+      timeval hs{1, 0};
+      ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &hs, sizeof(hs));
+      Hello h{};
+      try {
+        recv_all(fd, &h, sizeof(h));
+      } catch (const Error &) {
+        h.magic = 0;
+      }
+      timeval none{0, 0};
+      ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
+      if (h.magic != kHello) {
+        ::close(fd);
+        TZ_LOG(Warn, "ctrl rendezvous: dropped a connection without the handshake");
+        continue;
+      }
+      if (h.size != size_ || h.rank <= 0 || h.rank >= size_ || peers_[h.rank] >= 0) {
+        ::close(fd);
+        TZ_THROW("ctrl rendezvous: peer says rank " << h.rank << " of " << h.size << " (this job: "
+                                                    << size_ << " ranks; a duplicate rank or a "
+                                                                "rank of another job?)");
+      }
+      peers_[h.rank] = fd;
+      ++joined;
     }
     // release everyone
-    for (int i = 1; i < size_; ++i) {
-      char c = 1;
-      send_all(peers_[i], &c, 1);
-    }
+    for (int i = 1; i < size_; ++i) send_all(peers_[i], &kWelcome, sizeof(kWelcome));
     return;
   }
   addrinfo hints{}, *res = nullptr;
@@ -159,11 +202,19 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
   }
   ::freeaddrinfo(res);
   nodelay(fd);
-  int32_t r = rank_;
-  send_all(fd, &r, sizeof(r));
-  char c = 0;
-  recv_all(fd, &c, 1);
+  const Hello h{kHello, size_, rank_};
+  send_all(fd, &h, sizeof(h));
+  uint32_t w = 0;
+  recv_all(fd, &w, sizeof(w));
+  TZ_CHECK(w == kWelcome, "ctrl rendezvous: " << host << ":" << port << " is not this job's rank 0");
   peers_[0] = fd;
+}
+
+void TcpCtrl::rendezvous(const std::string &host, int port, double timeoutS) {
+  TZ_CHECK(port > 0 && port < 65536, "ctrl rendezvous port " << port << " out of range");
+  if (size_ == 1) return;
+  if (rank_ == 0) listen(port, "0.0.0.0");
+  connect(host, port, timeoutS);
 }
 
 void TcpCtrl::rendezvous_file(const std::string &path, const std::string &host, double timeoutS) {

@@ -64,6 +64,11 @@ public:
   void connect(const std::string &host, int port, double timeoutS = 300.0);
   /// rank 0 writes its port to `path`; others poll the file (CLI bootstrap without Python)
   void rendezvous_file(const std::string &path, const std::string &host, double timeoutS = 300.0);
+  /// rank 0 listens on `port` of every interface, the others connect to host:port (retrying
+  /// until rank 0 is up): a launcher-style rendezvous with no store and no torch.distributed.
+  /// Every connection carries a handshake (magic, world size, rank), so a stray connection to
+  /// the port is dropped instead of taken for a rank.
+  void rendezvous(const std::string &host, int port, double timeoutS = 300.0);
 
   int rank() const override { return rank_; }
   int size() const override { return size_; }

@@ -81,48 +81,53 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
   kern::abort_flag();
   if (watchdogS_ > 0) {
     watchdog_ = std::thread([this] {
-      // past the deadline: set the device abort flag (spinning kernels give up) and abort the
-      // RCCL communicators (their kernels return), so the run ends and throws, and the
+      // past the deadline: claim the run (one CAS on deadline_: the run's own exchange at its
+      // end and this claim cannot both succeed, so a run that finishes at its deadline is either
+      // aborted or not, never half), set the device abort flag (spinning kernels give up) and
+      // abort the RCCL communicators (their kernels return), so the run ends and throws, and the
       // benchmarker turns that into a collectively skipped candidate; if the run still has not
       // returned after a grace period, nothing can unblock it: exit
       double grace = 0;
       uint64_t firedRun = 0;
       while (!stop_.load()) {
         std::this_thread::sleep_for(std::chrono::milliseconds(100));
-        const double d = deadline_.load();
-        // a new run (or none) since the last firing: start over (the abort may have blocked
-        // this thread across the end of the run it fired for)
-        if (d <= 0 || runGen_.load() != firedRun) grace = 0;
-        if (d <= 0 || wtime() <= d) continue;
-        if (grace == 0) {
-          firedRun = runGen_.load();
-          // counted before anything can end the run, so the run waits for the abort below
-          std::shared_ptr<std::atomic<int>> pending = abortsPending_;
-          ++*pending;
-          // flag first, so the run sees it whenever it returns; the abort itself runs on a
-          // thread of its own: it may block for seconds (it frees device memory, which waits
-          // for the device), and this loop must keep watching the next runs meanwhile
-          aborted_ = true;
-          ++fired_;
-          note_abort();
-          kern::set_abort(true);
-          std::fprintf(stderr,
-                       "[tz] watchdog: a run exceeded its %.1f s budget (floor %.1f s + %.0f x "
-                       "expected %.3g s/iter); aborting the device waits and the RCCL "
-                       "communicators\n",
-                       budget_.load(), watchdogS_, watchdogK_, expected_);
-          std::fflush(stderr);
-          std::thread([pending] {
-            if (rccl_abort_all() > 0)
-              mark_domain_dead("rccl", "the watchdog aborted the RCCL communicators of a hung run");
-            --*pending;
-          }).detach();
-          grace = wtime() + std::max(10.0, watchdogS_);
-        } else if (wtime() > grace) {
-          // the run is stuck where no abort reaches (e.g. a graph node that never completes):
-          // leave, printing the run deadline's partial report (a bench still ends with its line)
-          exit_with_report(3, "watchdog: a hung run did not return after the abort");
+        double d = deadline_.load();
+        if (grace > 0) {
+          // a claimed run: still not returned (kClaimed) or draining after its abort (kDraining)
+          const bool pending = (d == kClaimed || d == kDraining) && runGen_.load() == firedRun;
+          if (!pending) {
+            grace = 0;
+          } else {
+            if (wtime() > grace)
+              // the run is stuck where no abort reaches (e.g. a graph node that never
+              // completes): leave, printing the run deadline's partial report
+              exit_with_report(3, "watchdog: a hung run did not return after the abort");
+            continue;
+          }
         }
+        if (d <= 0 || wtime() <= d) continue;
+        if (!deadline_.compare_exchange_strong(d, kClaimed)) continue; // the run ended meanwhile
+        firedRun = runGen_.load();
+        // counted before anything can end the run, so the run waits for the abort below
+        std::shared_ptr<std::atomic<int>> pending = abortsPending_;
+        ++*pending;
+        ++fired_;
+        note_abort();
+        kern::set_abort(true);
+        std::fprintf(stderr,
+                     "[tz] watchdog: a run exceeded its %.1f s budget (floor %.1f s + %.0f x "
+                     "expected %.3g s/iter); aborting the device waits and the RCCL "
+                     "communicators\n",
+                     budget_.load(), watchdogS_, watchdogK_, expected_.load());
+        std::fflush(stderr);
+        // the abort runs on a thread of its own: it may block for seconds (it frees device
+        // memory, which waits for the device), and this loop must keep watching meanwhile
+        std::thread([pending] {
+          if (rccl_abort_all() > 0)
+            mark_domain_dead("rccl", "the watchdog aborted the RCCL communicators of a hung run");
+          --*pending;
+        }).detach();
+        grace = wtime() + std::max(10.0, watchdogS_);
       }
     });
   }
@@ -277,77 +282,63 @@ void HipRuntime::set_mode(ExecMode m) {
 
 void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut) {
   const int nS = num_streams();
-  hipGraph_t graph = nullptr;
-  TZ_HIP(hipGraphCreate(&graph, 0));
   SyncModel model(nS);
   // per stream, in issue order: the graph nodes that stand for each issued GPU op. An op that
   // enqueued nothing stands for its own dependencies (no empty node: every empty node costs a
-  // barrier packet — ~10 us — at replay), an op that captured a fan-out for all its tails.
-  using NodeSet = std::vector<hipGraphNode_t>;
+  // barrier packet — ~10 us — at replay), an op that enqueued a fan-out for all its tails.
+  using NodeSet = std::vector<void *>;
   std::vector<std::vector<NodeSet>> nodes(nS);
-  // a schedule with RCCL ops between ranks is built from child graphs only (capture_op
-  // explains why); one-rank communicators (self send/recv) stay in flat graphs, which keep
-  // parallel branches concurrent
-  bool rccl = false;
-  for (const auto &e : seq_.entries)
-    if (e.op->op_class() == OpClass::BoundGpu &&
-        static_cast<const BoundGpuOp &>(*e.op).unbound()->order_domain() == "rccl")
-      rccl = true;
-  const bool child = child_capture_domain(rccl && rccl_multi_rank() ? "rccl" : "");
-  size_t edges = 0, real = 0;
-  try {
+  size_t edges = 0;
+  hipGraph_t graph = nullptr;
+  {
+    GraphBuilder gb(streams_, capture_mode());
     // replaying the sequence `iterations` times through one model orders iteration i+1 after
     // iteration i exactly as the schedule's closing host syncs do in eager mode
     for (int it = 0; it < iterations; ++it)
-    for (const auto &e : seq_.entries) {
-      const BoundOp &op = *e.op;
-      if (op.op_class() == OpClass::BoundGpu) {
-        const auto &b = static_cast<const BoundGpuOp &>(op);
-        const int s = b.stream();
-        TZ_CHECK(s >= 0 && s < nS, "stream " << s << " out of range");
-        // dependencies: previous op on this stream + the latest op of every other stream that
-        // the schedule's events / host syncs make complete before this one is issued
-        NodeSet deps;
-        if (!nodes[s].empty()) deps = nodes[s].back();
-        for (int t = 0; t < nS; ++t) {
-          if (t == s) continue;
-          const int k = model.known(s, t);
-          if (k > 0) {
-            const NodeSet &d = nodes[t][size_t(k) - 1];
-            deps.insert(deps.end(), d.begin(), d.end());
+      for (const auto &e : seq_.entries) {
+        const BoundOp &op = *e.op;
+        if (op.op_class() == OpClass::BoundGpu) {
+          const auto &b = static_cast<const BoundGpuOp &>(op);
+          const int s = b.stream();
+          TZ_CHECK(s >= 0 && s < nS, "stream " << s << " out of range");
+          // dependencies: previous op on this stream + the latest op of every other stream that
+          // the schedule's events / host syncs make complete before this one is issued
+          NodeSet deps;
+          if (!nodes[s].empty()) deps = nodes[s].back();
+          for (int t = 0; t < nS; ++t) {
+            if (t == s) continue;
+            const int k = model.known(s, t);
+            if (k > 0) {
+              const NodeSet &d = nodes[t][size_t(k) - 1];
+              deps.insert(deps.end(), d.begin(), d.end());
+            }
+          }
+          std::sort(deps.begin(), deps.end());
+          deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
+          hipStream_t st = S(streams_[s]);
+          NodeSet tails = gb.add(s, deps, [&] { b.unbound()->launch(st, *this); });
+          if (tails.empty()) {
+            nodes[s].push_back(deps); // enqueued nothing: stands for its dependencies
+          } else {
+            nodes[s].push_back(tails);
+            edges += deps.size();
           }
         }
-        std::sort(deps.begin(), deps.end());
-        deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
-        // record the op alone on its own stream, directly into the schedule graph behind its
-        // dependencies (flat graph: no child-graph indirection at replay; schedules with RCCL
-        // ops excepted, see capture_op)
-        hipStream_t st = S(streams_[s]);
-        size_t added = 0;
-        const std::vector<void *> t =
-            capture_op(graph, std::vector<void *>(deps.begin(), deps.end()), st, child,
-                       [&] { b.unbound()->launch(st, *this); }, &added);
-        NodeSet tails;
-        for (void *n : t) tails.push_back(static_cast<hipGraphNode_t>(n));
-        std::sort(tails.begin(), tails.end());
-        if (added == 0) {
-          nodes[s].push_back(deps); // enqueued nothing: stands for its dependencies
-        } else {
-          nodes[s].push_back(tails);
-          real += added;
-          edges += deps.size();
-        }
+        model.apply(op);
       }
-      model.apply(op);
-    }
+    graph = static_cast<hipGraph_t>(gb.finish());
+  }
+  try {
+    size_t real = 0;
+    TZ_HIP(hipGraphGetNodes(graph, nullptr, &real)); // the capture has ended: safe to inspect
     hipGraphExec_t exec = nullptr;
     TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
     graphOf_[exec] = graph; // destroyed with the exec (destroy_exec)
     graph = nullptr;
     nodesOut = real;
     edgesOut = edges;
-    TZ_LOG(Debug, "graph mode: " << iterations << " iteration(s), " << real << " nodes, " << edges
-                                 << " edges");
+    TZ_LOG(Debug, "graph mode (" << capture_mode_name(capture_mode()) << " capture): " << iterations
+                                 << " iteration(s), " << real << " nodes, " << edges << " edges");
     // upload once so the first timed launch does not pay for it
     try {
       TZ_HIP(hipGraphUpload(exec, S(streams_[0])));
@@ -363,32 +354,87 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
   }
 }
 
-bool child_capture_domain(const std::string &domain) {
-  // the default builds schedules that contain RCCL ops from child graphs, all others flat
-  static const std::string how = [] {
-    const char *v = std::getenv("TZ_GRAPH_CHILD");
-    return std::string(v ? v : "rccl");
+CaptureMode capture_mode() {
+  static const CaptureMode m = [] {
+    const char *v = std::getenv("TZ_GRAPH_CAPTURE");
+    const std::string how = v ? v : "schedule";
+    if (how == "child") return CaptureMode::Child;
+    TZ_CHECK(how == "schedule", "TZ_GRAPH_CAPTURE must be schedule or child (got " << how << ")");
+    return CaptureMode::Schedule;
   }();
-  if (how == "1") return true;
-  if (how == "rccl") return domain == "rccl";
-  return false;
+  return m;
 }
 
-std::vector<void *> capture_op(void *graphP, const std::vector<void *> &depsP, void *streamP, bool child,
-                               const std::function<void()> &launch, size_t *added) {
-  if (added) *added = 0;
-  hipGraph_t graph = static_cast<hipGraph_t>(graphP);
-  hipStream_t st = S(streamP);
+const char *capture_mode_name(CaptureMode m) {
+  return m == CaptureMode::Child ? "child" : "schedule";
+}
+
+GraphBuilder::GraphBuilder(const std::vector<void *> &streams, CaptureMode mode)
+    : streams_(streams), mode_(mode) {
+  TZ_CHECK(!streams_.empty(), "a graph build needs at least one stream");
+  if (mode_ == CaptureMode::Child) {
+    hipGraph_t g = nullptr;
+    TZ_HIP(hipGraphCreate(&g, 0));
+    graph_ = g;
+    return;
+  }
+  // events first: nothing may be created once the capture runs
+  for (size_t i = 0; i <= streams_.size(); ++i) {
+    hipEvent_t ev = nullptr;
+    const hipError_t r = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (r != hipSuccess) {
+      abandon();
+      TZ_HIP(r);
+    }
+    forkJoin_.push_back(ev);
+  }
+  hipStream_t origin = S(streams_[0]);
+  TZ_HIP(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
+  capturing_ = true;
+  try {
+    // fork: every other stream joins the capture behind the (empty) origin
+    TZ_HIP(hipEventRecord(E(forkJoin_[0]), origin));
+    for (size_t i = 1; i < streams_.size(); ++i)
+      TZ_HIP(hipStreamWaitEvent(S(streams_[i]), E(forkJoin_[0]), 0));
+  } catch (...) {
+    abandon();
+    throw;
+  }
+}
+
+GraphBuilder::~GraphBuilder() { abandon(); }
+
+void GraphBuilder::abandon() {
+  if (capturing_) {
+    capturing_ = false;
+    // join every forked stream (an unjoined stream would stay in capture mode), then end
+    hipStream_t origin = S(streams_[0]);
+    for (size_t i = 1; i < streams_.size(); ++i) {
+      (void)hipEventRecord(E(forkJoin_[i]), S(streams_[i]));
+      (void)hipStreamWaitEvent(origin, E(forkJoin_[i]), 0);
+    }
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(origin, &g);
+    if (g) (void)hipGraphDestroy(g);
+  }
+  for (void *e : forkJoin_)
+    if (e) (void)hipEventDestroy(E(e));
+  forkJoin_.clear();
+  if (graph_) {
+    (void)hipGraphDestroy(static_cast<hipGraph_t>(graph_));
+    graph_ = nullptr;
+  }
+}
+
+std::vector<void *> GraphBuilder::add(int stream, const std::vector<void *> &depsP,
+                                      const std::function<void()> &launch) {
+  TZ_CHECK(stream >= 0 && stream < int(streams_.size()), "stream " << stream << " out of range");
+  hipStream_t st = S(streams_[stream]);
   std::vector<hipGraphNode_t> deps;
   for (void *d : depsP) deps.push_back(static_cast<hipGraphNode_t>(d));
-  hipGraph_t captured = nullptr;
   std::vector<void *> tails;
-  if (child) {
-    // captured into a graph of its own, then one child-graph node behind the dependencies.
-    // Schedules with RCCL ops are built this way throughout: captured straight into the
-    // schedule graph (hipStreamBeginCaptureToGraph) their RCCL operations never completed, and
-    // RCCL child graphs mixed with ops captured straight in delivered the previous launch's data
-    // in some directions; child graphs throughout ran exact (profiles/r3b_rccl_loopback/)
+  if (mode_ == CaptureMode::Child) {
+    hipGraph_t captured = nullptr;
     TZ_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     try {
       launch();
@@ -399,41 +445,64 @@ std::vector<void *> capture_op(void *graphP, const std::vector<void *> &depsP, v
     }
     TZ_HIP(hipStreamEndCapture(st, &captured));
     size_t nsub = 0;
-    const hipError_t rn = hipGraphGetNodes(captured, nullptr, &nsub);
+    const hipError_t rn = hipGraphGetNodes(captured, nullptr, &nsub); // its capture has ended
     if (rn == hipSuccess && nsub > 0) {
       hipGraphNode_t node = nullptr;
-      const hipError_t r = hipGraphAddChildGraphNode(&node, graph, deps.data(), deps.size(), captured);
+      const hipError_t r = hipGraphAddChildGraphNode(&node, static_cast<hipGraph_t>(graph_),
+                                                     deps.data(), deps.size(), captured);
       (void)hipGraphDestroy(captured); // the child node holds its own copy
       TZ_HIP(r);
       tails.push_back(node);
-      if (added) *added = 1;
     } else {
       (void)hipGraphDestroy(captured);
       TZ_HIP(rn);
     }
     return tails;
   }
-  // (the same call sequence the runtime has always used for flat graphs)
-  TZ_HIP(hipStreamBeginCaptureToGraph(st, graph, deps.data(), nullptr, deps.size(),
-                                      hipStreamCaptureModeThreadLocal));
-  size_t before = 0, after = 0;
-  TZ_HIP(hipGraphGetNodes(graph, nullptr, &before));
-  try {
-    launch();
-    hipStreamCaptureStatus cs;
-    const hipGraphNode_t *d = nullptr;
-    size_t nd = 0;
-    TZ_HIP(hipStreamGetCaptureInfo_v2(st, &cs, nullptr, nullptr, &d, &nd));
-    for (size_t k = 0; k < nd; ++k) tails.push_back(d[k]);
-  } catch (...) {
-    (void)hipStreamEndCapture(st, &captured);
-    throw;
-  }
-  TZ_HIP(hipStreamEndCapture(st, &captured));
-  TZ_HIP(hipGraphGetNodes(graph, nullptr, &after));
-  if (after == before) tails.clear(); // enqueued nothing
-  if (added) *added = after - before;
+  TZ_CHECK(capturing_, "graph build already finished");
+  // this op runs behind exactly its schedule dependencies, whatever the stream ran before
+  TZ_HIP(hipStreamUpdateCaptureDependencies(st, deps.empty() ? nullptr : deps.data(), deps.size(),
+                                            hipStreamSetCaptureDependencies));
+  launch();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  const hipGraphNode_t *d = nullptr;
+  size_t nd = 0;
+  TZ_HIP(hipStreamGetCaptureInfo_v2(st, &cs, nullptr, nullptr, &d, &nd));
+  TZ_CHECK(cs == hipStreamCaptureStatusActive, "stream capture was invalidated by an op's launch");
+  std::vector<hipGraphNode_t> after(d, d + nd);
+  std::sort(after.begin(), after.end());
+  std::vector<hipGraphNode_t> before = deps;
+  std::sort(before.begin(), before.end());
+  if (after == before) return tails; // enqueued nothing
+  for (hipGraphNode_t n : after) tails.push_back(n);
   return tails;
+}
+
+void *GraphBuilder::finish() {
+  if (mode_ == CaptureMode::Child) {
+    void *g = graph_;
+    graph_ = nullptr;
+    return g;
+  }
+  TZ_CHECK(capturing_, "graph build already finished");
+  hipStream_t origin = S(streams_[0]);
+  capturing_ = false;
+  hipGraph_t g = nullptr;
+  hipError_t r = hipSuccess;
+  for (size_t i = 1; i < streams_.size() && r == hipSuccess; ++i) {
+    r = hipEventRecord(E(forkJoin_[i]), S(streams_[i]));
+    if (r == hipSuccess) r = hipStreamWaitEvent(origin, E(forkJoin_[i]), 0);
+  }
+  if (r != hipSuccess) {
+    capturing_ = true; // abandon() joins what it can and ends the capture
+    abandon();
+    TZ_HIP(r);
+  }
+  TZ_HIP(hipStreamEndCapture(origin, &g));
+  TZ_CHECK(g != nullptr, "stream capture produced no graph");
+  for (void *e : forkJoin_) (void)hipEventDestroy(E(e));
+  forkJoin_.clear();
+  return g;
 }
 
 void HipRuntime::set_graph_unroll(int u) {
@@ -613,15 +682,24 @@ Json chrome_trace(const std::vector<HipRuntime::Span> &spans) {
 
 void HipRuntime::run(int64_t n) {
   ++runGen_;
-  aborted_ = false;
+  // a device abort flag still set (an earlier abort whose drain was cut short, or a transport
+  // preflight that left it): drain and clear it, or every spinning kernel of this run would
+  // give up at once
+  if (kern::abort_set()) {
+    (void)hipDeviceSynchronize();
+    kern::set_abort(false);
+  }
   const double t0 = wtime();
   if (watchdogS_ > 0) {
     budget_ = watchdog_budget(n);
     deadline_ = t0 + budget_.load();
   }
-  auto aborted_run = [&] {
-    // let every kernel the abort released drain before the flag is cleared for the next run
-    // (the deadline stays armed meanwhile: a drain that never ends hits the grace exit)
+  // the end of the run: one exchange against the watchdog's claim
+  auto finish = [&] {
+    if (deadline_.exchange(0) != kClaimed) return;
+    // aborted: let every kernel the abort released drain before the flag is cleared for the
+    // next run (kDraining keeps the watchdog's grace exit armed: a drain that never ends hits it)
+    deadline_ = kDraining;
     (void)hipDeviceSynchronize();
     kern::set_abort(false);
     // the communicator abort normally ends well before the run returns; give it a bounded wait
@@ -634,15 +712,13 @@ void HipRuntime::run(int64_t n) {
   try {
     run_impl(n);
   } catch (...) {
-    if (aborted_.exchange(false)) aborted_run();
-    deadline_ = 0;
+    finish(); // throws the watchdog's error instead when it had claimed the run
     throw;
   }
-  if (aborted_.exchange(false)) aborted_run();
-  deadline_ = 0;
+  finish();
   // what the next run of this schedule may take: its longest per-iteration time so far
   const double per = (wtime() - t0) / double(std::max<int64_t>(1, n));
-  expected_ = std::max(expected_, per);
+  expected_ = std::max(expected_.load(), per);
   if (!slots_.empty() && slot_ < slots_.size()) slots_[slot_].expected = expected_;
 }
 

@@ -10,11 +10,11 @@
 //  * a pool of timing-disabled hipEvents indexed by the schedule's abstract event ids;
 //  * two execution modes for one schedule: Eager (host issues every op each iteration, like the
 //    reference) and Graph (the schedule is compiled once into a hipGraph and replayed with one
-//    hipGraphLaunch per iteration). Graph mode does not rely on multi-stream stream capture:
-//    the schedule's happens-before relation is replayed in the same vector-clock model the
-//    synchronizer uses, every GPU op is captured alone on its stream into a child graph, and
-//    the child-graph nodes get exactly the dependencies the schedule's events / host syncs
-//    imply. Host synchronizations therefore cost nothing inside a replay;
+//    hipGraphLaunch per iteration). The whole schedule is one stream capture (GraphBuilder):
+//    its happens-before relation is replayed in the same vector-clock model the synchronizer
+//    uses, and every GPU op is enqueued on its stream with that stream's capture dependencies
+//    set to exactly the nodes the schedule's events / host syncs imply. Host synchronizations
+//    therefore cost nothing inside a replay, and RCCL ops are ordinary concurrent nodes;
 //  * a watchdog: a run of n iterations gets `watchdog_s + watchdog_k * expected * n` seconds,
 //    where `expected` is the longest per-iteration time of an earlier run of the same prepared
 //    schedule (0 before the first one: the floor alone bounds the first, short, sizing run).
@@ -162,11 +162,14 @@ private:
 
   double watchdogS_ = 0;
   double watchdogK_ = 50;
-  double expected_ = 0; // longest per-iteration seconds of a run of the prepared schedule
+  // longest per-iteration seconds of a run of the prepared schedule (read by the watchdog)
+  std::atomic<double> expected_{0};
   std::atomic<int> fired_{0};
+  // > 0: the armed deadline of the current run; 0: no run; kClaimed: the watchdog claimed the
+  // run (set only by its CAS); kDraining: the aborted run is draining the device
+  static constexpr double kClaimed = -1, kDraining = -2;
   std::atomic<double> deadline_{0};
   std::atomic<double> budget_{0}; // seconds the current run was given
-  std::atomic<bool> aborted_{false}; // the watchdog fired during the current run
   std::atomic<uint64_t> runGen_{0};  // runs started so far
   // communicator aborts still running on their own threads (shared: a thread may outlive this)
   std::shared_ptr<std::atomic<int>> abortsPending_ = std::make_shared<std::atomic<int>>(0);
@@ -179,18 +182,47 @@ private:
 /// stream plus a host track
 Json chrome_trace(const std::vector<HipRuntime::Span> &spans);
 
-/// Graph-mode capture of one op's launches (`launch` enqueues them on `stream`) into `graph`
-/// behind `deps` (hipGraph_t / hipGraphNode_t / hipStream_t as void*). The runtime's graph build
-/// and the transports' preflights share it, so a preflight tests what candidates run. Straight
-/// into the graph (hipStreamBeginCaptureToGraph), or with `child` captured alone and added as
-/// one child-graph node. Returns the op's tail nodes (empty if it enqueued nothing); `added`
-/// (optional) receives the number of nodes added to `graph`.
-std::vector<void *> capture_op(void *graph, const std::vector<void *> &deps, void *stream, bool child,
-                               const std::function<void()> &launch, size_t *added = nullptr);
-/// whether a schedule whose ops include ordering domain `domain` ("rccl" if it has RCCL ops) is
-/// built from child graphs (env TZ_GRAPH_CHILD: "rccl" = schedules with RCCL ops, the default;
-/// "1" = every schedule; "0" = none)
-bool child_capture_domain(const std::string &domain);
+/// How a schedule becomes a hipGraph (env TZ_GRAPH_CAPTURE):
+///  * Schedule (default): ONE stream capture for the whole schedule. It begins on the origin
+///    stream, is forked to the other streams by an event, every op is enqueued in issue order
+///    on its own stream with that stream's capture dependencies set to exactly the nodes the
+///    schedule's happens-before relation implies (hipStreamUpdateCaptureDependencies), and the
+///    streams are joined back to the origin before the capture ends. One capture sequence per
+///    graph is the pattern NCCL-API capture is built for: RCCL keeps one persistent plan set per
+///    capture id and ties its lifetime to the captured graph (which lives as long as its exec).
+///  * Child ("child"): every op captured alone into a graph of its own and added as a child-graph
+///    node. Kept only for A/B diagnosis: HIP runs child-graph nodes one after another, so it
+///    costs all branch concurrency (profiles/r3b_rccl_loopback/child_graph_overlap.jsonl).
+enum class CaptureMode { Schedule, Child };
+CaptureMode capture_mode();
+const char *capture_mode_name(CaptureMode m);
+
+/// Builds one hipGraph from ops enqueued on a fixed set of streams (hipStream_t as void*;
+/// streams[0] is the origin). The runtime's graph build and the transports' preflights share
+/// it, so a preflight tests exactly what candidates run. Not copyable; the destructor abandons
+/// an unfinished build (joins and ends the capture, destroys the partial graph).
+class GraphBuilder {
+public:
+  GraphBuilder(const std::vector<void *> &streams, CaptureMode mode);
+  ~GraphBuilder();
+  GraphBuilder(const GraphBuilder &) = delete;
+  GraphBuilder &operator=(const GraphBuilder &) = delete;
+  /// enqueue one op (`launch` issues its work on streams[stream]) behind `deps` (hipGraphNode_t
+  /// as void*). Returns the op's tail nodes; empty when it enqueued nothing.
+  std::vector<void *> add(int stream, const std::vector<void *> &deps,
+                          const std::function<void()> &launch);
+  /// end the build: the caller owns the returned hipGraph_t (as void*)
+  void *finish();
+  CaptureMode mode() const { return mode_; }
+
+private:
+  void abandon();
+  std::vector<void *> streams_;
+  CaptureMode mode_;
+  void *graph_ = nullptr;              // Child: the graph being assembled
+  std::vector<void *> forkJoin_;       // Schedule: fork event + one join event per stream
+  bool capturing_ = false;
+};
 
 /// route the core's trace ranges (MCTS phases, schedule ops in eager runs) to roctx
 void enable_roctx(bool on);

@@ -590,31 +590,33 @@ std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
       why = "per-direction exchange: " + std::to_string(bad) + " wrong cells";
     }
     if (why.empty()) {
-      // (2) compiled into hipGraphs the way the runtime compiles candidates (capture_op, so
+      // (2) compiled into hipGraphs the way the runtime compiles candidates (GraphBuilder, so
       // RCCL ops take the same capture path): every remote direction in one group, then one
-      // RCCL node per direction with the communicators in turn, chained. Each graph runs twice,
-      // with a new value generation in between: a hang is bounded, and a delivery of the
-      // previous launch's data fails the check
+      // RCCL node per direction with the communicators in turn, chained, over three streams of
+      // one capture. Each graph runs twice, with a new value generation in between: a hang is
+      // bounded, and a delivery of the previous launch's data fails the check
       for (int form = 0; form < 2 && why.empty() && graphWhy->empty(); ++form) {
-        TZ_HIP(hipGraphCreate(&graph, 0));
-        // as the runtime builds such schedules
-        const bool child = child_capture_domain(rccl_multi_rank() ? "rccl" : "");
-        std::vector<void *> tail = capture_op(graph, {}, s, child, [&] {
-          if (!local.empty()) direct_group(local, s);
-          pack_group(remote, s);
-        });
-        if (form == 0) {
-          tail = capture_op(graph, tail, s, child, [&] { shift_group(remote, s, 0); });
-        } else {
-          // as schedules spread them: direction k on stream k % 3 with that stream's
-          // communicator (comm_for), chained in one total order like the rccl ordering domain
-          for (size_t k = 0; k < remote.size(); ++k) {
-            const int si = int(k % 3);
-            hipStream_t sk = si == 0 ? s : side[si - 1];
-            tail = capture_op(graph, tail, sk, child, [&] { shift(remote[k], sk, si); });
+        {
+          GraphBuilder gb({s, side[0], side[1]}, capture_mode());
+          std::vector<void *> tail = gb.add(0, {}, [&] {
+            if (!local.empty()) direct_group(local, s);
+            pack_group(remote, s);
+          });
+          if (form == 0) {
+            tail = gb.add(0, tail, [&] { shift_group(remote, s, 0); });
+          } else {
+            // as schedules spread them: direction k on stream k % 3 with that stream's
+            // communicator (comm_for), chained in one total order like the rccl ordering domain
+            for (size_t k = 0; k < remote.size(); ++k) {
+              const int si = int(k % 3);
+              hipStream_t sk = si == 0 ? s : side[si - 1];
+              std::vector<void *> t = gb.add(si, tail, [&] { shift(remote[k], sk, si); });
+              if (!t.empty()) tail = t;
+            }
           }
+          gb.add(0, tail, [&] { unpack_group(remote, s); });
+          graph = static_cast<hipGraph_t>(gb.finish());
         }
-        capture_op(graph, tail, s, child, [&] { unpack_group(remote, s); });
         TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
         const char *what = form == 0 ? "fused hipGraph exchange" : "per-direction hipGraph exchange";
         const int gens[2][2] = {{1, 2}, {3, 1}}; // (generations are 0..3; 0 is the search's)

@@ -1,11 +1,14 @@
 """Multi-process bootstrap.
 
 One process per GPU (``torchrun --nproc-per-node N``; RANK / WORLD_SIZE / LOCAL_RANK /
-MASTER_ADDR / MASTER_PORT from the environment). The launcher's rendezvous (torch.distributed
-with the gloo backend) is used exactly once: rank 0 opens the native TCP control-plane listener on
-an ephemeral port and broadcasts the port; every rank then joins the native star
-(``tenzing_amd._tz.TcpCtrl``). RCCL communicators for the data plane are created later by the
-workloads, with their unique ids broadcast over that control plane.
+MASTER_ADDR / MASTER_PORT from the environment). The control plane is the native TCP star
+(``tenzing_amd._tz.TcpCtrl``) and needs nothing from torch: rank 0 listens on the control port
+(``TZ_CTRL_PORT``, default MASTER_PORT + 1: torchrun's agent already serves its own store on
+MASTER_PORT) and every other rank connects to MASTER_ADDR with a handshake. So a multi-rank run
+can use the system ROCm runtime (``TZ_NO_TORCH=1``) as well as torch's bundled one.
+``TZ_CTRL_BOOTSTRAP=torch`` restores the old path (one gloo broadcast of an ephemeral port). RCCL
+communicators for the data plane are created later by the workloads, with their unique ids
+broadcast over that control plane.
 
 Processes started by an MPI launcher instead (``mpirun -n 8 python bench.py``, the reference's
 launch model) use ``MpiCtrl``: the control collectives then run over MPI_COMM_WORLD (host MPI,
@@ -67,6 +70,15 @@ def init_ctrl(rank: int | None = None, world: int | None = None, master_addr: st
     _tz.set_log_rank(rank)
     if world == 1:
         return _tz.SelfCtrl()
+    how = os.environ.get("TZ_CTRL_BOOTSTRAP", "tcp")
+    if how not in ("tcp", "torch"):
+        raise ValueError(f"TZ_CTRL_BOOTSTRAP must be tcp or torch (got {how!r})")
+    ctrl = _tz.TcpCtrl(rank, world)
+    host = master_addr or e.master_addr
+    if how == "tcp":
+        port = int(os.environ.get("TZ_CTRL_PORT", e.master_port + 1))
+        ctrl.rendezvous(host, port, timeout_s)
+        return ctrl
     import datetime
 
     import torch.distributed as dist
@@ -74,11 +86,10 @@ def init_ctrl(rank: int | None = None, world: int | None = None, master_addr: st
     if not dist.is_initialized():
         dist.init_process_group("gloo", rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s))
-    ctrl = _tz.TcpCtrl(rank, world)
     port = ctrl.listen(0) if rank == 0 else 0
     box = [port]
     dist.broadcast_object_list(box, src=0)
-    ctrl.connect(master_addr or e.master_addr, int(box[0]), timeout_s)
+    ctrl.connect(host, int(box[0]), timeout_s)
     return ctrl
 
 

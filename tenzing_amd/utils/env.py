@@ -99,22 +99,62 @@ def xgmi_topology_summary(timeout_s: float = 20.0):
             "xgmi_links": sum(1 for i in range(n) for j in range(i + 1, n) if mat[i][j] == "XGMI")}
 
 
+def mapped_library(stem: str, maps: str | None = None) -> str | None:
+    """Path of the shared library whose file name starts with ``stem`` (e.g. "libamdhip64")
+    mapped into this process (``/proc/self/maps``), or None. Which copy a process maps decides
+    what runs: torch's bundled runtime or the system ROCm's, whichever was loaded first."""
+    if maps is None:
+        maps = _read("/proc/self/maps")
+    for line in maps.splitlines():
+        parts = line.split(None, 5)
+        if len(parts) == 6 and os.path.basename(parts[5]).startswith(stem + "."):
+            return parts[5].strip()
+    return None
+
+
+def _hip_version_str(v: int) -> str | None:
+    if v is None or v < 0:
+        return None
+    return f"{v // 10000000}.{(v // 100000) % 100}.{v % 100000}"
+
+
+def _rccl_version_str(v: str) -> str:
+    try:
+        n = int(v)
+    except ValueError:
+        return v
+    # NCCL_VERSION_CODE: major*10000 + minor*100 + patch (>= 2.9)
+    return f"{n // 10000}.{(n // 100) % 100}.{n % 100}"
+
+
+def runtime_libraries(maps: str | None = None) -> dict:
+    """The HIP runtime and RCCL this process actually runs: mapped file + version reported by
+    that library (not what /opt/rocm holds). Reference: src/reproduce.cpp:22-37 (version dump)."""
+    return {
+        "hip_runtime": {"path": mapped_library("libamdhip64", maps),
+                        "version": _hip_version_str(_tz.hip_runtime_version())},
+        "rccl_library": {"path": mapped_library("librccl", maps),
+                         "version": _rccl_version_str(_tz.rccl_version())},
+        "torch_loaded": "torch" in sys.modules,
+    }
+
+
 def env_report(device: int | None = None, topology: bool = False) -> dict:
+    libs = runtime_libraries()
     r = {
         "tenzing_amd": _tz.version(),
         "python": sys.version.split()[0],
         "host": platform.node(),
-        "rocm": _read("/opt/rocm/.info/version"),
-        "rccl": _tz.rccl_version(),
+        # what is installed under /opt/rocm; the process may run another copy (hip_runtime)
+        "rocm_install": _read("/opt/rocm/.info/version"),
+        "hip_runtime": libs["hip_runtime"],
+        "rccl_library": libs["rccl_library"],
         "gpus": _tz.hip_device_count(),
     }
-    try:
-        import torch
-
+    torch = sys.modules.get("torch")  # reported when loaded; never imported just for this
+    if torch is not None:
         r["torch"] = torch.__version__
         r["torch_hip"] = torch.version.hip
-    except Exception:  # noqa: BLE001
-        pass
     if device is not None and r["gpus"] > 0:
         rt = _tz.HipRuntime(device=device, n_streams=1)
         r["device"] = rt.device_name()

@@ -220,6 +220,84 @@ def main():
         out["mcts"] = len(res.sims)
         out["runs"] = runs
         out["nranks"] = comms[0].size if hasattr(comms[0], "size") else None
+    elif case == "rccl_overlap":
+        # an RCCL send/recv node beside two independent ~200 us kernels, all three on different
+        # streams of one hipGraph: with whole-schedule capture the RCCL node must overlap the
+        # kernels (one launch ~ one kernel), and the received data must follow every new value
+        # generation of the send buffer
+        import time
+
+        import torch
+        from tenzing_amd.ops import comm
+
+        W, R = ctrl.size, ctrl.rank
+        n = int(os.environ.get("TZ_TEST_N", str(1 << 12)))
+        us = float(os.environ.get("TZ_TEST_BUSY_US", "200"))
+        torch.cuda.set_device(dev)
+        f64 = dict(dtype=torch.float64, device=f"cuda:{dev}")
+        comms = tz._tz.make_rccl_comms(ctrl, dev, 3)
+        a, c = torch.zeros(n, **f64), torch.zeros(n, **f64)
+        nxt, prv = (R + 1) % W, (R - 1) % W
+        sr = comm.send_recv("sr", comms, a, nxt, c, prv)
+        ka, kb = tz.BusyKernelOp("busy_a", us), tz.BusyKernelOp("busy_b", us)
+        g = tz.Graph()
+        for op in (ka, kb, sr):
+            g.start_then(op)
+            g.then_finish(op)
+        msg = ""
+        if R == 0:
+            for seed in range(400):
+                s = tz.random_rollout(tz.State(g, tz.Platform(3)), seed)
+                st = {o.name: o.stream for o in s.ops() if o.name in ("busy_a", "busy_b", "sr")}
+                if len(set(st.values())) == 3:
+                    msg = s.json(True)
+                    break
+        seq = tz.OpIndex(g).sequence_from_json(ctrl.bcast(msg, 0).decode())
+        rt = tz.HipRuntime(device=dev, n_streams=3, mode=tz.ExecMode.Graph, watchdog_s=60.0)
+        rt.prepare(seq)
+        out["effective_mode"] = str(rt.effective_mode)
+        out["graph_nodes"] = rt.graph_nodes
+        idx = torch.arange(n, **f64)
+        bad = []
+        for gen in (1, 2, 3):
+            a.copy_(idx + 1000.0 * (R + 1) + 7.0 * gen)
+            c.zero_()
+            torch.cuda.synchronize()
+            ctrl.barrier()
+            rt.run(1)
+            rt.device_sync()
+            want = idx + 1000.0 * (prv + 1) + 7.0 * gen
+            bad.append(int((c != want).sum()))
+            say("gen", gen, "bad", bad[-1])
+        out["bad"] = bad
+        iters = int(os.environ.get("TZ_TEST_ITERS", "50"))
+        rt.run(5)
+        rt.device_sync()
+        times = []
+        for _ in range(3):
+            ctrl.barrier()
+            t0 = time.perf_counter()
+            rt.run(iters)
+            rt.device_sync()
+            times.append((time.perf_counter() - t0) / iters * 1e6)
+        out["iter_us"] = min(times)
+        out["iter_us_all"] = times
+        out["one_kernel_us"] = us
+        # the RCCL op alone, same capture path: what the overlap hides
+        g2 = tz.Graph()
+        g2.start_then(sr)
+        g2.then_finish(sr)
+        msg = tz.random_rollout(tz.State(g2, tz.Platform(3)), 0).json(True) if R == 0 else ""
+        rt.prepare(tz.OpIndex(g2).sequence_from_json(ctrl.bcast(msg, 0).decode()))
+        rt.run(5)
+        rt.device_sync()
+        ctrl.barrier()
+        t0 = time.perf_counter()
+        rt.run(iters)
+        rt.device_sync()
+        out["rccl_alone_us"] = (time.perf_counter() - t0) / iters * 1e6
+        out["capture"] = os.environ.get("TZ_GRAPH_CAPTURE", "schedule")
+        del rt
     elif case == "ipc_abort":
         # a candidate that hangs on rank 0 (a spinning kernel ahead of its puts): the watchdogs
         # abort it on every rank, the benchmarker fails it collectively, the recovery hooks reset

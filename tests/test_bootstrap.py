@@ -1,0 +1,128 @@
+"""Multi-rank bootstrap without torch: the native TCP control plane's own rendezvous
+(``TcpCtrl.rendezvous`` on MASTER_PORT + 1, handshake-checked), as bench.py uses it at N > 1.
+Reference: MPI_Init + MPI_COMM_WORLD (tenzing-mcts/examples/halo_min_time.cu:11)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+BODY = r"""
+import json, os, sys
+sys.path.insert(0, os.environ["TZ_ROOT"])
+from tenzing_amd.parallel import init_ctrl
+from tenzing_amd.utils.env import runtime_libraries
+c = init_ctrl(timeout_s=60)
+c.barrier()
+got = c.bcast("hello" if c.rank == 0 else "", 0).decode()
+mx = c.allreduce_max([float(c.rank)])[0]
+ag = [x.decode() for x in c.allgather(f"r{c.rank}")]
+libs = runtime_libraries()
+print("RESULT " + json.dumps(dict(rank=c.rank, size=c.size, got=got, mx=mx, ag=ag,
+                                  torch="torch" in sys.modules, libs=libs)), flush=True)
+"""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(world, port, extra=None, timeout=120):
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TZ_NO_TORCH="1",
+                   TZ_ROOT=ROOT, **(extra or {}))
+        env.pop("TZ_CTRL_BOOTSTRAP", None)
+        procs.append(subprocess.Popen([sys.executable, "-c", BODY], env=env, text=True,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=timeout))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return procs, outs
+
+
+def _results(procs, outs):
+    res = []
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+        line = [x for x in o.splitlines() if x.startswith("RESULT ")][-1]
+        res.append(json.loads(line[len("RESULT "):]))
+    return res
+
+
+def test_two_ranks_without_torch():
+    """two ranks rendezvous on MASTER_PORT + 1 with torch never imported; every collective
+    works, and each rank reports the HIP runtime / RCCL it actually mapped"""
+    res = _results(*_launch(2, _free_port()))
+    for r in res:
+        assert r["size"] == 2 and r["got"] == "hello" and r["mx"] == 1.0 and r["ag"] == ["r0", "r1"]
+        assert r["torch"] is False
+        # without torch the system ROCm's runtime is the one mapped
+        assert r["libs"]["hip_runtime"]["path"].startswith("/opt/rocm")
+        assert r["libs"]["rccl_library"]["path"].startswith("/opt/rocm")
+        assert r["libs"]["torch_loaded"] is False
+
+
+def test_four_ranks_explicit_ctrl_port():
+    port = _free_port()
+    res = _results(*_launch(4, 29000, extra={"TZ_CTRL_PORT": str(port)}))
+    assert sorted(r["rank"] for r in res) == [0, 1, 2, 3]
+    assert all(r["ag"] == ["r0", "r1", "r2", "r3"] for r in res)
+
+
+def test_stray_connection_is_dropped():
+    """a connection to the control port that does not speak the handshake is dropped, and the
+    job's ranks still join"""
+    import threading
+
+    port = _free_port()
+
+    def stray():
+        t0 = time.time()
+        while time.time() - t0 < 30:
+            try:
+                s = socket.create_connection(("127.0.0.1", port + 1), timeout=1)
+                s.sendall(b"GET / HTTP/1.0\r\n\r\n")
+                time.sleep(0.2)
+                s.close()
+                return
+            except OSError:
+                time.sleep(0.05)
+
+    th = threading.Thread(target=stray)
+    th.start()
+    res = _results(*_launch(2, port))
+    th.join()
+    assert [r["got"] for r in res] == ["hello", "hello"]
+
+
+def test_world_size_mismatch_fails_loudly():
+    """a rank of a differently sized job is refused with a clear error, not taken for a rank"""
+    port = _free_port()
+    env = dict(os.environ, TZ_NO_TORCH="1", TZ_ROOT=ROOT, MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port))
+    p0 = subprocess.Popen([sys.executable, "-c", BODY], env=dict(env, RANK="0", WORLD_SIZE="2"),
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    p1 = subprocess.Popen([sys.executable, "-c", BODY], env=dict(env, RANK="1", WORLD_SIZE="3"),
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        _, e0 = p0.communicate(timeout=90)
+        p1.communicate(timeout=90)
+    finally:
+        for p in (p0, p1):
+            if p.poll() is None:
+                p.kill()
+    assert p0.returncode != 0 and "of 3" in e0, e0[-2000:]

@@ -53,7 +53,11 @@ def test_native_cli_sim(tmp_path):
 def test_env_report():
     out = _py("env")
     j = json.loads(out)
-    assert "tenzing_amd" in j and "rccl" in j
+    assert "tenzing_amd" in j and "rccl_library" in j and "hip_runtime" in j
+    # the runtime actually mapped into the process, not /opt/rocm's version file
+    assert j["hip_runtime"]["path"] and "libamdhip64" in j["hip_runtime"]["path"]
+    assert j["rccl_library"]["path"] and "librccl" in j["rccl_library"]["path"]
+    assert j["rccl_library"]["version"].count(".") == 2
 
 
 def test_native_cli_sigint_dumps_partial_csv():
