@@ -110,6 +110,7 @@ public:
   void allreduce_max(double *v, size_t n) override;
   void allreduce_sum(double *v, size_t n) override;
   std::vector<std::string> allgather(const std::string &mine) override;
+  std::vector<std::string> alltoallv(const std::vector<std::string> &out) override;
   using Ctrl::allreduce_max;
 
 private:

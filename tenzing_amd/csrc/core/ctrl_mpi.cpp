@@ -49,6 +49,9 @@ struct Api {
   int (*Allgather)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, MPI_Comm) = nullptr;
   int (*Allgatherv)(const void *, int, MPI_Datatype, void *, const int *, const int *, MPI_Datatype,
                     MPI_Comm) = nullptr;
+  int (*Alltoall)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, MPI_Comm) = nullptr;
+  int (*Alltoallv)(const void *, const int *, const int *, MPI_Datatype, void *, const int *,
+                   const int *, MPI_Datatype, MPI_Comm) = nullptr;
   bool initializedHere = false;
 };
 
@@ -128,6 +131,8 @@ Api &api(const std::string &want) {
   sym(*a, a->Allreduce, "MPI_Allreduce");
   sym(*a, a->Allgather, "MPI_Allgather");
   sym(*a, a->Allgatherv, "MPI_Allgatherv");
+  sym(*a, a->Alltoall, "MPI_Alltoall");
+  sym(*a, a->Alltoallv, "MPI_Alltoallv");
   int init = 0, fin = 0;
   a->Initialized(&init);
   a->Finalized(&fin);
@@ -227,6 +232,40 @@ std::vector<std::string> MpiCtrl::allgather(const std::string &mine) {
   std::vector<std::string> out(static_cast<size_t>(size_));
   for (int r = 0; r < size_; ++r) out[size_t(r)] = all.substr(size_t(offs[size_t(r)]), size_t(lens[size_t(r)]));
   return out;
+}
+
+std::vector<std::string> MpiCtrl::alltoallv(const std::vector<std::string> &out) {
+  // each rank moves only its own payloads (the base version's allgather would hand every rank
+  // every payload: P x all faces per rank per exchange for the host-staged halo)
+  TZ_CHECK(int(out.size()) == size_, "alltoallv: " << out.size() << " payloads for " << size_ << " ranks");
+  const size_t P = static_cast<size_t>(size_);
+  std::vector<int> sendLen(P, 0), sendOff(P, 0), recvLen(P, 0), recvOff(P, 0);
+  long long st = 0;
+  for (int r = 0; r < size_; ++r) {
+    TZ_CHECK(out[size_t(r)].size() < (size_t(1) << 31), "MPI alltoallv: payload too large");
+    sendLen[size_t(r)] = int(out[size_t(r)].size());
+    sendOff[size_t(r)] = int(st);
+    st += sendLen[size_t(r)];
+  }
+  TZ_CHECK(st < (1ll << 31), "MPI alltoallv: " << st << " bytes sent in total");
+  TZ_MPI(g_api->Alltoall(sendLen.data(), 1, kInt, recvLen.data(), 1, kInt, kCommWorld));
+  long long rt = 0;
+  for (int r = 0; r < size_; ++r) {
+    recvOff[size_t(r)] = int(rt);
+    rt += recvLen[size_t(r)];
+  }
+  TZ_CHECK(rt < (1ll << 31), "MPI alltoallv: " << rt << " bytes received in total");
+  std::string sendBuf;
+  sendBuf.reserve(size_t(st));
+  for (const auto &o : out) sendBuf += o;
+  std::string recvBuf(size_t(rt), '\0');
+  TZ_MPI(g_api->Alltoallv(st ? sendBuf.data() : nullptr, sendLen.data(), sendOff.data(), kByte,
+                          rt ? &recvBuf[0] : nullptr, recvLen.data(), recvOff.data(), kByte,
+                          kCommWorld));
+  std::vector<std::string> in(static_cast<size_t>(size_));
+  for (int r = 0; r < size_; ++r)
+    in[size_t(r)] = recvBuf.substr(size_t(recvOff[size_t(r)]), size_t(recvLen[size_t(r)]));
+  return in;
 }
 
 } // namespace tz

@@ -59,11 +59,14 @@ namespace {
 // bootstrap that cannot connect) would leave the others blocked forever, and a blocked init has
 // no handle to abort. So the init runs on a helper thread (with this thread's device) and the
 // caller waits with a bound (env TZ_RCCL_INIT_S, default 120 s): on timeout the caller raises,
-// the collective agreement that follows drops RCCL, and the stuck helper is abandoned.
+// the collective agreement that follows drops RCCL, and the helper is abandoned. An abandoned
+// helper whose init still completes (a late rank joined after all) aborts the communicator it
+// got, so nothing unregistered keeps RCCL proxy threads and device resources alive.
 struct InitState {
   std::mutex mu;
   std::condition_variable cv;
   bool done = false;
+  bool abandoned = false; // the caller gave up waiting: the helper owns the outcome
   ncclResult_t res = ncclSuccess;
   ncclComm_t comm = nullptr;
 };
@@ -79,15 +82,22 @@ ncclComm_t init_bounded(int nranks, const ncclUniqueId &id, int rank) {
     ncclResult_t r = ncclSuccess;
     if (hipSetDevice(dev) != hipSuccess) r = ncclSystemError;
     else r = ncclCommInitRank(&c, nranks, id, rank);
-    std::lock_guard<std::mutex> lk(st->mu);
+    std::unique_lock<std::mutex> lk(st->mu);
+    if (st->abandoned) {
+      lk.unlock();
+      if (r == ncclSuccess && c) ncclCommAbort(c); // nobody will ever use or free it
+      return;
+    }
     st->res = r;
     st->comm = c;
     st->done = true;
     st->cv.notify_all();
   }).detach();
   std::unique_lock<std::mutex> lk(st->mu);
-  if (!st->cv.wait_for(lk, std::chrono::microseconds(int64_t(limit * 1e6)), [&] { return st->done; }))
+  if (!st->cv.wait_for(lk, std::chrono::microseconds(int64_t(limit * 1e6)), [&] { return st->done; })) {
+    st->abandoned = true;
     TZ_THROW("ncclCommInitRank did not complete within " << limit << " s (a rank missing?)");
+  }
   if (st->res != ncclSuccess)
     TZ_THROW("ncclCommInitRank failed: " << ncclGetErrorString(st->res));
   return st->comm;

@@ -4,6 +4,7 @@
 #include "halo_internal.hpp"
 
 #include "core/health.hpp"
+#include "core/solve.hpp"
 
 #include <algorithm>
 #include <chrono>
@@ -50,6 +51,10 @@ std::string HaloExchange::Dir::name() const {
 
 HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.nx > 0 && a_.ny > 0 && a_.nz > 0 && a_.nq > 0 && a_.ghost > 0, "bad halo extents");
+  // the verification values (halo_value, kernels/halo_kernels.hip) pack (gen, q, z, y, x) into
+  // the 53 exact bits of a double: q in 3 bits below the generation, 16 bits per global axis
+  TZ_CHECK(a_.nq <= 8, "at most 8 quantities per cell (got " << a_.nq
+                                                             << "): the grid checks encode q in 3 bits");
   TZ_CHECK(a_.ghost <= a_.nx && a_.ghost <= a_.ny && a_.ghost <= a_.nz, "ghost wider than domain");
   TZ_CHECK(a_.neighbors == 6 || a_.neighbors == 26, "neighbors must be 6 or 26");
   TZ_CHECK(a_.order == "xyzq" || a_.order == "qxyz", "order must be xyzq or qxyz");
@@ -560,7 +565,6 @@ std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
   // a hung exchange: release every spinning kernel first (an abort may wait for the device),
   // then abort the communicators on a thread of their own (their kernels return; the abort
   // itself may block), drain the stream with a bound, clear the flag again
-  bool stuck = false; // work on the streams never drained: nothing they use may be freed
   auto hung = [&](const std::string &what) {
     kern::set_abort(true);
     std::vector<std::shared_ptr<RcclComm>> cs = comms_;
@@ -569,10 +573,15 @@ std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
         if (c && !c->aborted()) c->abort();
     }).detach();
     const bool drained = bounded_wait(s, limit);
-    if (drained) kern::set_abort(false); // else leave it set: something still spins
-    else stuck = true;
-    why = what + " (no completion within " + std::to_string(int(limit)) + " s; communicators aborted" +
-          (drained ? ")" : "; the device did not drain)");
+    if (!drained)
+      // the abort flag cannot be cleared while something still spins, and with it set every
+      // device-side wait of every later candidate (IPC arrivals, relays, host split) gives up at
+      // once: the search would skip every candidate and measure nothing. End the run with the
+      // reason instead (the deadline's partial report says how far it came).
+      exit_with_report(6, "RCCL preflight (" + what + "): the device did not drain after the "
+                          "communicator abort");
+    kern::set_abort(false);
+    why = what + " (no completion within " + std::to_string(int(limit)) + " s; communicators aborted)";
   };
   try {
     // (1) eagerly, one direction at a time, the communicators in turn
@@ -629,7 +638,6 @@ std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
             *graphWhy = std::string(what) + ", launch " + std::to_string(launch) + ": " +
                         std::to_string(bad) + " wrong cells";
         }
-        if (stuck) break; // the exec may still run: left to the cleanup below (leaked)
         (void)hipGraphExecDestroy(exec);
         exec = nullptr;
         (void)hipGraphDestroy(graph);
@@ -651,7 +659,6 @@ std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
       why = first + "; " + why;
     }
   }
-  if (stuck) return why; // a graph or stream still in use by the device is deliberately leaked
   if (exec) (void)hipGraphExecDestroy(exec);
   if (graph) (void)hipGraphDestroy(graph);
   (void)hipStreamDestroy(s);

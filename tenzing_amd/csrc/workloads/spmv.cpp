@@ -1,4 +1,5 @@
 #include "workloads.hpp"
+#include "core/solve.hpp"
 
 #include "core/util.hpp"
 #include "hip/hip_runtime.hpp"
@@ -637,8 +638,13 @@ std::string DistSpmv::rccl_preflight_local() {
       kern::set_abort(true);
       auto c = comm_;
       std::thread([c] { c->abort(); }).detach();
-      const bool drained = wait();
-      if (drained) kern::set_abort(false);
+      if (!wait())
+        // the abort flag cannot be cleared while something still spins, and with it set every
+        // device-side wait of every later candidate gives up at once: the search would measure
+        // nothing. End the run with the reason instead.
+        exit_with_report(6, "RCCL preflight (spmv): the device did not drain after the "
+                            "communicator abort");
+      kern::set_abort(false);
       why = "exchange did not complete within " + std::to_string(int(limit)) + " s (communicator aborted)";
     } else {
       std::vector<float> xr(remoteCols_.size());

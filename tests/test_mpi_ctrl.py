@@ -29,6 +29,8 @@ got2 = c.bcast("x" * 100000 if c.rank == 2 else "", 2).decode()
 mx = c.allreduce_max([float(c.rank), -float(c.rank)])
 sm = c.allreduce_sum([1.0, 2.0])
 ag = [x.decode() for x in c.allgather("r" * c.rank)]
+# personalized exchange (MPI_Alltoallv): element j to rank j, of varying sizes incl. empty
+a2a = [x.decode() for x in c.alltoallv([f"{{c.rank}}>{{j}}" * j for j in range(c.size)])]
 # a collective search on top of it: rank 0 owns the tree, every rank benchmarks every candidate
 g = tz.Graph()
 a, b = tz.SimGpuOp("a", 20.0), tz.SimGpuOp("b", 30.0)
@@ -36,7 +38,7 @@ g.start_then(a); g.start_then(b); g.then_finish(a); g.then_finish(b)
 o = tz.MctsOpts(); o.n_iters = 8; o.bench = tz.BenchOpts(n_iters=3)
 r = tz.mcts_explore(g, tz.Platform(2), tz.SimBenchmarker(2), c, o)
 print(json.dumps(dict(rank=c.rank, size=c.size, local=env().local_rank, got=got,
-                      got2=len(got2), mx=mx, sm=sm, ag=ag, n=len(r.sims))), flush=True)
+                      got2=len(got2), mx=mx, sm=sm, ag=ag, a2a=a2a, n=len(r.sims))), flush=True)
 """
 
 
@@ -60,6 +62,7 @@ def test_mpi_ctrl_collectives_and_search():
         assert r["got"] == "hello" and r["got2"] == 100000
         assert r["mx"] == [2.0, 0.0] and r["sm"] == [3.0, 6.0]
         assert r["ag"] == ["", "r", "rr"]
+        assert r["a2a"] == [f"{src}>{r['rank']}" * r["rank"] for src in range(3)]
     assert rs[0]["n"] == 8 and rs[1]["n"] == 0  # only rank 0 holds results
 
 
