@@ -217,6 +217,7 @@ def main() -> int:
     import tenzing_amd as tz
     from tenzing_amd.models import HaloConfig, build_halo
     from tenzing_amd.parallel import init
+    from tenzing_amd.utils.env import runtime_libraries
 
     elapsed = time.time() - T_START
     deadline = (tz.RunDeadline(max(1.0, args.deadline_s - elapsed), 5)
@@ -303,6 +304,15 @@ def main() -> int:
     bench = tz.EmpiricalBenchmarker(rt, ctrl)
     setup_s = time.time() - t_setup
     transports = halo.transport_report()
+    # which device every peer rank sits on and whether this GPU reaches it peer-to-peer
+    # (collective); rank 0's view goes into the record, the "peer_access" line into
+    # transports_available
+    peers = None
+    if world > 1:
+        from tenzing_amd.parallel.topology import peer_device_facts
+        nb = [halo.neighbor(k) for k in range(halo.ndirs()) if not halo.is_direct(k)]
+        peers = peer_device_facts(ctrl, device, nb, ipc_mapped=halo.ipc_peer_devices())
+        transports["peer_access"] = peers["summary"]
     report(phase="search", setup_s=setup_s, transport=halo.transport(),
            transports_available=transports, rccl_nranks=halo.rccl_nranks() or None)
 
@@ -592,6 +602,8 @@ def main() -> int:
             "cpus_bound": len(cpus) or None,
             "rccl_socket_ifname": os.environ.get("NCCL_SOCKET_IFNAME") if world > 1 else None,
             "xgmi_topology": topo,
+            "peer_devices": peers,
+            "runtime": runtime_libraries(),
             "link_probe": probe,
             "elapsed_s": round(time.time() - T_START, 1),
         })

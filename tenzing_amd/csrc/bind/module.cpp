@@ -200,6 +200,14 @@ PYBIND11_MODULE(_tz, m) {
     int v = 0;
     return hipRuntimeGetVersion(&v) == hipSuccess ? v : -1;
   }, "HIP_VERSION of the libamdhip64 this process actually uses (major*1e7 + minor*1e5 + patch)");
+  m.def("device_by_pci_bus_id", [](const std::string &bus) {
+    int d = -1;
+    return hipDeviceGetByPCIBusId(&d, bus.c_str()) == hipSuccess ? d : -1;
+  }, "this process's index of the GPU at PCI bus id `bus` (-1: not visible here)");
+  m.def("can_access_peer", [](int a, int b) {
+    int v = 0;
+    return hipDeviceCanAccessPeer(&v, a, b) == hipSuccess && v != 0;
+  }, "hipDeviceCanAccessPeer(a, b)");
   m.def("hip_driver_version", [] {
     int v = 0;
     return hipDriverGetVersion(&v) == hipSuccess ? v : -1;
@@ -923,6 +931,8 @@ PYBIND11_MODULE(_tz, m) {
       .def("uses_host", &HaloExchange::uses_host)
       .def("rccl_nranks", &HaloExchange::rccl_nranks)
       .def("transport_report", &HaloExchange::transport_report)
+      .def("ipc_peer_devices", &HaloExchange::ipc_peer_devices,
+           "peer rank -> device its IPC-mapped memory reports (hipPointerGetAttributes)")
       .def("reset_transport_state", &HaloExchange::reset_transport_state, py::arg("ctrl"),
            py::call_guard<py::gil_scoped_release>())
       .def("host_exchange", &HaloExchange::host_exchange, py::call_guard<py::gil_scoped_release>())

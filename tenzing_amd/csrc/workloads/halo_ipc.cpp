@@ -246,6 +246,16 @@ std::string HaloExchange::setup_ipc(Ctrl *ctrl) {
   return "";
 }
 
+std::map<int, int> HaloExchange::ipc_peer_devices() const {
+  std::map<int, int> out;
+  for (size_t q = 0; q < peerFlags_.size(); ++q) {
+    if (!peerFlags_[q]) continue;
+    hipPointerAttribute_t at{};
+    out[int(q)] = hipPointerGetAttributes(&at, peerFlags_[q]) == hipSuccess ? at.device : -1;
+  }
+  return out;
+}
+
 void HaloExchange::put_group(const std::vector<int> &dirs, void *stream) const {
   TZ_CHECK(ready() && ipcReady_, "ipc transport not set up");
   TZ_CHECK(!dirs.empty() && dirs.size() <= size_t(kern::kMaxBoxes), "bad put group");

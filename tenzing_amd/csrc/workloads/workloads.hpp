@@ -279,6 +279,10 @@ public:
   /// per transport ("rccl", "ipc", "relay", "host"): "ok", "not offered", or why it is
   /// unavailable (creation or preflight failure), after setup
   std::map<std::string, std::string> transport_report() const;
+  /// for every peer rank whose memory this rank mapped over IPC: the device the mapped flags
+  /// allocation reports (hipPointerGetAttributes), -1 if that query fails. On a multi-GPU node
+  /// a peer's memory must sit on another device than this rank's; on loopback, on the same one.
+  std::map<int, int> ipc_peer_devices() const;
   /// collective, every rank idle: restart the IPC put / wait counters (and clear the wait
   /// timeouts) from zero, e.g. after a verification run that timed out; a barrier otherwise
   void reset_transport_state(Ctrl *ctrl) {

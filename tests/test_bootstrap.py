@@ -126,3 +126,45 @@ def test_world_size_mismatch_fails_loudly():
             if p.poll() is None:
                 p.kill()
     assert p0.returncode != 0 and "of 3" in e0, e0[-2000:]
+
+
+def test_peer_device_facts_fake_two_device_topology():
+    """the device-pair record on a fake 2-GPU node (rank 0 on bus A / device 0, rank 1 on bus B /
+    device 1) and on a fake loopback pair (both ranks on bus A)"""
+    from tenzing_amd.parallel.topology import peer_device_facts
+
+    class FakeCtrl:
+        def __init__(self, rank, buses):
+            self.rank, self.buses = rank, buses
+
+        def allgather(self, mine):
+            assert mine == self.buses[self.rank]
+            return [b.encode() for b in self.buses]
+
+    devs = {"0000:0a:00.0": 0, "0000:1b:00.0": 1}
+    f = peer_device_facts(FakeCtrl(0, ["0000:0a:00.0", "0000:1b:00.0"]), 0, [1, 1, 0],
+                          bus_of=lambda d: "0000:0a:00.0", device_by_bus=lambda b: devs.get(b, -1),
+                          can_access=lambda a, b: (a, b) == (0, 1), ipc_mapped={1: 1})
+    p = f["peers"]["1"]
+    assert list(f["peers"]) == ["1"]  # self and duplicates dropped
+    assert p["same_device"] is False and p["visible_as"] == 1 and p["can_access_peer"] is True
+    assert p["ipc_mapped_on_device"] == 1 and p["ipc_mapping_consistent"] is True
+    assert f["summary"] == "1 of 1 peer(s) on other devices, 1 with peer access"
+    # a mapping that claims this rank's own device for a peer on another GPU is flagged
+    g = peer_device_facts(FakeCtrl(0, ["0000:0a:00.0", "0000:1b:00.0"]), 0, [1],
+                          bus_of=lambda d: "0000:0a:00.0", device_by_bus=lambda b: devs.get(b, -1),
+                          can_access=lambda a, b: True, ipc_mapped={1: 0})
+    assert g["peers"]["1"]["ipc_mapping_consistent"] is False and "unexpected" in g["summary"]
+    # the peer's GPU hidden from this process (device isolation): no access claim either way
+    h = peer_device_facts(FakeCtrl(0, ["0000:0a:00.0", "0000:1b:00.0"]), 0, [1],
+                          bus_of=lambda d: "0000:0a:00.0", device_by_bus=lambda b: -1,
+                          can_access=lambda a, b: True)
+    assert h["peers"]["1"]["can_access_peer"] is None and "not visible" in h["peers"]["1"]["reason"]
+    # loopback: both ranks on one device
+    lo = peer_device_facts(FakeCtrl(1, ["0000:0a:00.0", "0000:0a:00.0"]), 0, [0],
+                           bus_of=lambda d: "0000:0a:00.0", device_by_bus=lambda b: 0,
+                           can_access=lambda a, b: False, ipc_mapped={0: 0})
+    q = lo["peers"]["0"]
+    assert q["same_device"] is True and q["can_access_peer"] is None
+    assert q["ipc_mapping_consistent"] is True
+    assert lo["summary"] == "all 1 peer(s) on this rank's own device (loopback)"

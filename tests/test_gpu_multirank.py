@@ -177,6 +177,14 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     assert j["transport_by_group"]["remote"]["via"] in ("ipc", "sdma", "memcpy", "mixed",
                                                         "hostsplit10", "hostsplit20", "hostsplit30", "hostsplit40")
     assert j["watchdog"]["fired"] == 0 and j["dead_domains"] == []
+    # device-pair facts: on one GPU every peer is this rank's own device, and the IPC-mapped
+    # peer memory says so; the record names the HIP runtime / RCCL actually mapped
+    pd = j["peer_devices"]
+    assert pd["peers"] and all(p["same_device"] and p["ipc_mapping_consistent"]
+                               for p in pd["peers"].values()), pd
+    assert ta["peer_access"].endswith("(loopback)")
+    assert "libamdhip64" in j["runtime"]["hip_runtime"]["path"]
+    assert "librccl" in j["runtime"]["rccl_library"]["path"]
     if mode == "buffers":
         # one seed per remote transport, each measured before the search
         assert set(j["seeded_pct10_ms"]) == {"ipc", "sdma", "memcpy", "mixed", "hostsplit10",
