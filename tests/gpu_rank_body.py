@@ -15,9 +15,16 @@ def main():
     case = sys.argv[1]
     verbose = bool(os.environ.get("TZ_TEST_VERBOSE"))
 
+    import time as _time
+
+    t_start = _time.time()
+
     def say(*a):
         if verbose:
-            print(*a, file=sys.stderr, flush=True)
+            print(f"[rank {os.environ.get('RANK', '?')} +{_time.time() - t_start:.1f}s]", *a,
+                  file=sys.stderr, flush=True)
+
+    say("start", case)
 
     ctrl, dev = init(timeout_s=120)
     say("init done")

@@ -32,28 +32,59 @@ rccl_loopback = pytest.mark.skipif(os.environ.get("TZ_TEST_RCCL_LOOPBACK") != "1
                                    reason="RCCL across loopback ranks: set TZ_TEST_RCCL_LOOPBACK=1")
 
 
-def _launch(case, world, timeout=300, extra_env=None):
+def _tails(logs, n=40):
+    out = []
+    for r, path in enumerate(logs):
+        try:
+            with open(path) as f:
+                lines = f.read().splitlines()
+        except OSError:
+            lines = ["(no log)"]
+        out.append(f"== rank {r} ({path}), last {n} lines:\n" + "\n".join(lines[-n:]))
+    return "\n".join(out)
+
+
+def _launch(case, world, timeout=300, extra_env=None, tmp_path=None):
+    """W rank processes of gpu_rank_body.py; each rank's output goes to its own file AS IT RUNS
+    (TZ_TEST_VERBOSE progress lines, watchdog and [tz] messages), so a rank that hangs or dies
+    still leaves its trace: on a failure or a timeout every rank's tail is printed."""
+    import tempfile
+
     port = _free_port()
-    procs = []
+    logdir = str(tmp_path) if tmp_path is not None else tempfile.mkdtemp(prefix=f"tz_{case}_")
+    procs, logs = [], []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(extra_env or {}))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_rank_body.py"), case],
-                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                                      text=True))
-    outs = []
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TZ_TEST_VERBOSE="1",
+                   PYTHONFAULTHANDLER="1", **(extra_env or {}))
+        path = os.path.join(logdir, f"{case}_rank{r}.log")
+        logs.append(path)
+        f = open(path, "w")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "gpu_rank_body.py"), case],
+                                      env=env, stdout=f, stderr=subprocess.STDOUT, text=True))
+        f.close()
+    import time
+
+    t0 = time.time()
     try:
         for p in procs:
-            outs.append(p.communicate(timeout=timeout)[0])
+            try:
+                p.wait(timeout=max(1.0, timeout - (time.time() - t0)))
+            except subprocess.TimeoutExpired:
+                pytest.fail(f"{case} on {world} ranks: no exit within {timeout} s\n" + _tails(logs))
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
+                p.wait()
     res = []
-    for p, o in zip(procs, outs):
-        assert p.returncode == 0, o[-3000:]
-        line = [x for x in o.splitlines() if x.startswith("RESULT ")][-1]
-        res.append(json.loads(line[len("RESULT "):]))
+    for r, p in enumerate(procs):
+        if p.returncode != 0:
+            pytest.fail(f"{case}: rank {r} exited with {p.returncode}\n" + _tails(logs))
+        with open(logs[r]) as f:
+            lines = [x for x in f.read().splitlines() if x.startswith("RESULT ")]
+        assert lines, _tails(logs)
+        res.append(json.loads(lines[-1][len("RESULT "):]))
     return res
 
 
