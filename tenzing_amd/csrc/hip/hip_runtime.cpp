@@ -91,11 +91,9 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
       uint64_t firedRun = 0;
       while (!stop_.load()) {
         std::this_thread::sleep_for(std::chrono::milliseconds(100));
-        double d = deadline_.load();
         if (grace > 0) {
-          // a claimed run: still not returned (kClaimed) or draining after its abort (kDraining)
-          const bool pending = (d == kClaimed || d == kDraining) && runGen_.load() == firedRun;
-          if (!pending) {
+          // a claimed wait: still not returned, or draining after its abort
+          if (!(deadline_.abort_pending() && runGen_.load() == firedRun)) {
             grace = 0;
           } else {
             if (wtime() > grace)
@@ -105,8 +103,7 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
             continue;
           }
         }
-        if (d <= 0 || wtime() <= d) continue;
-        if (!deadline_.compare_exchange_strong(d, kClaimed)) continue; // the run ended meanwhile
+        if (!deadline_.try_claim(wtime())) continue; // not armed, not expired, or just ended
         firedRun = runGen_.load();
         // counted before anything can end the run, so the run waits for the abort below
         std::shared_ptr<std::atomic<int>> pending = abortsPending_;
@@ -225,7 +222,11 @@ void HipRuntime::stream_wait(int waiter, int waitee) {
   TZ_HIP(hipStreamWaitEvent(S(native_stream(waiter)), ev, 0));
 }
 
-void HipRuntime::device_sync() { TZ_HIP(hipDeviceSynchronize()); }
+void HipRuntime::device_sync() {
+  // bounded like a run: work still in flight after a run returned (RCCL's own streams, copy
+  // engines) must not block the caller forever where no watchdog looks
+  guarded(watchdogS_, "a device synchronization", [] { TZ_HIP(hipDeviceSynchronize()); });
+}
 
 void HipRuntime::destroy_exec(void *exec) {
   if (!exec) return;
@@ -680,7 +681,16 @@ Json chrome_trace(const std::vector<HipRuntime::Span> &spans) {
   return out;
 }
 
-void HipRuntime::run(int64_t n) {
+void HipRuntime::guarded(double budget, const char *what, const std::function<void()> &body) {
+  if (guarding_) { // nested (an op of a run synchronizes the device): the run's deadline covers it
+    body();
+    return;
+  }
+  struct Flag {
+    bool &f;
+    explicit Flag(bool &x) : f(x) { f = true; }
+    ~Flag() { f = false; }
+  } flag(guarding_);
   ++runGen_;
   // a device abort flag still set (an earlier abort whose drain was cut short, or a transport
   // preflight that left it): drain and clear it, or every spinning kernel of this run would
@@ -689,33 +699,36 @@ void HipRuntime::run(int64_t n) {
     (void)hipDeviceSynchronize();
     kern::set_abort(false);
   }
-  const double t0 = wtime();
   if (watchdogS_ > 0) {
-    budget_ = watchdog_budget(n);
-    deadline_ = t0 + budget_.load();
+    budget_ = budget;
+    deadline_.arm(wtime() + budget);
   }
-  // the end of the run: one exchange against the watchdog's claim
+  // the end of the guarded wait: one exchange against the watchdog's claim
   auto finish = [&] {
-    if (deadline_.exchange(0) != kClaimed) return;
+    if (!deadline_.finish()) return;
     // aborted: let every kernel the abort released drain before the flag is cleared for the
-    // next run (kDraining keeps the watchdog's grace exit armed: a drain that never ends hits it)
-    deadline_ = kDraining;
+    // next run (draining keeps the watchdog's grace exit armed: a drain that never ends hits it)
     (void)hipDeviceSynchronize();
     kern::set_abort(false);
     // the communicator abort normally ends well before the run returns; give it a bounded wait
     // so that the caller sees RCCL marked dead (and the domain agreement sees it) on return
     for (const double until = wtime() + 10.0; abortsPending_->load() > 0 && wtime() < until;)
       std::this_thread::sleep_for(std::chrono::milliseconds(5));
-    deadline_ = 0;
-    TZ_THROW("watchdog: the run exceeded its " << budget_.load() << " s budget and was aborted");
+    deadline_.drained();
+    TZ_THROW("watchdog: " << what << " exceeded its " << budget_.load() << " s budget and was aborted");
   };
   try {
-    run_impl(n);
+    body();
   } catch (...) {
-    finish(); // throws the watchdog's error instead when it had claimed the run
+    finish(); // throws the watchdog's error instead when it had claimed the wait
     throw;
   }
   finish();
+}
+
+void HipRuntime::run(int64_t n) {
+  const double t0 = wtime();
+  guarded(watchdog_budget(n), "the run", [&] { run_impl(n); });
   // what the next run of this schedule may take: its longest per-iteration time so far
   const double per = (wtime() - t0) / double(std::max<int64_t>(1, n));
   expected_ = std::max(expected_.load(), per);

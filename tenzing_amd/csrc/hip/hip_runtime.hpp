@@ -26,6 +26,7 @@
 #pragma once
 
 #include "core/benchmark.hpp"
+#include "core/deadline_claim.hpp"
 
 #include <atomic>
 #include <functional>
@@ -133,6 +134,9 @@ private:
   bool recordable(const Sequence &seq) const;
   void *build_graph(int iterations, size_t &nodes, size_t &edges);
   void run_impl(int64_t n);
+  /// run `body` (a blocking wait on the device) under the watchdog with `budget` seconds
+  void guarded(double budget, const char *what, const std::function<void()> &body);
+  bool guarding_ = false; // inside guarded() (runs are issued from one thread)
 
   int device_ = 0;
   ExecMode mode_;
@@ -165,10 +169,7 @@ private:
   // longest per-iteration seconds of a run of the prepared schedule (read by the watchdog)
   std::atomic<double> expected_{0};
   std::atomic<int> fired_{0};
-  // > 0: the armed deadline of the current run; 0: no run; kClaimed: the watchdog claimed the
-  // run (set only by its CAS); kDraining: the aborted run is draining the device
-  static constexpr double kClaimed = -1, kDraining = -2;
-  std::atomic<double> deadline_{0};
+  DeadlineClaim deadline_; // the current guarded wait vs the watchdog (core/deadline_claim.hpp)
   std::atomic<double> budget_{0}; // seconds the current run was given
   std::atomic<uint64_t> runGen_{0};  // runs started so far
   // communicator aborts still running on their own threads (shared: a thread may outlive this)

@@ -6,6 +6,7 @@
 // Run: tenzing_amd/bin/tz-unit [filter]
 #include "core/benchmark.hpp"
 #include "core/ctrl.hpp"
+#include "core/deadline_claim.hpp"
 #include "core/health.hpp"
 #include "core/solve.hpp"
 
@@ -681,6 +682,50 @@ TEST(run_deadline_arms_and_cancels) {
   CHECK(d.remaining() < left);
   d.cancel();
   CHECK(!d.armed());
+}
+
+TEST(deadline_claim_run_ends_at_its_deadline) {
+  // a run that finishes right at its deadline must be either aborted or not, never
+  // half: the watchdog's claim succeeds iff the run's finish reports the abort
+  DeadlineClaim c;
+  CHECK(!c.try_claim(1.0)); // nothing armed
+  c.arm(10.0);
+  CHECK(!c.try_claim(9.0)); // not expired
+  CHECK(!c.finish());        // ended in time
+  CHECK(c.value() == 0);
+  CHECK(!c.try_claim(11.0)); // ended: nothing to claim
+  c.arm(10.0);
+  CHECK(c.try_claim(10.5));
+  CHECK(!c.try_claim(10.6)); // claimed once
+  CHECK(c.abort_pending());
+  CHECK(c.finish());
+  CHECK(c.abort_pending()); // draining
+  c.drained();
+  CHECK(!c.abort_pending() && c.value() == 0);
+  // the race: the waiter ends exactly while the watchdog sweeps past the deadline, many times
+  int claimed = 0, reported = 0, mismatched = 0;
+  for (int it = 0; it < 20000; ++it) {
+    DeadlineClaim r;
+    r.arm(1.0); // already expired for the watchdog (now = 2.0)
+    std::atomic<bool> go{false};
+    bool won = false;
+    std::thread wd([&] {
+      while (!go.load()) {
+      }
+      won = r.try_claim(2.0);
+    });
+    go = true;
+    const bool aborted = r.finish();
+    wd.join();
+    claimed += won;
+    reported += aborted;
+    mismatched += won != aborted;
+    if (aborted) r.drained();
+    CHECK(r.value() == 0);
+  }
+  CHECK(mismatched == 0);
+  CHECK(claimed == reported);
+  std::printf("  deadline race: %d of 20000 ends claimed by the watchdog, all reported\n", claimed);
 }
 
 TEST(runs_test_behaviour) {
