@@ -786,6 +786,29 @@ PYBIND11_MODULE(_tz, m) {
   m.def("make_rccl_comms", &make_rccl_comms, py::arg("ctrl"), py::arg("device"), py::arg("n"),
         "n communicators over the same ranks (one per logical stream), one broadcast of ids");
 
+  // device memory without torch (TZ_NO_TORCH runs, tests on the system ROCm runtime)
+  py::class_<DeviceBuffer, std::shared_ptr<DeviceBuffer>>(m, "DeviceBuffer")
+      .def(py::init([](size_t bytes) {
+             TZ_CHECK(bytes > 0, "a device buffer needs at least one byte");
+             return std::make_shared<DeviceBuffer>(bytes);
+           }), py::arg("bytes"))
+      .def_property_readonly("ptr", [](const DeviceBuffer &b) { return reinterpret_cast<uintptr_t>(b.get()); })
+      .def_property_readonly("bytes", &DeviceBuffer::bytes)
+      .def("zero", [](DeviceBuffer &b) { TZ_HIP(hipMemset(b.get(), 0, b.bytes())); })
+      .def("to_bytes", [](const DeviceBuffer &b) {
+        std::string s(b.bytes(), '\0');
+        {
+          py::gil_scoped_release r;
+          b.download(&s[0], s.size());
+        }
+        return py::bytes(s);
+      }, "synchronous copy of the whole buffer to the host")
+      .def("from_bytes", [](DeviceBuffer &b, const py::bytes &data) {
+        const std::string s = data;
+        TZ_CHECK(s.size() <= b.bytes(), "from_bytes: " << s.size() << " bytes into " << b.bytes());
+        b.upload(s.data(), s.size());
+      });
+
   // ------------------------------------------------------------------ communication ops
   py::class_<CommOp, GpuOp, std::shared_ptr<CommOp>>(m, "CommOp")
       .def_property_readonly("dtype", &CommOp::dtype)

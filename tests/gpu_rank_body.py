@@ -231,21 +231,20 @@ def main():
         # an RCCL send/recv node beside two independent ~200 us kernels, all three on different
         # streams of one hipGraph: with whole-schedule capture the RCCL node must overlap the
         # kernels (one launch ~ one kernel), and the received data must follow every new value
-        # generation of the send buffer
+        # generation of the send buffer. Native buffers only: runs without torch (TZ_NO_TORCH=1,
+        # the system ROCm runtime) as well as on torch's bundled one
         import time
 
-        import torch
-        from tenzing_amd.ops import comm
+        import numpy as np
 
+        K = tz._tz.kernels
         W, R = ctrl.size, ctrl.rank
         n = int(os.environ.get("TZ_TEST_N", str(1 << 12)))
         us = float(os.environ.get("TZ_TEST_BUSY_US", "200"))
-        torch.cuda.set_device(dev)
-        f64 = dict(dtype=torch.float64, device=f"cuda:{dev}")
         comms = tz._tz.make_rccl_comms(ctrl, dev, 3)
-        a, c = torch.zeros(n, **f64), torch.zeros(n, **f64)
+        a, c = tz._tz.DeviceBuffer(8 * n), tz._tz.DeviceBuffer(8 * n)
         nxt, prv = (R + 1) % W, (R - 1) % W
-        sr = comm.send_recv("sr", comms, a, nxt, c, prv)
+        sr = tz.SendRecvOp("sr", comms, a.ptr, n, nxt, c.ptr, n, prv, 1, keep=(a, c))
         ka, kb = tz.BusyKernelOp("busy_a", us), tz.BusyKernelOp("busy_b", us)
         g = tz.Graph()
         for op in (ka, kb, sr):
@@ -262,19 +261,21 @@ def main():
         seq = tz.OpIndex(g).sequence_from_json(ctrl.bcast(msg, 0).decode())
         rt = tz.HipRuntime(device=dev, n_streams=3, mode=tz.ExecMode.Graph, watchdog_s=60.0)
         rt.prepare(seq)
+        say("prepared", seq.desc())
         out["effective_mode"] = str(rt.effective_mode)
         out["graph_nodes"] = rt.graph_nodes
-        idx = torch.arange(n, **f64)
+        idx = np.arange(n, dtype=np.float64)
         bad = []
         for gen in (1, 2, 3):
-            a.copy_(idx + 1000.0 * (R + 1) + 7.0 * gen)
-            c.zero_()
-            torch.cuda.synchronize()
+            K.iota_f64(n, 1000.0 * (R + 1) + 7.0 * gen, 1.0, a.ptr, 0)
+            c.zero()
+            rt.device_sync()
             ctrl.barrier()
             rt.run(1)
             rt.device_sync()
+            got = np.frombuffer(c.to_bytes(), dtype=np.float64)
             want = idx + 1000.0 * (prv + 1) + 7.0 * gen
-            bad.append(int((c != want).sum()))
+            bad.append(int((got != want).sum()))
             say("gen", gen, "bad", bad[-1])
         out["bad"] = bad
         iters = int(os.environ.get("TZ_TEST_ITERS", "50"))
@@ -304,6 +305,8 @@ def main():
         rt.device_sync()
         out["rccl_alone_us"] = (time.perf_counter() - t0) / iters * 1e6
         out["capture"] = os.environ.get("TZ_GRAPH_CAPTURE", "schedule")
+        from tenzing_amd.utils.env import runtime_libraries
+        out["runtime"] = runtime_libraries()
         del rt
     elif case == "ipc_abort":
         # a candidate that hangs on rank 0 (a spinning kernel ahead of its puts): the watchdogs
