@@ -3,6 +3,7 @@
 
 #include <arpa/inet.h>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <netdb.h>
@@ -68,6 +69,11 @@ void recv_all(int fd, void *buf, size_t n) {
     ssize_t r = ::recv(fd, p, n, 0);
     if (r < 0) {
       if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK)
+        // the peer's socket timeout (TZ_CTRL_TIMEOUT_S): a rank stuck outside every watchdog
+        // ends the job with this message instead of leaving every other rank blocked silently
+        TZ_THROW("ctrl: no message from a peer rank within the control-plane timeout "
+                 "(TZ_CTRL_TIMEOUT_S); that rank is hung or gone");
       TZ_THROW("ctrl recv failed: " << std::strerror(errno));
     }
     if (r == 0) TZ_THROW("ctrl peer closed connection");
@@ -90,6 +96,17 @@ std::string recv_frame(int fd) {
 void nodelay(int fd) {
   int one = 1;
   ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+}
+/// receive timeout of a joined peer socket: env TZ_CTRL_TIMEOUT_S (default 900 s: above any
+/// search step, below "forever"; 0 = none)
+void peer_timeout(int fd) {
+  double t = 900.0;
+  if (const char *v = std::getenv("TZ_CTRL_TIMEOUT_S")) t = std::atof(v);
+  if (t <= 0) return;
+  timeval tv{};
+  tv.tv_sec = long(t);
+  tv.tv_usec = long((t - double(tv.tv_sec)) * 1e6);
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
 }
 } // namespace
 
@@ -179,7 +196,10 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
       ++joined;
     }
     // release everyone
-    for (int i = 1; i < size_; ++i) send_all(peers_[i], &kWelcome, sizeof(kWelcome));
+    for (int i = 1; i < size_; ++i) {
+      send_all(peers_[i], &kWelcome, sizeof(kWelcome));
+      peer_timeout(peers_[i]);
+    }
     return;
   }
   addrinfo hints{}, *res = nullptr;
@@ -207,6 +227,7 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
   uint32_t w = 0;
   recv_all(fd, &w, sizeof(w));
   TZ_CHECK(w == kWelcome, "ctrl rendezvous: " << host << ":" << port << " is not this job's rank 0");
+  peer_timeout(fd);
   peers_[0] = fd;
 }
 

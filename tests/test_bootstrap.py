@@ -168,3 +168,38 @@ def test_peer_device_facts_fake_two_device_topology():
     assert q["same_device"] is True and q["can_access_peer"] is None
     assert q["ipc_mapping_consistent"] is True
     assert lo["summary"] == "all 1 peer(s) on this rank's own device (loopback)"
+
+
+def test_silent_peer_times_out_with_a_message():
+    """a rank that stops talking (hung outside every watchdog) ends its peers' collectives with
+    a clear error after TZ_CTRL_TIMEOUT_S, instead of blocking them forever"""
+    port = _free_port()
+    body = r"""
+import os, sys, time
+sys.path.insert(0, os.environ["TZ_ROOT"])
+from tenzing_amd.parallel import init_ctrl
+c = init_ctrl(timeout_s=60)
+if c.rank == 1:
+    time.sleep(8)
+    sys.exit(0)
+t0 = time.time()
+try:
+    c.barrier()
+    print("NO-TIMEOUT")
+except Exception as e:
+    print("TIMEOUT %.1f %s" % (time.time() - t0, e))
+"""
+    env = dict(os.environ, TZ_NO_TORCH="1", TZ_ROOT=ROOT, MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), WORLD_SIZE="2", TZ_CTRL_TIMEOUT_S="1.5")
+    ps = [subprocess.Popen([sys.executable, "-c", body], env=dict(env, RANK=str(r)),
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in (0, 1)]
+    try:
+        out0 = ps[0].communicate(timeout=60)[0]
+        ps[1].communicate(timeout=60)
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+    line = [x for x in out0.splitlines() if x.startswith(("TIMEOUT", "NO-TIMEOUT"))][-1]
+    assert line.startswith("TIMEOUT"), out0
+    assert float(line.split()[1]) < 6.0 and "hung or gone" in line
