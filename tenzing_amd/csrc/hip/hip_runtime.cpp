@@ -291,8 +291,15 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
   std::vector<std::vector<NodeSet>> nodes(nS);
   size_t edges = 0;
   hipGraph_t graph = nullptr;
+  // a schedule with RCCL ops between ranks is built the way the RCCL preflight found exact
+  bool rccl = false;
+  for (const auto &e : seq_.entries)
+    if (e.op->op_class() == OpClass::BoundGpu &&
+        static_cast<const BoundGpuOp &>(*e.op).unbound()->order_domain() == "rccl")
+      rccl = true;
+  const CaptureMode mode = rccl && rccl_multi_rank() ? rccl_capture_mode() : capture_mode();
   {
-    GraphBuilder gb(streams_, capture_mode());
+    GraphBuilder gb(streams_, mode);
     // replaying the sequence `iterations` times through one model orders iteration i+1 after
     // iteration i exactly as the schedule's closing host syncs do in eager mode
     for (int it = 0; it < iterations; ++it)
@@ -338,7 +345,7 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
     graph = nullptr;
     nodesOut = real;
     edgesOut = edges;
-    TZ_LOG(Debug, "graph mode (" << capture_mode_name(capture_mode()) << " capture): " << iterations
+    TZ_LOG(Debug, "graph mode (" << capture_mode_name(mode) << " capture): " << iterations
                                  << " iteration(s), " << real << " nodes, " << edges << " edges");
     // upload once so the first timed launch does not pay for it
     try {
@@ -365,6 +372,21 @@ CaptureMode capture_mode() {
   }();
   return m;
 }
+
+bool capture_mode_forced() {
+  static const bool forced = std::getenv("TZ_GRAPH_CAPTURE") != nullptr;
+  return forced;
+}
+
+namespace {
+std::atomic<int> g_rcclCapture{int(CaptureMode::Schedule)};
+}
+
+CaptureMode rccl_capture_mode() {
+  return capture_mode_forced() ? capture_mode() : CaptureMode(g_rcclCapture.load());
+}
+
+void set_rccl_capture_mode(CaptureMode m) { g_rcclCapture = int(m); }
 
 const char *capture_mode_name(CaptureMode m) {
   return m == CaptureMode::Child ? "child" : "schedule";

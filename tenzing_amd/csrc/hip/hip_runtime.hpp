@@ -195,7 +195,14 @@ Json chrome_trace(const std::vector<HipRuntime::Span> &spans);
 ///    node. Kept only for A/B diagnosis: HIP runs child-graph nodes one after another, so it
 ///    costs all branch concurrency (profiles/r3b_rccl_loopback/child_graph_overlap.jsonl).
 enum class CaptureMode { Schedule, Child };
+/// the mode for schedules without RCCL between ranks (env TZ_GRAPH_CAPTURE, default Schedule)
 CaptureMode capture_mode();
+/// whether TZ_GRAPH_CAPTURE was set (then it holds for every schedule, RCCL ones included)
+bool capture_mode_forced();
+/// the mode for schedules with RCCL ops between ranks: whichever the RCCL preflight found exact
+/// on every rank (Schedule first, Child as the fallback); Schedule until a preflight sets it
+CaptureMode rccl_capture_mode();
+void set_rccl_capture_mode(CaptureMode m);
 const char *capture_mode_name(CaptureMode m);
 
 /// Builds one hipGraph from ops enqueued on a fixed set of streams (hipStream_t as void*;

@@ -433,22 +433,14 @@ void HaloExchange::setup(Ctrl *ctrl) {
   if (useRccl_) {
     // a transfer that could hang or deliver wrong data must show up here, bounded, and not
     // mid-search on every rank: one verified exchange per form the search can build
-    std::string graphWhy;
-    std::string why = rccl_preflight_local(&graphWhy);
-    double bad[2] = {why.empty() ? 0.0 : 1.0, graphWhy.empty() ? 0.0 : 1.0};
-    ctrl->allreduce_max(bad, 2);
-    if (bad[0] != 0.0) {
-      drop_rccl("preflight: " + (why.empty() ? std::string("failed on another rank") : why));
+    const std::string why = rccl_preflight(*ctrl);
+    if (!why.empty()) {
+      drop_rccl("preflight: " + why);
     } else {
-      if (bad[1] != 0.0) {
-        // every rank alike: RCCL ops are left out of hipGraphs (candidates with them run eagerly)
-        rcclGraphOk_ = false;
-        rcclGraphWhy_ = graphWhy.empty() ? "hipGraph preflight failed on another rank" : graphWhy;
-        TZ_LOG(Warn, "RCCL ops run eagerly only: " << rcclGraphWhy_);
-      }
+      if (!rcclGraphOk_) TZ_LOG(Warn, "RCCL ops run eagerly only: " << rcclGraphWhy_);
       TZ_LOG(Info, "rccl preflight passed (" << comms_.size() << " communicators of "
                                              << rccl_nranks() << " ranks)"
-                                             << (rcclGraphOk_ ? "" : ", eager only"));
+                                             << (rcclGraphOk_ ? ", " + rcclCaptureNote_ : ", eager only"));
     }
     init_grid();
   }
@@ -511,7 +503,9 @@ std::map<std::string, std::string> HaloExchange::transport_report() const {
   std::map<std::string, std::string> r;
   const bool remote = std::any_of(nbr_.begin(), nbr_.end(), [&](int n) { return n != a_.rank; });
   const std::string &t = a_.transport;
-  if (useRccl_) r["rccl"] = rcclGraphOk_ ? "ok" : "ok (eager only: " + rcclGraphWhy_ + ")";
+  if (useRccl_)
+    r["rccl"] = rcclGraphOk_ ? (rcclCaptureNote_.empty() ? "ok" : "ok (hipGraph: " + rcclCaptureNote_ + ")")
+                             : "ok (eager only: " + rcclGraphWhy_ + ")";
   else if (!rcclWhy_.empty()) r["rccl"] = rcclWhy_;
   else r["rccl"] = "not offered";
   if (useIpc_ && ipcReady_) r["ipc"] = "ok";
@@ -545,23 +539,26 @@ bool HaloExchange::bounded_wait(void *stream, double seconds) const {
   }
 }
 
-std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
+std::string HaloExchange::rccl_preflight(Ctrl &ctrl) {
   std::vector<int> local, remote;
   for (int i = 0; i < ndirs(); ++i) {
     if (direct_[i]) local.push_back(i);
     else if (pipe_[i]) remote.push_back(i);
   }
-  if (remote.empty() || comms_.empty()) return "";
+  // every rank takes the same steps (the exchanges are collective): whether to run them at all
+  // is agreed first
+  double none = remote.empty() || comms_.empty() ? 1.0 : 0.0;
+  ctrl.allreduce_max(&none, 1);
+  if (none != 0.0) return "";
   double limit = 20.0;
   if (const char *v = std::getenv("TZ_RCCL_PREFLIGHT_S")) limit = std::atof(v);
   const std::string failEnv = std::getenv("TZ_FAIL_TRANSPORTS") ? std::getenv("TZ_FAIL_TRANSPORTS") : "";
   const bool simHang = ("," + failEnv + ",").find(",rccl_hang,") != std::string::npos;
+  const bool simGraph = ("," + failEnv + ",").find(",rccl_graph_schedule,") != std::string::npos;
   hipStream_t s = nullptr, side[2] = {nullptr, nullptr};
   TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   for (auto &x : side) TZ_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   std::string why;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
   // a hung exchange: release every spinning kernel first (an abort may wait for the device),
   // then abort the communicators on a thread of their own (their kernels return; the abort
   // itself may block), drain the stream with a bound, clear the flag again
@@ -583,8 +580,18 @@ std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
     kern::set_abort(false);
     why = what + " (no completion within " + std::to_string(int(limit)) + " s; communicators aborted)";
   };
+  // whatever an error left enqueued must drain, with the same bound
+  auto drain_after_error = [&](const std::string &err) {
+    bool drained = false;
+    try {
+      drained = bounded_wait(s, limit);
+    } catch (const std::exception &) {
+      drained = true; // the stream reports an error: nothing left to wait for
+    }
+    if (!drained) hung("after an error: " + err);
+  };
+  // (1) eagerly, one direction at a time, the communicators in turn
   try {
-    // (1) eagerly, one direction at a time, the communicators in turn
     if (simHang) kern::busy_wait(int64_t(1) << 50, 1, s); // released by the abort flag
     if (!local.empty()) direct_group(local, s);
     for (size_t k = 0; k < remote.size(); ++k) {
@@ -598,15 +605,30 @@ std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
     } else if (const uint64_t bad = check_grid(s)) {
       why = "per-direction exchange: " + std::to_string(bad) + " wrong cells";
     }
-    if (why.empty()) {
-      // (2) compiled into hipGraphs the way the runtime compiles candidates (GraphBuilder, so
-      // RCCL ops take the same capture path): every remote direction in one group, then one
-      // RCCL node per direction with the communicators in turn, chained, over three streams of
-      // one capture. Each graph runs twice, with a new value generation in between: a hang is
-      // bounded, and a delivery of the previous launch's data fails the check
-      for (int form = 0; form < 2 && why.empty() && graphWhy->empty(); ++form) {
+  } catch (const std::exception &e) {
+    why = e.what();
+    drain_after_error(why);
+  }
+  {
+    double failed = why.empty() ? 0.0 : 1.0;
+    ctrl.allreduce_max(&failed, 1);
+    if (failed != 0.0 && why.empty()) why = "failed on another rank";
+  }
+  // (2) compiled into hipGraphs the way the runtime compiles candidates (GraphBuilder, so RCCL
+  // ops take the same capture path): every remote direction in one group, then one RCCL node
+  // per direction with the communicators in turn, chained, over three streams of one build.
+  // Each graph runs twice, with a new value generation in between: a hang is bounded, and a
+  // delivery of the previous launch's data fails the check. Capture modes are tried in turn
+  // (whole-schedule capture first), every rank in step; wrong data in one mode moves on to the
+  // next, a hang drops RCCL.
+  auto graph_step = [&](CaptureMode mode) -> std::string {
+    std::string wrong;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    try {
+      for (int form = 0; form < 2 && why.empty() && wrong.empty(); ++form) {
         {
-          GraphBuilder gb({s, side[0], side[1]}, capture_mode());
+          GraphBuilder gb({s, side[0], side[1]}, mode);
           std::vector<void *> tail = gb.add(0, {}, [&] {
             if (!local.empty()) direct_group(local, s);
             pack_group(remote, s);
@@ -629,38 +651,66 @@ std::string HaloExchange::rccl_preflight_local(std::string *graphWhy) {
         TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
         const char *what = form == 0 ? "fused hipGraph exchange" : "per-direction hipGraph exchange";
         const int gens[2][2] = {{1, 2}, {3, 1}}; // (generations are 0..3; 0 is the search's)
-        for (int launch = 1; launch <= 2 && why.empty() && graphWhy->empty(); ++launch) {
+        for (int launch = 1; launch <= 2 && why.empty() && wrong.empty(); ++launch) {
           init_grid(s, gens[form][launch - 1]);
           TZ_HIP(hipGraphLaunch(exec, s));
-          if (!bounded_wait(s, limit)) hung(what); // communicators aborted: RCCL is gone
-          else if (const uint64_t bad = check_grid(s))
-            // wrong data, nothing hung: RCCL stays, but its ops run eagerly only
-            *graphWhy = std::string(what) + ", launch " + std::to_string(launch) + ": " +
-                        std::to_string(bad) + " wrong cells";
+          if (!bounded_wait(s, limit)) {
+            hung(what); // communicators aborted: RCCL is gone
+          } else {
+            uint64_t bad = check_grid(s);
+            if (simGraph && mode == CaptureMode::Schedule) bad += 1; // tests: force the fallback
+            if (bad)
+              wrong = std::string(what) + ", launch " + std::to_string(launch) + ": " +
+                      std::to_string(bad) + " wrong cells";
+          }
         }
         (void)hipGraphExecDestroy(exec);
         exec = nullptr;
         (void)hipGraphDestroy(graph);
         graph = nullptr;
       }
+    } catch (const std::exception &e) {
+      // a capture or instantiation error is not a broken transport: RCCL stays for eager runs
+      wrong = e.what();
+      drain_after_error(wrong);
     }
-  } catch (const std::exception &e) {
-    why = e.what();
-    // whatever was enqueued must drain, with the same bound
-    bool drained = false;
-    try {
-      drained = bounded_wait(s, limit);
-    } catch (const std::exception &) {
-      drained = true; // the stream reports an error: nothing left to wait for
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    return wrong;
+  };
+  std::vector<CaptureMode> modes;
+  if (capture_mode_forced()) modes = {capture_mode()};
+  else modes = {CaptureMode::Schedule, CaptureMode::Child};
+  std::vector<std::string> tried;
+  bool chosen = false;
+  for (size_t m = 0; m < modes.size(); ++m) {
+    double flags[2] = {why.empty() ? 0.0 : 1.0, 0.0}; // [failed / hung, wrong data]
+    std::string wrong;
+    if (flags[0] == 0.0) {
+      wrong = graph_step(modes[m]);
+      flags[0] = why.empty() ? 0.0 : 1.0;
+      flags[1] = wrong.empty() ? 0.0 : 1.0;
     }
-    if (!drained) {
-      const std::string first = why;
-      hung("after an error");
-      why = first + "; " + why;
+    ctrl.allreduce_max(flags, 2);
+    if (flags[0] != 0.0) {
+      if (why.empty()) why = "failed on another rank";
+      break;
     }
+    if (flags[1] == 0.0) {
+      set_rccl_capture_mode(modes[m]);
+      rcclCaptureNote_ = std::string(capture_mode_name(modes[m])) + " capture";
+      if (!tried.empty()) rcclCaptureNote_ += " (" + tried.front() + ")";
+      chosen = true;
+      break;
+    }
+    tried.push_back(std::string(capture_mode_name(modes[m])) + " capture: " +
+                    (wrong.empty() ? "wrong data on another rank" : wrong));
   }
-  if (exec) (void)hipGraphExecDestroy(exec);
-  if (graph) (void)hipGraphDestroy(graph);
+  if (why.empty() && !chosen) {
+    // every rank alike: RCCL ops are left out of hipGraphs (candidates with them run eagerly)
+    rcclGraphOk_ = false;
+    for (const std::string &t : tried) rcclGraphWhy_ += (rcclGraphWhy_.empty() ? "" : "; ") + t;
+  }
   (void)hipStreamDestroy(s);
   for (auto &x : side) (void)hipStreamDestroy(x);
   return why;

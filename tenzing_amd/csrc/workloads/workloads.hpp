@@ -423,13 +423,16 @@ private:
   /// verified RCCL exchanges before the search may use RCCL: every direction on its own (each
   /// communicator in turn) eagerly, then one fused group compiled into a hipGraph, each under a
   /// bounded wait (a hang aborts the communicators instead of blocking). "" on success
-  std::string rccl_preflight_local(std::string *graphWhy);
+  /// collective: the verified RCCL exchanges (eager, then hipGraphs in each capture mode until
+  /// one is exact on every rank); returns why RCCL must be dropped ("" = it stays)
+  std::string rccl_preflight(Ctrl &ctrl);
   /// wait for `stream` up to `seconds`; false on timeout (the caller aborts)
   bool bounded_wait(void *stream, double seconds) const;
   void drop_rccl(const std::string &why); // RCCL unavailable: abort and release communicators
   std::string rcclWhy_, ipcWhy_;
   bool rcclGraphOk_ = true;
   std::string rcclGraphWhy_; // why RCCL ops are not captured into hipGraphs ("" = they are)
+  std::string rcclCaptureNote_; // which capture mode the graph preflight settled on, and why
   bool useHost_ = false;
   Ctrl *ctrl_ = nullptr; // the control plane of setup (host transport)
   HaloArgs a_;
