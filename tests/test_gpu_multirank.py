@@ -366,6 +366,20 @@ def test_bench_rejected_finalist_loopback(gpu):
 
 
 @rccl_loopback
+def test_rccl_node_overlaps_kernels_loopback(gpu):
+    """an RCCL send/recv between two real ranks as a node of a whole-schedule-captured hipGraph,
+    beside two independent ~200 us kernels on two other streams: exact data over three value
+    generations, and one launch costs about one kernel (the RCCL node runs concurrently; round
+    3's child graphs serialized every node: 424 us for the two kernels alone)"""
+    res = _launch("rccl_overlap", 2, extra_env={"TZ_RCCL_LOOPBACK": "1"})
+    for r in res:
+        assert r["effective_mode"] == "ExecMode.Graph" and r["bad"] == [0, 0, 0], r
+        # concurrent: about the longest branch, never the serial sum of the kernels
+        assert r["iter_us"] <= max(250.0, r["rccl_alone_us"] + 50.0), r
+        assert r["iter_us"] < 1.6 * r["one_kernel_us"], r
+
+
+@rccl_loopback
 @pytest.mark.parametrize("world", [2, 4])
 def test_rccl_halo_across_ranks_loopback(gpu, world):
     """RCCL between real ranks: each rank gets a host id of its own (TZ_RCCL_LOOPBACK=1), so
