@@ -22,6 +22,7 @@
 #include <execinfo.h>
 #include <sstream>
 #include <unistd.h>
+#include <vector>
 
 namespace py = pybind11;
 using namespace tz;
@@ -168,9 +169,18 @@ void crash_handler(int sig, siginfo_t *si, void *uc) {
 }
 void install_crash_handler() {
   if (std::getenv("TZ_NO_CRASH_TRACE")) return;
+  // an alternate signal stack for this (the main) thread: a stack overflow must still print
+  static std::vector<char> altstack(size_t(1) << 16);
+  stack_t ss{};
+  ss.ss_sp = altstack.data();
+  ss.ss_size = altstack.size();
+  sigaltstack(&ss, nullptr);
+  // warm backtrace() up: its first call loads the unwinder, which a signal handler must not do
+  void *warm[2];
+  (void)backtrace(warm, 2);
   struct sigaction sa {};
   sa.sa_sigaction = crash_handler;
-  sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+  sa.sa_flags = SA_SIGINFO | SA_RESETHAND | SA_ONSTACK;
   sigemptyset(&sa.sa_mask);
   sigaction(SIGSEGV, &sa, &g_prevSegv);
   sigaction(SIGABRT, &sa, &g_prevAbrt);

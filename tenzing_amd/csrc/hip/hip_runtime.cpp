@@ -176,6 +176,8 @@ void *HipRuntime::native_stream(int stream) {
 }
 
 int HipRuntime::stream_index(const void *native) const {
+  // an op being captured on the origin stream answers for its own logical stream
+  if (captureAs_ >= 0 && native == streams_[0]) return captureAs_;
   for (size_t i = 0; i < streams_.size(); ++i)
     if (streams_[i] == native) return int(i);
   return -1;
@@ -323,8 +325,17 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
           }
           std::sort(deps.begin(), deps.end());
           deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
-          hipStream_t st = S(streams_[s]);
-          NodeSet tails = gb.add(s, deps, [&] { b.unbound()->launch(st, *this); });
+          // captured on the origin stream: the op still sees its own logical stream index
+          // (communicator choice, per-stream resources) through stream_index()
+          captureAs_ = s;
+          NodeSet tails;
+          try {
+            tails = gb.add(s, deps, [&](void *cs) { b.unbound()->launch(cs, *this); });
+          } catch (...) {
+            captureAs_ = -1;
+            throw;
+          }
+          captureAs_ = -1;
           if (tails.empty()) {
             nodes[s].push_back(deps); // enqueued nothing: stands for its dependencies
           } else {
@@ -401,28 +412,10 @@ GraphBuilder::GraphBuilder(const std::vector<void *> &streams, CaptureMode mode)
     graph_ = g;
     return;
   }
-  // events first: nothing may be created once the capture runs
-  for (size_t i = 0; i <= streams_.size(); ++i) {
-    hipEvent_t ev = nullptr;
-    const hipError_t r = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (r != hipSuccess) {
-      abandon();
-      TZ_HIP(r);
-    }
-    forkJoin_.push_back(ev);
-  }
   hipStream_t origin = S(streams_[0]);
+  TZ_LOG(Debug, "capture: begin");
   TZ_HIP(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
   capturing_ = true;
-  try {
-    // fork: every other stream joins the capture behind the (empty) origin
-    TZ_HIP(hipEventRecord(E(forkJoin_[0]), origin));
-    for (size_t i = 1; i < streams_.size(); ++i)
-      TZ_HIP(hipStreamWaitEvent(S(streams_[i]), E(forkJoin_[0]), 0));
-  } catch (...) {
-    abandon();
-    throw;
-  }
 }
 
 GraphBuilder::~GraphBuilder() { abandon(); }
@@ -430,19 +423,10 @@ GraphBuilder::~GraphBuilder() { abandon(); }
 void GraphBuilder::abandon() {
   if (capturing_) {
     capturing_ = false;
-    // join every forked stream (an unjoined stream would stay in capture mode), then end
-    hipStream_t origin = S(streams_[0]);
-    for (size_t i = 1; i < streams_.size(); ++i) {
-      (void)hipEventRecord(E(forkJoin_[i]), S(streams_[i]));
-      (void)hipStreamWaitEvent(origin, E(forkJoin_[i]), 0);
-    }
     hipGraph_t g = nullptr;
-    (void)hipStreamEndCapture(origin, &g);
+    (void)hipStreamEndCapture(S(streams_[0]), &g);
     if (g) (void)hipGraphDestroy(g);
   }
-  for (void *e : forkJoin_)
-    if (e) (void)hipEventDestroy(E(e));
-  forkJoin_.clear();
   if (graph_) {
     (void)hipGraphDestroy(static_cast<hipGraph_t>(graph_));
     graph_ = nullptr;
@@ -450,17 +434,17 @@ void GraphBuilder::abandon() {
 }
 
 std::vector<void *> GraphBuilder::add(int stream, const std::vector<void *> &depsP,
-                                      const std::function<void()> &launch) {
+                                      const std::function<void(void *)> &launch) {
   TZ_CHECK(stream >= 0 && stream < int(streams_.size()), "stream " << stream << " out of range");
-  hipStream_t st = S(streams_[stream]);
   std::vector<hipGraphNode_t> deps;
   for (void *d : depsP) deps.push_back(static_cast<hipGraphNode_t>(d));
   std::vector<void *> tails;
   if (mode_ == CaptureMode::Child) {
+    hipStream_t st = S(streams_[stream]);
     hipGraph_t captured = nullptr;
     TZ_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     try {
-      launch();
+      launch(st);
     } catch (...) {
       (void)hipStreamEndCapture(st, &captured);
       if (captured) (void)hipGraphDestroy(captured);
@@ -483,14 +467,21 @@ std::vector<void *> GraphBuilder::add(int stream, const std::vector<void *> &dep
     return tails;
   }
   TZ_CHECK(capturing_, "graph build already finished");
-  // this op runs behind exactly its schedule dependencies, whatever the stream ran before
-  TZ_HIP(hipStreamUpdateCaptureDependencies(st, deps.empty() ? nullptr : deps.data(), deps.size(),
+  // every op is enqueued on the origin stream, behind exactly its schedule dependencies
+  // (whatever was captured before): in a graph only the edges exist, not the streams, so one
+  // capture stream suffices. It also keeps every side stream an op forks internally (RCCL's
+  // own streams, copy engines) joined to the origin itself: HIP 7.0's hipStreamEndCapture
+  // recursed without end when RCCL's streams had joined the capture through other forked
+  // streams (profiles/r4_capture/self_torchrt2.log)
+  hipStream_t origin = S(streams_[0]);
+  TZ_LOG(Debug, "capture: op of stream " << stream << " behind " << deps.size() << " node(s)");
+  TZ_HIP(hipStreamUpdateCaptureDependencies(origin, deps.empty() ? nullptr : deps.data(), deps.size(),
                                             hipStreamSetCaptureDependencies));
-  launch();
+  launch(origin);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   const hipGraphNode_t *d = nullptr;
   size_t nd = 0;
-  TZ_HIP(hipStreamGetCaptureInfo_v2(st, &cs, nullptr, nullptr, &d, &nd));
+  TZ_HIP(hipStreamGetCaptureInfo_v2(origin, &cs, nullptr, nullptr, &d, &nd));
   TZ_CHECK(cs == hipStreamCaptureStatusActive, "stream capture was invalidated by an op's launch");
   std::vector<hipGraphNode_t> after(d, d + nd);
   std::sort(after.begin(), after.end());
@@ -508,23 +499,12 @@ void *GraphBuilder::finish() {
     return g;
   }
   TZ_CHECK(capturing_, "graph build already finished");
-  hipStream_t origin = S(streams_[0]);
   capturing_ = false;
   hipGraph_t g = nullptr;
-  hipError_t r = hipSuccess;
-  for (size_t i = 1; i < streams_.size() && r == hipSuccess; ++i) {
-    r = hipEventRecord(E(forkJoin_[i]), S(streams_[i]));
-    if (r == hipSuccess) r = hipStreamWaitEvent(origin, E(forkJoin_[i]), 0);
-  }
-  if (r != hipSuccess) {
-    capturing_ = true; // abandon() joins what it can and ends the capture
-    abandon();
-    TZ_HIP(r);
-  }
-  TZ_HIP(hipStreamEndCapture(origin, &g));
+  TZ_LOG(Debug, "capture: ending");
+  TZ_HIP(hipStreamEndCapture(S(streams_[0]), &g));
   TZ_CHECK(g != nullptr, "stream capture produced no graph");
-  for (void *e : forkJoin_) (void)hipEventDestroy(E(e));
-  forkJoin_.clear();
+  TZ_LOG(Debug, "capture: ended");
   return g;
 }
 

@@ -137,6 +137,7 @@ private:
   /// run `body` (a blocking wait on the device) under the watchdog with `budget` seconds
   void guarded(double budget, const char *what, const std::function<void()> &body);
   bool guarding_ = false; // inside guarded() (runs are issued from one thread)
+  int captureAs_ = -1;    // graph build: the logical stream of the op being captured on the origin
 
   int device_ = 0;
   ExecMode mode_;
@@ -207,18 +208,22 @@ const char *capture_mode_name(CaptureMode m);
 
 /// Builds one hipGraph from ops enqueued on a fixed set of streams (hipStream_t as void*;
 /// streams[0] is the origin). The runtime's graph build and the transports' preflights share
-/// it, so a preflight tests exactly what candidates run. Not copyable; the destructor abandons
-/// an unfinished build (joins and ends the capture, destroys the partial graph).
+/// it, so a preflight tests exactly what candidates run. Schedule mode: one capture on the
+/// origin; every op is enqueued there (its launch receives the capture stream) behind exactly
+/// the dependencies given, so the graph has the schedule's edges and nothing else. Child mode:
+/// every op captured alone on its own stream and added as a child-graph node. Not copyable; the
+/// destructor abandons an unfinished build (ends the capture, destroys the partial graph).
 class GraphBuilder {
 public:
   GraphBuilder(const std::vector<void *> &streams, CaptureMode mode);
   ~GraphBuilder();
   GraphBuilder(const GraphBuilder &) = delete;
   GraphBuilder &operator=(const GraphBuilder &) = delete;
-  /// enqueue one op (`launch` issues its work on streams[stream]) behind `deps` (hipGraphNode_t
-  /// as void*). Returns the op's tail nodes; empty when it enqueued nothing.
+  /// enqueue one op of logical stream `stream` behind `deps` (hipGraphNode_t as void*):
+  /// `launch(captureStream)` issues its work. Returns the op's tail nodes; empty when it
+  /// enqueued nothing.
   std::vector<void *> add(int stream, const std::vector<void *> &deps,
-                          const std::function<void()> &launch);
+                          const std::function<void(void *)> &launch);
   /// end the build: the caller owns the returned hipGraph_t (as void*)
   void *finish();
   CaptureMode mode() const { return mode_; }
@@ -227,8 +232,7 @@ private:
   void abandon();
   std::vector<void *> streams_;
   CaptureMode mode_;
-  void *graph_ = nullptr;              // Child: the graph being assembled
-  std::vector<void *> forkJoin_;       // Schedule: fork event + one join event per stream
+  void *graph_ = nullptr; // Child: the graph being assembled
   bool capturing_ = false;
 };
 

@@ -591,6 +591,7 @@ std::string HaloExchange::rccl_preflight(Ctrl &ctrl) {
     if (!drained) hung("after an error: " + err);
   };
   // (1) eagerly, one direction at a time, the communicators in turn
+  TZ_LOG(Debug, "rccl preflight: eager step, " << remote.size() << " remote direction(s)");
   try {
     if (simHang) kern::busy_wait(int64_t(1) << 50, 1, s); // released by the abort flag
     if (!local.empty()) direct_group(local, s);
@@ -627,28 +628,30 @@ std::string HaloExchange::rccl_preflight(Ctrl &ctrl) {
     hipGraphExec_t exec = nullptr;
     try {
       for (int form = 0; form < 2 && why.empty() && wrong.empty(); ++form) {
+        TZ_LOG(Debug, "rccl preflight: graph step, " << capture_mode_name(mode) << " capture, form " << form);
         {
           GraphBuilder gb({s, side[0], side[1]}, mode);
-          std::vector<void *> tail = gb.add(0, {}, [&] {
-            if (!local.empty()) direct_group(local, s);
-            pack_group(remote, s);
+          std::vector<void *> tail = gb.add(0, {}, [&](void *cs) {
+            if (!local.empty()) direct_group(local, cs);
+            pack_group(remote, cs);
           });
           if (form == 0) {
-            tail = gb.add(0, tail, [&] { shift_group(remote, s, 0); });
+            tail = gb.add(0, tail, [&](void *cs) { shift_group(remote, cs, 0); });
           } else {
             // as schedules spread them: direction k on stream k % 3 with that stream's
             // communicator (comm_for), chained in one total order like the rccl ordering domain
             for (size_t k = 0; k < remote.size(); ++k) {
               const int si = int(k % 3);
-              hipStream_t sk = si == 0 ? s : side[si - 1];
-              std::vector<void *> t = gb.add(si, tail, [&] { shift(remote[k], sk, si); });
+              std::vector<void *> t = gb.add(si, tail, [&](void *cs) { shift(remote[k], cs, si); });
               if (!t.empty()) tail = t;
             }
           }
-          gb.add(0, tail, [&] { unpack_group(remote, s); });
+          gb.add(0, tail, [&](void *cs) { unpack_group(remote, cs); });
           graph = static_cast<hipGraph_t>(gb.finish());
         }
+        TZ_LOG(Debug, "rccl preflight: instantiate");
         TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        TZ_LOG(Debug, "rccl preflight: launch");
         const char *what = form == 0 ? "fused hipGraph exchange" : "per-direction hipGraph exchange";
         const int gens[2][2] = {{1, 2}, {3, 1}}; // (generations are 0..3; 0 is the search's)
         for (int launch = 1; launch <= 2 && why.empty() && wrong.empty(); ++launch) {

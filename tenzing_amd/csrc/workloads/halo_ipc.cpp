@@ -380,8 +380,35 @@ void HaloExchange::engine_copies(const std::vector<Copy> &copies, void *stream, 
   EngineSet &es = engines_for(stream);
   const int E = 1 + int(es.streams.size());
   hipEvent_t fork = static_cast<hipEvent_t>(es.events[0]);
-  TZ_HIP(hipEventRecord(fork, s));
-  for (int k = 1; k < E; ++k) TZ_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(es.streams[size_t(k - 1)]), fork, 0));
+  // fork: each engine stream starts behind exactly what `s` has enqueued so far. Inside a graph
+  // capture, an engine stream already in the capture gets that dependency set replaced (a plain
+  // event wait would ADD it to whatever the engine stream captured for an earlier op: a false
+  // edge between independent copy ops that share the engine set of the capture stream)
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long capId = 0;
+  const hipGraphNode_t *dp = nullptr;
+  size_t nd = 0;
+  TZ_HIP(hipStreamGetCaptureInfo_v2(s, &cs, &capId, nullptr, &dp, &nd));
+  std::vector<hipGraphNode_t> sDeps(dp, dp + nd);
+  bool recorded = false;
+  for (int k = 1; k < E; ++k) {
+    hipStream_t e = static_cast<hipStream_t>(es.streams[size_t(k - 1)]);
+    if (cs == hipStreamCaptureStatusActive) {
+      hipStreamCaptureStatus ce = hipStreamCaptureStatusNone;
+      unsigned long long eid = 0;
+      TZ_HIP(hipStreamGetCaptureInfo_v2(e, &ce, &eid, nullptr, nullptr, nullptr));
+      if (ce == hipStreamCaptureStatusActive && eid == capId) {
+        TZ_HIP(hipStreamUpdateCaptureDependencies(e, sDeps.empty() ? nullptr : sDeps.data(), sDeps.size(),
+                                                  hipStreamSetCaptureDependencies));
+        continue;
+      }
+    }
+    if (!recorded) {
+      TZ_HIP(hipEventRecord(fork, s));
+      recorded = true;
+    }
+    TZ_HIP(hipStreamWaitEvent(e, fork, 0));
+  }
   for (const Copy &c : copies) {
     const size_t per = (c.bytes / size_t(E) + 255) / 256 * 256;
     for (int k = 0; k < E; ++k) {
