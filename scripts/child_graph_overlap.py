@@ -37,7 +37,7 @@ def main():
     rt.run(n)
     rt.device_sync()
     dt = (time.perf_counter() - t0) / n
-    print(json.dumps({"capture": os.environ.get("TZ_GRAPH_CAPTURE", "schedule"), "nodes": rt.graph_nodes, "mode": str(rt.effective_mode),
+    print(json.dumps({"capture": os.environ.get("TZ_GRAPH_CAPTURE", "schedule"), "nodes": rt.graph_nodes(), "mode": str(rt.effective_mode),
                       "iter_us": dt * 1e6, "one_kernel_us": us}))
 
 

@@ -20,7 +20,7 @@ def main():
             seq = tz.random_rollout(tz.State(g, tz.Platform(2)), seed)
             halo.init_grid()
             rt.prepare(seq)
-            print(m, seed, "prepared", rt.effective_mode, rt.graph_nodes, flush=True)
+            print(m, seed, "prepared", rt.effective_mode, rt.graph_nodes(), flush=True)
             rt.run(1)
             rt.device_sync()
             b1 = halo.check_grid()

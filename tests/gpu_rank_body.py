@@ -263,7 +263,7 @@ def main():
         rt.prepare(seq)
         say("prepared", seq.desc())
         out["effective_mode"] = str(rt.effective_mode)
-        out["graph_nodes"] = rt.graph_nodes
+        out["graph_nodes"] = rt.graph_nodes()
         idx = np.arange(n, dtype=np.float64)
         bad = []
         for gen in (1, 2, 3):

@@ -27,11 +27,23 @@ print("RESULT " + json.dumps(dict(rank=c.rank, size=c.size, got=got, mx=mx, ag=a
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """a MASTER_PORT whose control port (MASTER_PORT + 1) is free as well"""
+    for _ in range(100):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        if p >= 65535:
+            continue
+        t = socket.socket()
+        try:
+            t.bind(("0.0.0.0", p + 1))
+        except OSError:
+            continue
+        finally:
+            t.close()
+        return p
+    raise RuntimeError("no free port pair")
 
 
 def _launch(world, port, extra=None, timeout=120):
