@@ -75,6 +75,7 @@ from ._tz import (  # noqa: E402,F401
     HaloArgs,
     HaloExchange,
     HipRuntime,
+    HostFuncOp,
     HostExecutor,
     MctsOpts,
     NoOp,

@@ -260,6 +260,7 @@ PYBIND11_MODULE(_tz, m) {
            py::arg("fn"), py::arg("cost_us") = 0.0, py::arg("capturable") = true,
            py::arg("domain") = "");
   py::class_<EmptyKernelOp, GpuOp, std::shared_ptr<EmptyKernelOp>>(m, "EmptyKernelOp").def(py::init<std::string>());
+  py::class_<HostFuncOp, GpuOp, std::shared_ptr<HostFuncOp>>(m, "HostFuncOp").def(py::init<std::string>());
   py::class_<BusyKernelOp, GpuOp, std::shared_ptr<BusyKernelOp>>(m, "BusyKernelOp")
       .def(py::init<std::string, double, int>(), py::arg("name"), py::arg("us"), py::arg("blocks") = 1);
   py::class_<BoundGpuOp, BoundOp, std::shared_ptr<BoundGpuOp>>(m, "BoundGpuOp")
@@ -689,6 +690,8 @@ PYBIND11_MODULE(_tz, m) {
       .def("graph_nodes", &HipRuntime::graph_nodes)
       .def("graph_edges", &HipRuntime::graph_edges)
       .def("num_streams", &HipRuntime::num_streams)
+      .def("graph_node_types", &HipRuntime::graph_node_types,
+           "node count by type of the compiled graph (kernel, host, memcpy, event_record, ...)")
       .def("native_stream", [](HipRuntime &r, int s) { return reinterpret_cast<uintptr_t>(r.native_stream(s)); })
       .def("device_sync", &HipRuntime::device_sync, py::call_guard<py::gil_scoped_release>())
       .def("set_watchdog", &HipRuntime::set_watchdog, py::arg("floor_s"), py::arg("k") = -1.0)

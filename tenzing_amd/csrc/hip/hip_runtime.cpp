@@ -263,6 +263,36 @@ void HipRuntime::destroy_graph() {
   }
 }
 
+std::map<std::string, int> HipRuntime::graph_node_types() const {
+  std::map<std::string, int> out;
+  if (!graphExec_) return out;
+  auto it = graphOf_.find(graphExec_);
+  if (it == graphOf_.end()) return out;
+  hipGraph_t g = static_cast<hipGraph_t>(it->second);
+  size_t n = 0;
+  TZ_HIP(hipGraphGetNodes(g, nullptr, &n));
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) TZ_HIP(hipGraphGetNodes(g, nodes.data(), &n));
+  for (hipGraphNode_t x : nodes) {
+    hipGraphNodeType t;
+    TZ_HIP(hipGraphNodeGetType(x, &t));
+    const char *name = "other";
+    switch (t) {
+    case hipGraphNodeTypeKernel: name = "kernel"; break;
+    case hipGraphNodeTypeMemcpy: name = "memcpy"; break;
+    case hipGraphNodeTypeMemset: name = "memset"; break;
+    case hipGraphNodeTypeHost: name = "host"; break;
+    case hipGraphNodeTypeGraph: name = "child_graph"; break;
+    case hipGraphNodeTypeEmpty: name = "empty"; break;
+    case hipGraphNodeTypeWaitEvent: name = "event_wait"; break;
+    case hipGraphNodeTypeEventRecord: name = "event_record"; break;
+    default: break;
+    }
+    ++out[name];
+  }
+  return out;
+}
+
 bool HipRuntime::recordable(const Sequence &seq) const {
   for (const auto &e : seq.entries) {
     const OpClass c = e.op->op_class();

@@ -30,6 +30,7 @@
 
 #include <atomic>
 #include <functional>
+#include <map>
 #include <memory>
 #include <string>
 #include <thread>
@@ -94,6 +95,9 @@ public:
   size_t graph_nodes() const { return graphNodes_; }
   /// number of dependency edges of the compiled graph
   size_t graph_edges() const { return graphEdges_; }
+  /// node count by type of the compiled single-iteration graph ("kernel", "host", "memcpy",
+  /// "event_record", ...; empty in eager mode)
+  std::map<std::string, int> graph_node_types() const;
   void set_watchdog(double s, double k = -1) {
     watchdogS_ = s;
     if (k >= 0) watchdogK_ = k;

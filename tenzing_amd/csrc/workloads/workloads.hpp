@@ -119,6 +119,20 @@ private:
   std::string name_;
 };
 
+/// a host function enqueued on the stream (hipLaunchHostFunc; a host node when captured): what
+/// RCCL's network proxies add to a captured schedule. Diagnostic op for graph-concurrency probes
+class HostFuncOp : public GpuOp {
+public:
+  explicit HostFuncOp(std::string name) : name_(std::move(name)) {}
+  std::string name() const override { return name_; }
+  std::string kind() const override { return "HostFunc"; }
+  double cost_us() const override { return 5.0; }
+  void launch(void *stream, Executor &) const override;
+
+private:
+  std::string name_;
+};
+
 /// a kernel that occupies `blocks` workgroups for `us` microseconds
 class BusyKernelOp : public GpuOp {
 public:

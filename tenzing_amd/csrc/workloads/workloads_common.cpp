@@ -139,6 +139,12 @@ std::string node_identity() {
 
 void EmptyKernelOp::launch(void *stream, Executor &) const { kern::empty(stream); }
 
+static void host_noop(void *) {}
+
+void HostFuncOp::launch(void *stream, Executor &) const {
+  TZ_HIP(hipLaunchHostFunc(static_cast<hipStream_t>(stream), host_noop, nullptr));
+}
+
 Json BusyKernelOp::json() const {
   Json j;
   j["name"] = name_;

@@ -245,17 +245,19 @@ def main():
         a, c = tz._tz.DeviceBuffer(8 * n), tz._tz.DeviceBuffer(8 * n)
         nxt, prv = (R + 1) % W, (R - 1) % W
         sr = tz.SendRecvOp("sr", comms, a.ptr, n, nxt, c.ptr, n, prv, 1, keep=(a, c))
-        ka, kb = tz.BusyKernelOp("busy_a", us), tz.BusyKernelOp("busy_b", us)
+        kernels = [tz.BusyKernelOp("busy_a", us), tz.BusyKernelOp("busy_b", us)]
+        kernels = kernels[:int(os.environ.get("TZ_TEST_OVERLAP_KERNELS", "2"))]
         g = tz.Graph()
-        for op in (ka, kb, sr):
+        for op in kernels + [sr]:
             g.start_then(op)
             g.then_finish(op)
+        names = [o.name for o in kernels] + ["sr"]
         msg = ""
         if R == 0:
             for seed in range(400):
                 s = tz.random_rollout(tz.State(g, tz.Platform(3)), seed)
-                st = {o.name: o.stream for o in s.ops() if o.name in ("busy_a", "busy_b", "sr")}
-                if len(set(st.values())) == 3:
+                st = {o.name: o.stream for o in s.ops() if o.name in names}
+                if len(set(st.values())) == len(names):
                     msg = s.json(True)
                     break
         seq = tz.OpIndex(g).sequence_from_json(ctrl.bcast(msg, 0).decode())
@@ -264,6 +266,8 @@ def main():
         say("prepared", seq.desc())
         out["effective_mode"] = str(rt.effective_mode)
         out["graph_nodes"] = rt.graph_nodes()
+        out["node_types"] = rt.graph_node_types()
+        out["kernels"] = len(kernels)
         idx = np.arange(n, dtype=np.float64)
         bad = []
         for gen in (1, 2, 3):
