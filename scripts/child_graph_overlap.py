@@ -3,10 +3,12 @@ one hipGraph by the runtime, in one whole-schedule capture (TZ_GRAPH_CAPTURE=sch
 default) or as child graphs (TZ_GRAPH_CAPTURE=child; the env is read once per process, so run
 this script once per setting).
 
-  python scripts/child_graph_overlap.py [kernels|host]
+  python scripts/child_graph_overlap.py [kernels|host|kernel3|hostchain|chainhost]
 
 kernels: two busy kernels (one workgroup each, ~200 us); host: the same plus a host function
-(hipLaunchHostFunc, a host node: what RCCL's network proxies add) on a third stream. Prints one
+(hipLaunchHostFunc, a host node: what RCCL's network proxies add) on a third stream; kernel3: a
+third, 50 us kernel instead (control); hostchain / chainhost: a third branch of a host node then
+a 50 us kernel (RCCL's shape over its network transport) / the other order. Prints one
 JSON line: per-iteration time, the serial time of one kernel, the graph's node types."""
 import json
 import os
@@ -22,19 +24,30 @@ def main():
     variant = sys.argv[1] if len(sys.argv) > 1 else "kernels"
     us = 200.0
     ops = [tz.BusyKernelOp("a", us), tz.BusyKernelOp("b", us)]
+    chain = []  # (first, second): one branch of two ops in order, on a stream of its own
     if variant == "host":
         ops.append(tz.HostFuncOp("h"))
-    names = [o.name for o in ops]
+    elif variant == "kernel3":  # control: a third, short kernel branch
+        ops.append(tz.BusyKernelOp("c", 50.0))
+    elif variant == "hostchain":  # RCCL's shape: a host node, then a kernel behind it
+        chain = [tz.HostFuncOp("h"), tz.BusyKernelOp("c", 50.0)]
+    elif variant == "chainhost":  # the other order: a kernel, then a host node
+        chain = [tz.BusyKernelOp("c", 50.0), tz.HostFuncOp("h")]
+    names = [o.name for o in ops] + ([chain[0].name] if chain else [])
     g = tz.Graph()
     for op in ops:
         g.start_then(op)
         g.then_finish(op)
-    ns = len(ops)
+    if chain:
+        g.start_then(chain[0])
+        g.then(chain[0], chain[1])
+        g.then_finish(chain[1])
+    ns = len(names)
     seq = None
-    for seed in range(400):  # a schedule with every op on a stream of its own
+    for seed in range(2000):  # every branch on a stream of its own, a chain on one stream
         s = tz.random_rollout(tz.State(g, tz.Platform(ns)), seed)
-        st = {o.name: o.stream for o in s.ops() if o.name in names}
-        if len(set(st.values())) == ns:
+        st = {o.name: o.stream for o in s.ops() if o.name in names + [c.name for c in chain]}
+        if len({st[n] for n in names}) == ns and (not chain or st[chain[0].name] == st[chain[1].name]):
             seq = s
             break
     rt = tz.HipRuntime(device=0, n_streams=ns, mode=tz.ExecMode.Graph)
