@@ -29,6 +29,8 @@ def main():
         ops.append(tz.HostFuncOp("h"))
     elif variant == "kernel3":  # control: a third, short kernel branch
         ops.append(tz.BusyKernelOp("c", 50.0))
+    elif variant == "kernel4":  # and a fourth
+        ops += [tz.BusyKernelOp("c", 50.0), tz.BusyKernelOp("d", 50.0)]
     elif variant == "hostchain":  # RCCL's shape: a host node, then a kernel behind it
         chain = [tz.HostFuncOp("h"), tz.BusyKernelOp("c", 50.0)]
     elif variant == "chainhost":  # the other order: a kernel, then a host node
@@ -50,7 +52,8 @@ def main():
         if len({st[n] for n in names}) == ns and (not chain or st[chain[0].name] == st[chain[1].name]):
             seq = s
             break
-    rt = tz.HipRuntime(device=0, n_streams=ns, mode=tz.ExecMode.Graph)
+    eager = os.environ.get("TZ_OVERLAP_EAGER") == "1"
+    rt = tz.HipRuntime(device=0, n_streams=ns, mode=tz.ExecMode.Eager if eager else tz.ExecMode.Graph)
     rt.prepare(seq)
     rt.run(5)
     rt.device_sync()
