@@ -26,10 +26,10 @@ def _free_port():
 
 
 # RCCL between loopback ranks goes through RCCL's socket transport with every rank's kernels on
-# one GPU: exercised on demand (TZ_TEST_RCCL_LOOPBACK=1), not in the default suite, because one
-# full-suite run hung in it (profiles/r3b_rccl_loopback/README.md)
-rccl_loopback = pytest.mark.skipif(os.environ.get("TZ_TEST_RCCL_LOOPBACK") != "1",
-                                   reason="RCCL across loopback ranks: set TZ_TEST_RCCL_LOOPBACK=1")
+# one GPU. Part of the default suite again since round 4 (whole-schedule capture; every rank's
+# log kept as it runs); TZ_TEST_NO_RCCL_LOOPBACK=1 skips them
+rccl_loopback = pytest.mark.skipif(os.environ.get("TZ_TEST_NO_RCCL_LOOPBACK") == "1",
+                                   reason="RCCL across loopback ranks skipped (TZ_TEST_NO_RCCL_LOOPBACK=1)")
 
 
 def _tails(logs, n=40):
@@ -369,14 +369,17 @@ def test_bench_rejected_finalist_loopback(gpu):
 def test_rccl_node_overlaps_kernels_loopback(gpu):
     """an RCCL send/recv between two real ranks as a node of a whole-schedule-captured hipGraph,
     beside two independent ~200 us kernels on two other streams: exact data over three value
-    generations, and one launch costs about one kernel (the RCCL node runs concurrently; round
-    3's child graphs serialized every node: 424 us for the two kernels alone)"""
+    generations; the RCCL node (a kernel plus its network proxy's host node) is an ordinary
+    branch of the graph, so the two kernels still overlap (round 3's child graphs serialized
+    every node: 424 us for the two kernels alone). HIP's graph executor runs a third branch of
+    any kind partly behind the first two (~295 us with a 50 us kernel instead of RCCL,
+    profiles/r4_capture/), which the bound allows for"""
     res = _launch("rccl_overlap", 2, extra_env={"TZ_RCCL_LOOPBACK": "1"})
     for r in res:
         assert r["effective_mode"] == "ExecMode.Graph" and r["bad"] == [0, 0, 0], r
-        # concurrent: about the longest branch, never the serial sum of the kernels
-        assert r["iter_us"] <= max(250.0, r["rccl_alone_us"] + 50.0), r
-        assert r["iter_us"] < 1.6 * r["one_kernel_us"], r
+        assert r["node_types"].get("kernel") == 3 and "child_graph" not in r["node_types"], r
+        # concurrent kernels: never the serial sum of the two
+        assert r["iter_us"] < 1.75 * r["one_kernel_us"], r
 
 
 @rccl_loopback
