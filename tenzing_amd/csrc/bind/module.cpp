@@ -947,6 +947,7 @@ PYBIND11_MODULE(_tz, m) {
       .def("direct", [](const HaloExchange &h, int i, uintptr_t s) { h.direct(i, P(s)); })
       .def("direct_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.direct_group(d, P(s)); })
       .def("uses_rccl", &HaloExchange::uses_rccl)
+      .def("rccl_graph_ok", &HaloExchange::rccl_graph_ok, "RCCL ops may be captured into hipGraphs")
       .def("uses_direct", &HaloExchange::uses_direct)
       .def("is_direct", &HaloExchange::is_direct)
       .def("is_ipc", &HaloExchange::is_ipc)

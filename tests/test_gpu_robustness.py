@@ -81,12 +81,33 @@ def test_rccl_preflight_one_rank(tz, gpu):
     h, g = build_halo(HaloConfig(n=32, neighbors=26, transport="rccl", fuse="choice"),
                       tz.SelfCtrl(), device=gpu)
     rep = h.transport_report()
-    assert rep["rccl"] == "ok" and h.rccl_nranks() == 1, rep
+    # RCCL passed eager and hipGraph preflights, in whole-schedule capture
+    assert rep["rccl"] == "ok (hipGraph: schedule capture)" and h.rccl_nranks() == 1, rep
     seq = tz.random_rollout(tz.State(g, tz.Platform(2)), 0)
     rt = tz.HipRuntime(device=gpu, n_streams=2)
     h.init_grid()
     rt.prepare(seq)
     rt.run(1)
+    rt.device_sync()
+    assert h.check_grid() == 0
+
+
+def test_rccl_graph_preflight_falls_back_to_child_capture(tz, gpu, monkeypatch):
+    """whole-schedule capture failing the RCCL graph preflight (simulated wrong data) is not the
+    end of RCCL in hipGraphs: the preflight moves on to child-graph capture, which passes, and
+    the report says which mode RCCL schedules are built in and why"""
+    from tenzing_amd.models import HaloConfig, build_halo
+
+    monkeypatch.setenv("TZ_FAIL_TRANSPORTS", "rccl_graph_schedule")
+    h, g = build_halo(HaloConfig(n=32, neighbors=6, transport="rccl"), tz.SelfCtrl(), device=gpu)
+    rep = h.transport_report()["rccl"]
+    assert rep.startswith("ok (hipGraph: child capture (schedule capture: ") and "wrong cells" in rep, rep
+    assert h.rccl_graph_ok()
+    rt = tz.HipRuntime(device=gpu, n_streams=2, mode=tz.ExecMode.Graph)
+    h.init_grid()
+    rt.prepare(tz.random_rollout(tz.State(g, tz.Platform(2)), 1))
+    assert rt.effective_mode == tz.ExecMode.Graph
+    rt.run(2)
     rt.device_sync()
     assert h.check_grid() == 0
 
