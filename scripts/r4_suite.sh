@@ -1,6 +1,6 @@
 # the full GPU suite, verbose (a hang names its test), then smoke
 mkdir -p gpurun_out/r4_suite
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+TZ_TEST_LOGDIR=gpurun_out/r4_suite/ranklogs timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread -p no:cacheprovider \
   > gpurun_out/r4_suite/pytest_gpu.log 2>&1
 rc=$?; echo "pytest -m gpu rc=$rc"; tail -15 gpurun_out/r4_suite/pytest_gpu.log
 case $rc in 0|1) ;; *) exit $rc;; esac

@@ -44,19 +44,29 @@ def _tails(logs, n=40):
     return "\n".join(out)
 
 
-def _launch(case, world, timeout=300, extra_env=None, tmp_path=None):
+def _launch(case, world, timeout=150, extra_env=None, tmp_path=None):
     """W rank processes of gpu_rank_body.py; each rank's output goes to its own file AS IT RUNS
     (TZ_TEST_VERBOSE progress lines, watchdog and [tz] messages), so a rank that hangs or dies
-    still leaves its trace: on a failure or a timeout every rank's tail is printed."""
+    still leaves its trace: on a failure or a timeout every rank's tail is printed. The files go
+    under TZ_TEST_LOGDIR when set (e.g. gpurun_out/..., so they come back from the GPU box even
+    when the whole run is killed). The limits are below the GPU box's 180 s silence limit: a
+    rank blocked in a control-plane collective fails after TZ_CTRL_TIMEOUT_S (90 s here), and
+    the test itself after `timeout`, each with the ranks' tails."""
     import tempfile
 
     port = _free_port()
-    logdir = str(tmp_path) if tmp_path is not None else tempfile.mkdtemp(prefix=f"tz_{case}_")
+    base = os.environ.get("TZ_TEST_LOGDIR")
+    if base:
+        os.makedirs(base, exist_ok=True)
+        logdir = tempfile.mkdtemp(prefix=f"{case}_w{world}_", dir=base)
+    else:
+        logdir = str(tmp_path) if tmp_path is not None else tempfile.mkdtemp(prefix=f"tz_{case}_")
     procs, logs = [], []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TZ_TEST_VERBOSE="1",
-                   PYTHONFAULTHANDLER="1", **(extra_env or {}))
+                   PYTHONFAULTHANDLER="1", TZ_CTRL_TIMEOUT_S=os.environ.get("TZ_CTRL_TIMEOUT_S", "90"),
+                   **(extra_env or {}))
         path = os.path.join(logdir, f"{case}_rank{r}.log")
         logs.append(path)
         f = open(path, "w")
@@ -189,7 +199,7 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
            "--cells", "64", "--mcts-iters", "6", "--bench-iters", "3", "--deadline-s", "240"]
     env = dict(os.environ, TZ_IPC_GRID="1" if mode == "grid" else "0")
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=160, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     j = json.loads(line)
@@ -249,7 +259,7 @@ def test_bench_two_ranks_under_mpiexec(gpu):
     cmd = [mpiexec, "-n", "2", sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
            "--steps", "6", "--warmup", "2", "--cells", "64", "--mcts-iters", "6",
            "--bench-iters", "3", "--deadline-s", "240", "--link-probe-iters", "0"]
-    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=160, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the one result line
@@ -313,7 +323,7 @@ def test_bench_host_fallback_loopback(gpu, tmp_path):
            "--cells", "48", "--mcts-iters", "6", "--bench-iters", "2", "--deadline-s", "240",
            "--link-probe-iters", "0"]
     env = dict(os.environ, TZ_IPC_COPY="0", TZ_FAIL_TRANSPORTS="ipc")
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=160, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     j = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert j["verified_bad_cells"] == 0 and j["value"] > 0
@@ -354,7 +364,7 @@ def test_bench_rejected_finalist_loopback(gpu):
            "--cells", "48", "--mcts-iters", "8", "--bench-iters", "2", "--deadline-s", "240",
            "--link-probe-iters", "0", "--hostsplit", "off"]
     env = dict(os.environ, TZ_IPC_GRID="0", TZ_BENCH_REJECT="1")
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=160, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     j = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert j["verified_bad_cells"] == 0 and j["verified_bad_cells_after_timing"] == 0
@@ -415,7 +425,7 @@ def test_bench_rccl_across_ranks_loopback(gpu):
            "--cells", "48", "--mcts-iters", "8", "--bench-iters", "2", "--deadline-s", "240",
            "--link-probe-iters", "2", "--link-probe-rccl", "--hostsplit", "off"]
     env = dict(os.environ, TZ_IPC_GRID="0", TZ_RCCL_LOOPBACK="1")
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=160, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     j = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert j["verified_bad_cells"] == 0 and j["verified_bad_cells_after_timing"] == 0
