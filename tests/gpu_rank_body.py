@@ -214,10 +214,12 @@ def main():
                 torch.cuda.synchronize()
                 ctrl.barrier()
                 rt.prepare(seq)
+                say("schedule", k, str(mode), seq.desc())
                 rt.run(3)
                 rt.device_sync()
                 runs.append(dict(mode=str(mode), k=k, eff=str(rt.effective_mode),
                                  bad=int((h != want).sum())))
+                say("schedule", k, "bad", runs[-1]["bad"])
             del rt
         rt = tz.HipRuntime(device=dev, n_streams=2, mode=tz.ExecMode.Graph, watchdog_s=60.0)
         o = tz.MctsOpts()
