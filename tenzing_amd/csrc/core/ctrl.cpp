@@ -139,8 +139,9 @@ int TcpCtrl::listen(int port, const std::string &bindAddr) {
 }
 
 namespace {
-constexpr uint32_t kHello = 0x545a4331; // "TZC1": a peer rank's first frame
-constexpr uint32_t kWelcome = 0x545a4f4b; // "TZOK": rank 0's release
+constexpr uint32_t kHello = 0x545a4331;   // "TZC1": a peer rank's first frame
+constexpr uint32_t kAck = 0x545a4143;     // "TZAC": rank 0 took the peer (sent at once)
+constexpr uint32_t kWelcome = 0x545a4f4b; // "TZOK": rank 0's release (once every rank joined)
 struct Hello {
   uint32_t magic;
   int32_t size, rank;
@@ -193,6 +194,7 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
                                                                 "rank of another job?)");
       }
       peers_[h.rank] = fd;
+      send_all(fd, &kAck, sizeof(kAck));
       ++joined;
     }
     // release everyone
@@ -209,24 +211,45 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
   TZ_CHECK(::getaddrinfo(host.c_str(), ps.c_str(), &hints, &res) == 0, "getaddrinfo " << host);
   const double t0 = wtime();
   int fd = -1;
+  std::string lastWhy = "connection refused";
   while (true) {
     fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
+      nodelay(fd);
+      // rank 0 acknowledges a peer at once; a listener that does not (another program that
+      // holds the port: rank 0 then failed to bind it) is left, not waited on forever
+      timeval ack{5, 0};
+      ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &ack, sizeof(ack));
+      uint32_t a = 0;
+      try {
+        const Hello h{kHello, size_, rank_};
+        send_all(fd, &h, sizeof(h));
+        recv_all(fd, &a, sizeof(a));
+      } catch (const Error &) {
+        a = 0;
+      }
+      if (a == kAck) break;
+      lastWhy = "a listener on the port that is not this job's rank 0";
+    }
     ::close(fd);
     fd = -1;
     if (wtime() - t0 > timeoutS) {
       ::freeaddrinfo(res);
-      TZ_THROW("ctrl connect to " << host << ":" << port << " timed out");
+      TZ_THROW("ctrl connect to " << host << ":" << port << " timed out (" << lastWhy << ")");
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
   ::freeaddrinfo(res);
-  nodelay(fd);
-  const Hello h{kHello, size_, rank_};
-  send_all(fd, &h, sizeof(h));
+  // the release comes once every rank joined: wait for it as long as the rendezvous may take
+  const double left = std::max(1.0, timeoutS - (wtime() - t0));
+  timeval rel{};
+  rel.tv_sec = long(left);
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &rel, sizeof(rel));
   uint32_t w = 0;
   recv_all(fd, &w, sizeof(w));
   TZ_CHECK(w == kWelcome, "ctrl rendezvous: " << host << ":" << port << " is not this job's rank 0");
+  timeval none{0, 0};
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
   peer_timeout(fd);
   peers_[0] = fd;
 }

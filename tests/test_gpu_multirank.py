@@ -18,11 +18,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """a MASTER_PORT whose control-plane port (MASTER_PORT + 1) is free as well"""
+    for _ in range(100):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        t = socket.socket()
+        try:
+            t.bind(("0.0.0.0", p + 1))
+        except OSError:
+            continue
+        finally:
+            t.close()
+        return p
+    raise RuntimeError("no free port pair")
 
 
 # RCCL between loopback ranks goes through RCCL's socket transport with every rank's kernels on
