@@ -546,8 +546,9 @@ PYBIND11_MODULE(_tz, m) {
       .def("connect", &TcpCtrl::connect, py::arg("host"), py::arg("port"), py::arg("timeout_s") = 300.0,
            py::call_guard<py::gil_scoped_release>())
       .def("rendezvous", &TcpCtrl::rendezvous, py::arg("host"), py::arg("port"),
-           py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>(),
-           "rank 0 listens on `port`, the others connect (handshake-checked): no store, no torch")
+           py::arg("timeout_s") = 300.0, py::arg("nports") = 8, py::call_guard<py::gil_scoped_release>(),
+           "rank 0 listens on the first free port of port..port+nports-1, the others connect "
+           "(handshake-checked): no store, no torch")
       .def("rendezvous_file", &TcpCtrl::rendezvous_file, py::arg("path"), py::arg("host") = "127.0.0.1",
            py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>());
   py::class_<MpiCtrl, Ctrl, std::shared_ptr<MpiCtrl>>(m, "MpiCtrl")

@@ -148,6 +148,38 @@ struct Hello {
 };
 } // namespace
 
+int TcpCtrl::connect_acked(const std::string &host, int port, std::string &why) const {
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  const std::string ps = std::to_string(port);
+  TZ_CHECK(::getaddrinfo(host.c_str(), ps.c_str(), &hints, &res) == 0, "getaddrinfo " << host);
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  const int rc = ::connect(fd, res->ai_addr, res->ai_addrlen);
+  ::freeaddrinfo(res);
+  if (rc != 0) {
+    ::close(fd);
+    return -1;
+  }
+  nodelay(fd);
+  // rank 0 acknowledges a peer at once; a listener that does not (another program that holds
+  // the port) is left, not waited on forever
+  timeval ack{5, 0};
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &ack, sizeof(ack));
+  uint32_t a = 0;
+  try {
+    const Hello h{kHello, size_, rank_};
+    send_all(fd, &h, sizeof(h));
+    recv_all(fd, &a, sizeof(a));
+  } catch (const Error &) {
+    a = 0;
+  }
+  if (a == kAck) return fd;
+  why = "a listener on port " + ps + " that is not this job's rank 0";
+  ::close(fd);
+  return -1;
+}
+
 void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
   if (size_ == 1) return;
   if (rank_ == 0) {
@@ -204,42 +236,21 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
     }
     return;
   }
-  addrinfo hints{}, *res = nullptr;
-  hints.ai_family = AF_INET;
-  hints.ai_socktype = SOCK_STREAM;
-  const std::string ps = std::to_string(port);
-  TZ_CHECK(::getaddrinfo(host.c_str(), ps.c_str(), &hints, &res) == 0, "getaddrinfo " << host);
   const double t0 = wtime();
   int fd = -1;
   std::string lastWhy = "connection refused";
-  while (true) {
-    fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
-      nodelay(fd);
-      // rank 0 acknowledges a peer at once; a listener that does not (another program that
-      // holds the port: rank 0 then failed to bind it) is left, not waited on forever
-      timeval ack{5, 0};
-      ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &ack, sizeof(ack));
-      uint32_t a = 0;
-      try {
-        const Hello h{kHello, size_, rank_};
-        send_all(fd, &h, sizeof(h));
-        recv_all(fd, &a, sizeof(a));
-      } catch (const Error &) {
-        a = 0;
-      }
-      if (a == kAck) break;
-      lastWhy = "a listener on the port that is not this job's rank 0";
-    }
-    ::close(fd);
-    fd = -1;
-    if (wtime() - t0 > timeoutS) {
-      ::freeaddrinfo(res);
-      TZ_THROW("ctrl connect to " << host << ":" << port << " timed out (" << lastWhy << ")");
-    }
-    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  // every candidate port in turn (rendezvous: rank 0 took the first one it could bind), until
+  // one answers as this job's rank 0
+  const int nports = std::max(1, connectPorts_);
+  for (int k = 0;; k = (k + 1) % nports) {
+    fd = connect_acked(host, port + k, lastWhy);
+    if (fd >= 0) break;
+    if (wtime() - t0 > timeoutS)
+      TZ_THROW("ctrl connect to " << host << ":" << port
+                                  << (nports > 1 ? "+" + std::to_string(nports - 1) : std::string())
+                                  << " timed out (" << lastWhy << ")");
+    if (k == nports - 1) std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
-  ::freeaddrinfo(res);
   // the release comes once every rank joined: wait for it as long as the rendezvous may take
   const double left = std::max(1.0, timeoutS - (wtime() - t0));
   timeval rel{};
@@ -254,11 +265,29 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
   peers_[0] = fd;
 }
 
-void TcpCtrl::rendezvous(const std::string &host, int port, double timeoutS) {
-  TZ_CHECK(port > 0 && port < 65536, "ctrl rendezvous port " << port << " out of range");
+void TcpCtrl::rendezvous(const std::string &host, int port, double timeoutS, int nports) {
+  TZ_CHECK(port > 0 && port + nports - 1 < 65536 && nports >= 1,
+           "ctrl rendezvous ports " << port << "+" << nports - 1 << " out of range");
   if (size_ == 1) return;
-  if (rank_ == 0) listen(port, "0.0.0.0");
+  if (rank_ == 0) {
+    // the first of the candidate ports that is free (another program may hold one); the other
+    // ranks try them all, and only this job's rank 0 acknowledges them
+    std::string errs;
+    for (int k = 0; k < nports && listenFd_ < 0; ++k) {
+      try {
+        listen(port + k, "0.0.0.0");
+      } catch (const Error &e) {
+        if (listenFd_ >= 0) ::close(listenFd_);
+        listenFd_ = -1;
+        errs += std::string("\n  ") + e.what();
+      }
+    }
+    TZ_CHECK(listenFd_ >= 0, "ctrl rendezvous: none of ports " << port << ".." << port + nports - 1
+                                                               << " could be bound:" << errs);
+  }
+  connectPorts_ = nports;
   connect(host, port, timeoutS);
+  connectPorts_ = 1;
 }
 
 void TcpCtrl::rendezvous_file(const std::string &path, const std::string &host, double timeoutS) {

@@ -68,7 +68,8 @@ public:
   /// until rank 0 is up): a launcher-style rendezvous with no store and no torch.distributed.
   /// Every connection carries a handshake (magic, world size, rank), so a stray connection to
   /// the port is dropped instead of taken for a rank.
-  void rendezvous(const std::string &host, int port, double timeoutS = 300.0);
+  /// `nports` candidate ports from `port` on: rank 0 listens on the first it can bind
+  void rendezvous(const std::string &host, int port, double timeoutS = 300.0, int nports = 8);
 
   int rank() const override { return rank_; }
   int size() const override { return size_; }
@@ -82,6 +83,9 @@ public:
 
 private:
   void allreduce(double *v, size_t n, bool isMax);
+  /// one connection attempt to host:port with the handshake; the fd, or -1 (`why` updated)
+  int connect_acked(const std::string &host, int port, std::string &why) const;
+  int connectPorts_ = 1; // candidate ports connect() cycles through (rendezvous)
   int rank_, size_;
   int listenFd_ = -1;
   std::vector<int> peers_; // rank 0: fd per rank (index 0 unused); others: peers_[0] = root

@@ -4,7 +4,8 @@ One process per GPU (``torchrun --nproc-per-node N``; RANK / WORLD_SIZE / LOCAL_
 MASTER_ADDR / MASTER_PORT from the environment). The control plane is the native TCP star
 (``tenzing_amd._tz.TcpCtrl``) and needs nothing from torch: rank 0 listens on the control port
 (``TZ_CTRL_PORT``, default MASTER_PORT + 1: torchrun's agent already serves its own store on
-MASTER_PORT) and every other rank connects to MASTER_ADDR with a handshake. So a multi-rank run
+MASTER_PORT; if another program holds it, the next of ``TZ_CTRL_PORTS`` = 8 candidates) and every
+other rank connects to MASTER_ADDR with a handshake that only this job's rank 0 answers. So a multi-rank run
 can use the system ROCm runtime (``TZ_NO_TORCH=1``) as well as torch's bundled one.
 ``TZ_CTRL_BOOTSTRAP=torch`` restores the old path (one gloo broadcast of an ephemeral port). RCCL
 communicators for the data plane are created later by the workloads, with their unique ids
@@ -77,7 +78,8 @@ def init_ctrl(rank: int | None = None, world: int | None = None, master_addr: st
     host = master_addr or e.master_addr
     if how == "tcp":
         port = int(os.environ.get("TZ_CTRL_PORT", e.master_port + 1))
-        ctrl.rendezvous(host, port, timeout_s)
+        # rank 0 takes the first free one of TZ_CTRL_PORTS candidate ports from there
+        ctrl.rendezvous(host, port, timeout_s, int(os.environ.get("TZ_CTRL_PORTS", "8")))
         return ctrl
     import datetime
 
