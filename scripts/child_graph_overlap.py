@@ -31,6 +31,8 @@ def main():
         ops.append(tz.BusyKernelOp("c", 50.0))
     elif variant == "kernel4":  # and a fourth
         ops += [tz.BusyKernelOp("c", 50.0), tz.BusyKernelOp("d", 50.0)]
+    elif variant.startswith("equal"):  # equalN: N independent 200 us kernels
+        ops = [tz.BusyKernelOp(chr(ord("a") + i), us) for i in range(int(variant[5:]))]
     elif variant == "hostchain":  # RCCL's shape: a host node, then a kernel behind it
         chain = [tz.HostFuncOp("h"), tz.BusyKernelOp("c", 50.0)]
     elif variant == "chainhost":  # the other order: a kernel, then a host node
