@@ -47,13 +47,13 @@ def main():
         g.then(chain[0], chain[1])
         g.then_finish(chain[1])
     ns = len(names)
-    seq = None
-    for seed in range(2000):  # every branch on a stream of its own, a chain on one stream
-        s = tz.random_rollout(tz.State(g, tz.Platform(ns)), seed)
-        st = {o.name: o.stream for o in s.ops() if o.name in names + [c.name for c in chain]}
-        if len({st[n] for n in names}) == ns and (not chain or st[chain[0].name] == st[chain[1].name]):
-            seq = s
-            break
+    # every branch on a stream of its own, a chain on one stream
+    from tenzing_amd.search import greedy_schedule
+
+    sid = {n: i for i, n in enumerate(names)}
+    if chain:
+        sid[chain[1].name] = sid[chain[0].name]
+    seq = greedy_schedule(g, tz.Platform(ns, symmetric_streams=False), stream_for=lambda n: sid[n])
     eager = os.environ.get("TZ_OVERLAP_EAGER") == "1"
     rt = tz.HipRuntime(device=0, n_streams=ns, mode=tz.ExecMode.Eager if eager else tz.ExecMode.Graph)
     rt.prepare(seq)
