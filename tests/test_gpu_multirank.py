@@ -151,6 +151,21 @@ def test_mixed_engines_loopback(gpu, world):
             assert run["bad1"] == run["bad2"] == run["bad3"] == 0 and run["err"] == 0, run
 
 
+def test_copy_puts_over_two_engines_loopback(gpu):
+    """copy-engine puts cut over two engine streams (TZ_COPY_ENGINES=2: a fork to a side stream
+    and a join back inside the op): exact eager and inside whole-schedule hipGraph captures,
+    where the side stream's capture dependencies are set per op (no false edge between copy ops
+    of different schedule streams)"""
+    extra = {"TZ_IPC_GRID": "0", "TZ_COPY_ENGINES": "2", "TZ_TEST_FUSES": "choice",
+             "TZ_TEST_REQUIRE": "he_copyput_", "TZ_TEST_SEEDS": "3", "TZ_TEST_NO_MCTS": "1"}
+    res = _launch("ipc_halo", 2, extra_env=extra)
+    for r in res:
+        assert r["runs"] and all(run["copyput"] for run in r["runs"]), r["runs"]
+        assert {run["mode"] for run in r["runs"]} == {"ExecMode.Eager", "ExecMode.Graph"}
+        for run in r["runs"]:
+            assert run["bad1"] == run["bad2"] == run["bad3"] == 0 and run["err"] == 0, run
+
+
 def test_relay_routing_loopback(gpu):
     """the 2x2x2 grid with every remote direction through relay routing (a share of each face
     via the corner peer, forwarded over its edge-diagonal link): every ghost right on all 8
