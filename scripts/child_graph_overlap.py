@@ -33,14 +33,22 @@ def main():
         ops += [tz.BusyKernelOp("c", 50.0), tz.BusyKernelOp("d", 50.0)]
     elif variant.startswith("equal"):  # equalN: N independent 200 us kernels
         ops = [tz.BusyKernelOp(chr(ord("a") + i), us) for i in range(int(variant[5:]))]
+    elif variant.startswith("fork"):  # forkN: N 200 us kernels behind one empty kernel
+        ops = [tz.BusyKernelOp(chr(ord("a") + i), us) for i in range(int(variant[4:]))]
     elif variant == "hostchain":  # RCCL's shape: a host node, then a kernel behind it
         chain = [tz.HostFuncOp("h"), tz.BusyKernelOp("c", 50.0)]
     elif variant == "chainhost":  # the other order: a kernel, then a host node
         chain = [tz.BusyKernelOp("c", 50.0), tz.HostFuncOp("h")]
     names = [o.name for o in ops] + ([chain[0].name] if chain else [])
     g = tz.Graph()
+    root = tz.EmptyKernelOp("root") if variant.startswith("fork") else None
+    if root is not None:
+        g.start_then(root)
     for op in ops:
-        g.start_then(op)
+        if root is not None:
+            g.then(root, op)
+        else:
+            g.start_then(op)
         g.then_finish(op)
     if chain:
         g.start_then(chain[0])
@@ -51,6 +59,7 @@ def main():
     from tenzing_amd.search import greedy_schedule
 
     sid = {n: i for i, n in enumerate(names)}
+    sid["root"] = 0
     if chain:
         sid[chain[1].name] = sid[chain[0].name]
     seq = greedy_schedule(g, tz.Platform(ns, symmetric_streams=False), stream_for=lambda n: sid[n])
