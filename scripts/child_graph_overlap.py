@@ -59,7 +59,10 @@ def main():
     from tenzing_amd.search import greedy_schedule
 
     sid = {n: i for i, n in enumerate(names)}
-    sid["root"] = 0
+    if root is not None:  # the root alone on stream 0, every branch on a stream of its own after it
+        sid = {n: i + 1 for i, n in enumerate(names)}
+        sid["root"] = 0
+        ns += 1
     if chain:
         sid[chain[1].name] = sid[chain[0].name]
     seq = greedy_schedule(g, tz.Platform(ns, symmetric_streams=False), stream_for=lambda n: sid[n])
