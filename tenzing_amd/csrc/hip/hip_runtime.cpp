@@ -446,6 +446,40 @@ GraphBuilder::GraphBuilder(const std::vector<void *> &streams, CaptureMode mode)
   TZ_LOG(Debug, "capture: begin");
   TZ_HIP(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
   capturing_ = true;
+  const std::string root = graph_root_mode();
+  if (root == "none") return;
+  try {
+    if (root == "kernel") {
+      kern::empty(origin);
+    } else {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      hipGraph_t g = nullptr;
+      TZ_HIP(hipStreamGetCaptureInfo_v2(origin, &cs, nullptr, &g, nullptr, nullptr));
+      hipGraphNode_t n = nullptr;
+      TZ_HIP(hipGraphAddEmptyNode(&n, g, nullptr, 0));
+      TZ_HIP(hipStreamUpdateCaptureDependencies(origin, &n, 1, hipStreamSetCaptureDependencies));
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipGraphNode_t *d = nullptr;
+    size_t nd = 0;
+    TZ_HIP(hipStreamGetCaptureInfo_v2(origin, &cs, nullptr, nullptr, &d, &nd));
+    TZ_CHECK(nd == 1, "graph root: " << nd << " capture dependencies after the root");
+    root_ = d[0];
+  } catch (...) {
+    abandon();
+    throw;
+  }
+}
+
+const char *graph_root_mode() {
+  static const std::string m = [] {
+    const char *v = std::getenv("TZ_GRAPH_ROOT");
+    const std::string how = v ? v : "kernel";
+    TZ_CHECK(how == "kernel" || how == "empty" || how == "none",
+             "TZ_GRAPH_ROOT must be kernel, empty or none (got " << how << ")");
+    return how;
+  }();
+  return m.c_str();
 }
 
 GraphBuilder::~GraphBuilder() { abandon(); }
@@ -504,6 +538,7 @@ std::vector<void *> GraphBuilder::add(int stream, const std::vector<void *> &dep
   // recursed without end when RCCL's streams had joined the capture through other forked
   // streams (profiles/r4_capture/self_torchrt2.log)
   hipStream_t origin = S(streams_[0]);
+  if (deps.empty() && root_) deps.push_back(static_cast<hipGraphNode_t>(root_)); // one root
   TZ_LOG(Debug, "capture: op of stream " << stream << " behind " << deps.size() << " node(s)");
   TZ_HIP(hipStreamUpdateCaptureDependencies(origin, deps.empty() ? nullptr : deps.data(), deps.size(),
                                             hipStreamSetCaptureDependencies));

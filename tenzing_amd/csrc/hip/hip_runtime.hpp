@@ -238,7 +238,15 @@ private:
   CaptureMode mode_;
   void *graph_ = nullptr; // Child: the graph being assembled
   bool capturing_ = false;
+  void *root_ = nullptr;  // Schedule: the single root every op without dependencies follows
 };
+
+/// The root of a whole-schedule capture (env TZ_GRAPH_ROOT): "kernel" (default) = an empty
+/// kernel that every op without dependencies follows, "empty" = a graph empty node, "none" = no
+/// root. HIP's graph executor runs independent branches far better from one root than from
+/// several: three 200 us kernels as three roots take 449 us per launch, forked from one root
+/// 248 us (profiles/r4_capture/fork.jsonl)
+const char *graph_root_mode();
 
 /// route the core's trace ranges (MCTS phases, schedule ops in eager runs) to roctx
 void enable_roctx(bool on);

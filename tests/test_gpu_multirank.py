@@ -412,7 +412,9 @@ def test_rccl_node_overlaps_kernels_loopback(gpu):
     res = _launch("rccl_overlap", 2, extra_env={"TZ_RCCL_LOOPBACK": "1"})
     for r in res:
         assert r["effective_mode"] == "ExecMode.Graph" and r["bad"] == [0, 0, 0], r
-        assert r["node_types"].get("kernel") == 3 and "child_graph" not in r["node_types"], r
+        # 2 busy kernels + the RCCL kernel (+ the capture root, an empty kernel, unless TZ_GRAPH_ROOT
+        # says otherwise)
+        assert r["node_types"].get("kernel") in (3, 4) and "child_graph" not in r["node_types"], r
         # concurrent kernels: never the serial sum of the two
         assert r["iter_us"] < 1.75 * r["one_kernel_us"], r
 
