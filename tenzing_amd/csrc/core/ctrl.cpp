@@ -145,6 +145,7 @@ constexpr uint32_t kWelcome = 0x545a4f4b; // "TZOK": rank 0's release (once ever
 struct Hello {
   uint32_t magic;
   int32_t size, rank;
+  int32_t job; // the job's base port (rendezvous): a rank 0 of another job does not take it
 };
 } // namespace
 
@@ -168,7 +169,7 @@ int TcpCtrl::connect_acked(const std::string &host, int port, std::string &why) 
   ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &ack, sizeof(ack));
   uint32_t a = 0;
   try {
-    const Hello h{kHello, size_, rank_};
+    const Hello h{kHello, size_, rank_, job_};
     send_all(fd, &h, sizeof(h));
     recv_all(fd, &a, sizeof(a));
   } catch (const Error &) {
@@ -214,9 +215,11 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
       }
       timeval none{0, 0};
       ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
-      if (h.magic != kHello) {
+      if (h.magic != kHello || h.job != job_) {
+        // not this job: no acknowledgement, so the peer moves on to the next candidate port
         ::close(fd);
-        TZ_LOG(Warn, "ctrl rendezvous: dropped a connection without the handshake");
+        TZ_LOG(Warn, "ctrl rendezvous: dropped a connection "
+                         << (h.magic != kHello ? "without the handshake" : "of another job"));
         continue;
       }
       if (h.size != size_ || h.rank <= 0 || h.rank >= size_ || peers_[h.rank] >= 0) {
@@ -286,6 +289,7 @@ void TcpCtrl::rendezvous(const std::string &host, int port, double timeoutS, int
                                                                << " could be bound:" << errs);
   }
   connectPorts_ = nports;
+  job_ = port;
   connect(host, port, timeoutS);
   connectPorts_ = 1;
 }

@@ -86,6 +86,7 @@ private:
   /// one connection attempt to host:port with the handshake; the fd, or -1 (`why` updated)
   int connect_acked(const std::string &host, int port, std::string &why) const;
   int connectPorts_ = 1; // candidate ports connect() cycles through (rendezvous)
+  int32_t job_ = 0;      // job token of the handshake (rendezvous: the base port; else 0)
   int rank_, size_;
   int listenFd_ = -1;
   std::vector<int> peers_; // rank 0: fd per rank (index 0 unused); others: peers_[0] = root
