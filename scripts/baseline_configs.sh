@@ -10,7 +10,7 @@
 # torchrun (the driver's scaling run).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/baseline
+OUT=${OUT:-gpurun_out/baseline}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
