@@ -6,9 +6,10 @@
 //   torchrun --nproc-per-node 8 ... tz-search (one process per GPU; RANK/WORLD_SIZE/LOCAL_RANK)
 //   mpirun -n 8 tz-search ...                 (the reference's launch; control plane over MPI)
 //
-// Under torchrun the control-plane rendezvous goes through a file (--rdzv-file, default under
-// /tmp keyed by MASTER_PORT); under an MPI launcher it is MPI_COMM_WORLD (--ctrl mpi, picked
-// automatically). The data plane is RCCL / IPC puts either way.
+// Under torchrun the control plane rendezvouses on MASTER_ADDR, rank 0 listening on the first
+// free of 8 ports from MASTER_PORT + 1 (TZ_CTRL_PORT / TZ_CTRL_PORTS as in Python), or through a
+// file (--rdzv-file, single node; the default without MASTER_PORT); under an MPI launcher it is
+// MPI_COMM_WORLD (--ctrl mpi, picked automatically). The data plane is RCCL / IPC puts either way.
 #include "core/solve.hpp"
 #include "hip/hip_runtime.hpp"
 #include "workloads/workloads.hpp"
@@ -168,8 +169,16 @@ int main(int argc, char **argv) {
 
     if (!ctrl && size > 1) {
       auto t = std::make_shared<TcpCtrl>(rank, size);
-      const std::string port = std::getenv("MASTER_PORT") ? std::getenv("MASTER_PORT") : "default";
-      t->rendezvous_file(a.get("rdzv-file", "/tmp/tz_rdzv_" + port), a.get("master-addr", "127.0.0.1"));
+      const char *mp = std::getenv("MASTER_PORT");
+      const char *ma = std::getenv("MASTER_ADDR");
+      const std::string host = a.get("master-addr", ma ? ma : "127.0.0.1");
+      if (mp && !a.flag("rdzv-file")) {
+        const int base = std::getenv("TZ_CTRL_PORT") ? std::atoi(std::getenv("TZ_CTRL_PORT")) : std::atoi(mp) + 1;
+        const int nports = std::getenv("TZ_CTRL_PORTS") ? std::atoi(std::getenv("TZ_CTRL_PORTS")) : 8;
+        t->rendezvous(host, base, 300.0, nports);
+      } else {
+        t->rendezvous_file(a.get("rdzv-file", std::string("/tmp/tz_rdzv_") + (mp ? mp : "default")), host);
+      }
       ctrl = t;
     } else if (!ctrl) {
       ctrl = std::make_shared<SelfCtrl>();

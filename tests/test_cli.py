@@ -217,3 +217,34 @@ def test_native_cli_deadline_prints_partial_csv():
     assert len(rows) >= 1 and all(len(x.split("|")) > 7 for x in rows)
     assert [int(x.split("|")[0]) for x in rows] == list(range(len(rows)))
     assert "run deadline" in r.stderr
+
+
+def test_native_cli_two_ranks_port_rendezvous():
+    """tz-search started the torchrun way (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT, no
+    file): the native control plane's port rendezvous, a collective simulated search, the
+    results CSV from rank 0 only"""
+    import socket
+
+    exe = os.path.join(ROOT, "tenzing_amd", "bin", "tz-search")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ps = []
+    for r in (0, 1):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        ps.append(subprocess.Popen([exe, "--workload", "diamond", "--sim", "--iters", "6",
+                                    "--streams", "2"], env=env, stdout=subprocess.PIPE,
+                                   stderr=subprocess.PIPE, text=True))
+    try:
+        outs = [p.communicate(timeout=120) for p in ps]
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in ps), [e[-1500:] for _, e in outs]
+    best = [json.loads(ln) for ln in outs[0][1].splitlines() if ln.startswith('{"best')]
+    assert best and best[0]["ranks"] == 2 and best[0]["candidates"] == 6
+    assert sum(ln.startswith("0|") for ln in outs[0][0].splitlines()) == 1
+    assert not any(ln.startswith("0|") for ln in outs[1][0].splitlines())
