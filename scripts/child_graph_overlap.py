@@ -67,7 +67,9 @@ def main():
         sid[chain[1].name] = sid[chain[0].name]
     seq = greedy_schedule(g, tz.Platform(ns, symmetric_streams=False), stream_for=lambda n: sid[n])
     eager = os.environ.get("TZ_OVERLAP_EAGER") == "1"
-    rt = tz.HipRuntime(device=0, n_streams=ns, mode=tz.ExecMode.Eager if eager else tz.ExecMode.Graph)
+    # TZ_OVERLAP_STREAMS: the runtime owns this many streams (at least the schedule's)
+    nrt = max(ns, int(os.environ.get("TZ_OVERLAP_STREAMS", "0")))
+    rt = tz.HipRuntime(device=0, n_streams=nrt, mode=tz.ExecMode.Eager if eager else tz.ExecMode.Graph)
     rt.prepare(seq)
     rt.run(5)
     rt.device_sync()
@@ -79,7 +81,7 @@ def main():
         rt.device_sync()
         dt = (time.perf_counter() - t0) / n
         best = dt if best is None else min(best, dt)
-    print(json.dumps({"variant": variant, "capture": os.environ.get("TZ_GRAPH_CAPTURE", "schedule"),
+    print(json.dumps({"variant": variant, "runtime_streams": nrt, "capture": os.environ.get("TZ_GRAPH_CAPTURE", "schedule"),
                       "nodes": rt.graph_nodes(), "node_types": rt.graph_node_types(),
                       "mode": str(rt.effective_mode), "iter_us": best * 1e6, "one_kernel_us": us}))
 
