@@ -474,7 +474,7 @@ GraphBuilder::GraphBuilder(const std::vector<void *> &streams, CaptureMode mode)
 const char *graph_root_mode() {
   static const std::string m = [] {
     const char *v = std::getenv("TZ_GRAPH_ROOT");
-    const std::string how = v ? v : "kernel";
+    const std::string how = v ? v : "none";
     TZ_CHECK(how == "kernel" || how == "empty" || how == "none",
              "TZ_GRAPH_ROOT must be kernel, empty or none (got " << how << ")");
     return how;

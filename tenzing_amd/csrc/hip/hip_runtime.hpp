@@ -241,11 +241,10 @@ private:
   void *root_ = nullptr;  // Schedule: the single root every op without dependencies follows
 };
 
-/// The root of a whole-schedule capture (env TZ_GRAPH_ROOT): "kernel" (default) = an empty
-/// kernel that every op without dependencies follows, "empty" = a graph empty node, "none" = no
-/// root. HIP's graph executor runs independent branches far better from one root than from
-/// several: three 200 us kernels as three roots take 449 us per launch, forked from one root
-/// 248 us (profiles/r4_capture/fork.jsonl)
+/// The root of a whole-schedule capture (env TZ_GRAPH_ROOT): "none" (default) = the ops without
+/// dependencies are the graph's roots, "kernel" = an empty kernel that every such op follows,
+/// "empty" = a graph empty node. A/B on one MI355X (profiles/r4_root/): a single root changes
+/// neither the branch probes nor the RCCL probe, and costs the headline 0.2-0.9 %
 const char *graph_root_mode();
 
 /// route the core's trace ranges (MCTS phases, schedule ops in eager runs) to roctx
