@@ -76,6 +76,18 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
     }
     streams_.push_back(s);
   }
+  // spare streams (never used) up to TZ_PAD_STREAMS in all: HIP deals its hardware queues to
+  // streams round-robin, and hipGraph launches run their parallel branches on streams of HIP's
+  // own; with 3 schedule streams one of those landed on the launch stream's queue (three
+  // independent 200 us kernels: 447 us per launch; with a 4th stream owned: 244 us,
+  // profiles/r4_capture/nstreams.jsonl)
+  int pad = 4;
+  if (const char *v = std::getenv("TZ_PAD_STREAMS")) pad = std::atoi(v);
+  for (int i = opts.n_streams; i < pad; ++i) {
+    hipStream_t s = nullptr;
+    TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    spare_.push_back(s);
+  }
   // the device abort flag (polled by every spinning kernel) is allocated now: not inside a timed
   // run, and never inside a stream capture, where host allocations are not allowed
   kern::abort_flag();
@@ -143,6 +155,7 @@ HipRuntime::~HipRuntime() {
   for (void *e : timerEv_)
     if (e) (void)hipEventDestroy(E(e));
   for (void *s : streams_) (void)hipStreamDestroy(S(s));
+  for (void *s : spare_) (void)hipStreamDestroy(S(s));
 }
 
 std::string HipRuntime::device_name() const {
