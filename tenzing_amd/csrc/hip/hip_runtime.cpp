@@ -79,9 +79,10 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
   // spare streams (never used) up to TZ_PAD_STREAMS in all: HIP deals its hardware queues to
   // streams round-robin, and hipGraph launches run their parallel branches on streams of HIP's
   // own; with 3 schedule streams one of those landed on the launch stream's queue (three
-  // independent 200 us kernels: 447 us per launch; with a 4th stream owned: 244 us,
-  // profiles/r4_capture/nstreams.jsonl)
-  int pad = 4;
+  // independent 200 us kernels: 447 us per launch; with 4-8 streams owned: 241-244 us; a host
+  // node then a kernel beside two kernels: 319 -> 241 us). 6: the RCCL probe between two
+  // loopback ranks also stays at its unpadded time (profiles/r4_pad/)
+  int pad = 6;
   if (const char *v = std::getenv("TZ_PAD_STREAMS")) pad = std::atoi(v);
   for (int i = opts.n_streams; i < pad; ++i) {
     hipStream_t s = nullptr;
