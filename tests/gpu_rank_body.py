@@ -243,7 +243,7 @@ def main():
         W, R = ctrl.size, ctrl.rank
         n = int(os.environ.get("TZ_TEST_N", str(1 << 12)))
         us = float(os.environ.get("TZ_TEST_BUSY_US", "200"))
-        comms = tz._tz.make_rccl_comms(ctrl, dev, 3)
+        comms = tz._tz.make_rccl_comms(ctrl, dev, int(os.environ.get("TZ_TEST_COMMS", "3")))
         a, c = tz._tz.DeviceBuffer(8 * n), tz._tz.DeviceBuffer(8 * n)
         nxt, prv = (R + 1) % W, (R - 1) % W
         sr = tz.SendRecvOp("sr", comms, a.ptr, n, nxt, c.ptr, n, prv, 1, keep=(a, c))
