@@ -10,6 +10,11 @@
 #include "core/health.hpp"
 #include "core/solve.hpp"
 
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/select.h>
+#include <sys/socket.h>
+#include <unistd.h>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -472,6 +477,58 @@ TEST(mcts_checkpoint_resume) {
   SearchResult r2 = mcts_explore(*g, Platform::make_n_streams(2), sb, ctrl, o2);
   CHECK(r2.sims.size() >= r1.sims.size());
   std::remove(o.checkpoint_path.c_str());
+}
+
+TEST(tcp_ctrl_rendezvous_skips_a_foreign_listener) {
+  // the torch-free bootstrap: rank 0 listens on the first free of several candidate ports (the
+  // first is held by a "foreign" listener that accepts and never answers), the other ranks try
+  // the candidates and take the one that acknowledges their handshake; then one collective
+  int probe = ::socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  a.sin_port = 0;
+  CHECK(::bind(probe, reinterpret_cast<sockaddr *>(&a), sizeof(a)) == 0);
+  socklen_t len = sizeof(a);
+  ::getsockname(probe, reinterpret_cast<sockaddr *>(&a), &len);
+  const int base = ntohs(a.sin_port);
+  CHECK(::listen(probe, 8) == 0); // the foreign listener on the first candidate port
+  std::atomic<bool> stop{false};
+  std::vector<int> held;
+  std::thread foreign([&] {
+    while (!stop.load()) {
+      fd_set rd;
+      FD_ZERO(&rd);
+      FD_SET(probe, &rd);
+      timeval tv{0, 100000};
+      if (::select(probe + 1, &rd, nullptr, nullptr, &tv) > 0) held.push_back(::accept(probe, nullptr, nullptr));
+    }
+  });
+  constexpr int N = 3;
+  std::vector<std::string> got(N), err(N);
+  auto body = [&](int r) {
+    try {
+      TcpCtrl c(r, N);
+      c.rendezvous("127.0.0.1", base, 60.0, 4);
+      std::string s = r == 0 ? "hello" : "";
+      c.bcast(s, 0);
+      got[r] = s;
+    } catch (const std::exception &e) {
+      err[r] = e.what();
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int r = 0; r < N; ++r) ts.emplace_back(body, r);
+  for (auto &t : ts) t.join();
+  stop = true;
+  foreign.join();
+  for (int fd : held)
+    if (fd >= 0) ::close(fd);
+  ::close(probe);
+  for (int r = 0; r < N; ++r) {
+    if (!err[r].empty()) std::fprintf(stderr, "  rank %d: %s\n", r, err[r].c_str());
+    CHECK(err[r].empty() && got[r] == "hello");
+  }
 }
 
 TEST(tcp_ctrl_ranks_as_threads) {
