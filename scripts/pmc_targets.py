@@ -19,7 +19,8 @@ from tenzing_amd.models import HaloConfig, build_halo  # noqa: E402
 def main():
     torch.zeros(1, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
-    hd, _ = build_halo(HaloConfig(n=512, neighbors=26, order="qxyz", transport="direct"),
+    order = os.environ.get("TZ_PMC_ORDER", "qxyz")  # xyzq: the reference driver's layout
+    hd, _ = build_halo(HaloConfig(n=512, neighbors=26, order=order, transport="direct"),
                        tz.SelfCtrl(), device=0)
     if len(sys.argv) > 2 and sys.argv[1] == "--only-move":
         # steady state of the headline: the 26-direction move back to back, as in the hipGraph
