@@ -604,6 +604,7 @@ def main() -> int:
             "xgmi_topology": topo,
             "peer_devices": peers,
             "runtime": runtime_libraries(),
+            "graph_capture": tz._tz.graph_capture_info(),
             "link_probe": probe,
             "elapsed_s": round(time.time() - T_START, 1),
         })

@@ -210,6 +210,16 @@ PYBIND11_MODULE(_tz, m) {
     int v = 0;
     return hipRuntimeGetVersion(&v) == hipSuccess ? v : -1;
   }, "HIP_VERSION of the libamdhip64 this process actually uses (major*1e7 + minor*1e5 + patch)");
+  m.def("graph_capture_info", [] {
+    py::dict d;
+    d["mode"] = std::string(capture_mode_name(capture_mode()));
+    d["forced"] = capture_mode_forced();
+    d["rccl_mode"] = std::string(capture_mode_name(rccl_capture_mode()));
+    d["root"] = std::string(graph_root_mode());
+    d["pad_streams"] = pad_streams();
+    return d;
+  }, "how schedules become hipGraphs: capture mode (schedules with RCCL between ranks: the mode "
+     "the RCCL preflight settled on), capture root, stream padding");
   m.def("device_by_pci_bus_id", [](const std::string &bus) {
     int d = -1;
     return hipDeviceGetByPCIBusId(&d, bus.c_str()) == hipSuccess ? d : -1;

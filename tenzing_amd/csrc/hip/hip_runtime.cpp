@@ -82,9 +82,7 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
   // independent 200 us kernels: 447 us per launch; with 4-8 streams owned: 241-244 us; a host
   // node then a kernel beside two kernels: 319 -> 241 us). 6: the RCCL probe between two
   // loopback ranks also stays at its unpadded time (profiles/r4_pad/)
-  int pad = 6;
-  if (const char *v = std::getenv("TZ_PAD_STREAMS")) pad = std::atoi(v);
-  for (int i = opts.n_streams; i < pad; ++i) {
+  for (int i = opts.n_streams; i < pad_streams(); ++i) {
     hipStream_t s = nullptr;
     TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     spare_.push_back(s);
@@ -483,6 +481,14 @@ GraphBuilder::GraphBuilder(const std::vector<void *> &streams, CaptureMode mode)
     abandon();
     throw;
   }
+}
+
+int pad_streams() {
+  static const int n = [] {
+    const char *v = std::getenv("TZ_PAD_STREAMS");
+    return v ? std::max(0, std::atoi(v)) : 6;
+  }();
+  return n;
 }
 
 const char *graph_root_mode() {

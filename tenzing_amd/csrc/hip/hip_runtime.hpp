@@ -247,6 +247,8 @@ private:
 /// "empty" = a graph empty node. A/B on one MI355X (profiles/r4_root/): a single root changes
 /// neither the branch probes nor the RCCL probe, and costs the headline 0.2-0.9 %
 const char *graph_root_mode();
+/// streams a runtime owns at least (env TZ_PAD_STREAMS, default 6; the spare ones are never used)
+int pad_streams();
 
 /// route the core's trace ranges (MCTS phases, schedule ops in eager runs) to roctx
 void enable_roctx(bool on);
