@@ -292,3 +292,21 @@ def test_foreign_listener_with_one_candidate_port_fails_fast():
     assert time.time() - t0 < 60
     assert ps[0].returncode != 0 and "could be bound" in errs[0], errs[0][-1500:]
     assert ps[1].returncode != 0 and "not this job's rank 0" in errs[1], errs[1][-1500:]
+
+
+def test_graph_capture_info_defaults():
+    """the record of how schedules become hipGraphs (bench.py's `graph_capture`): whole-schedule
+    capture, no extra root, 6 streams owned at least; env overrides are reported as forced"""
+    code = ("import sys, json; sys.path.insert(0, %r); import tenzing_amd as tz; "
+            "print(json.dumps(tz._tz.graph_capture_info()))" % ROOT)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("TZ_GRAPH_CAPTURE", "TZ_GRAPH_ROOT", "TZ_PAD_STREAMS")}
+    env["TZ_NO_TORCH"] = "1"
+    j = json.loads(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True,
+                                  text=True, timeout=120).stdout.strip().splitlines()[-1])
+    assert j == {"mode": "schedule", "forced": False, "rccl_mode": "schedule", "root": "none",
+                 "pad_streams": 6}, j
+    env.update(TZ_GRAPH_CAPTURE="child", TZ_PAD_STREAMS="0")
+    j = json.loads(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True,
+                                  text=True, timeout=120).stdout.strip().splitlines()[-1])
+    assert j["mode"] == "child" and j["forced"] and j["rccl_mode"] == "child" and j["pad_streams"] == 0
