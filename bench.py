@@ -523,6 +523,9 @@ def main() -> int:
            eager_ms_per_step=t_eager / args.steps * 1e3)
     rt.set_graph_unroll(args.graph_unroll)
     t_graph, eff = timed(tz.ExecMode.Graph)
+    # what the timed hipGraph is made of (kernel / host / memcpy / event nodes per iteration):
+    # e.g. whether RCCL over this node's transport adds proxy host nodes
+    graph_nodes = rt.graph_node_types() if eff == tz.ExecMode.Graph else None
     # and again after every timed exchange (ghosts of an unchanged interior must still be
     # exact): catches anything that goes wrong only in later iterations, e.g. a receiver
     # reading lines its caches kept from the previous exchange
@@ -605,6 +608,7 @@ def main() -> int:
             "peer_devices": peers,
             "runtime": runtime_libraries(),
             "graph_capture": tz._tz.graph_capture_info(),
+            "timed_graph_node_types": graph_nodes,
             "link_probe": probe,
             "elapsed_s": round(time.time() - T_START, 1),
         })
