@@ -32,6 +32,7 @@ import sys  # noqa: E402
 
 # which transport an op of a halo schedule belongs to (by op-name prefix)
 VIA_PREFIXES = (("direct", "he_direct_"), ("rccl", "he_shift_"), ("ipc", "he_put_"),
+                ("ipc_wide", "he_putw_"),
                 ("sdma", "he_copyput_"), ("memcpy", "he_mcput_"), ("relay", "he_rl"),
                 ("hostsplit", "he_hs"), ("host", "he_hostxfer"))
 
@@ -72,7 +73,7 @@ def link_probe(tz, halo, ctrl, iters, rccl=False):
         return None
     face = 8.0 * halo.box_elems(i)
     rates = {}
-    for via in ("put", "sdma", "memcpy") + (("rccl",) if rccl else ()):
+    for via in ("put", "put_wide", "sdma", "memcpy") + (("rccl",) if rccl else ()):
         try:
             t = halo.link_probe(i, via, iters, ctrl)
             rates[via] = face / t / 1e9
@@ -84,7 +85,7 @@ def link_probe(tz, halo, ctrl, iters, rccl=False):
     # engines, or one of each concurrently -- what the busiest link carries in practice
     pair = {}
     if not halo.is_direct(halo.opposite(i)):
-        for how in ("put", "sdma", "mixed"):
+        for how in ("put", "put_wide", "sdma", "mixed"):
             try:
                 t = halo.link_probe(i, "pair_" + how, iters, ctrl)
                 pair[how] = 2.0 * face / t / 1e9
@@ -149,6 +150,12 @@ def main() -> int:
                          "beside xGMI (auto), never, or only it")
     ap.add_argument("--hostsplit-chunks", type=int, default=1,
                     help="host share pipelined in this many chunks (1: all stores, then the DMA)")
+    ap.add_argument("--wide-puts", default="auto", choices=["auto", "on", "off"],
+                    help="several ranks, ipc: offer kernel puts with --wide-put-blocks "
+                         "workgroups per box beside the default 64 (auto: when the peers sit "
+                         "on other devices, i.e. puts cross xGMI)")
+    ap.add_argument("--wide-put-blocks", type=int, default=256,
+                    help="workgroups per box of the wide put")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=0,
@@ -247,7 +254,8 @@ def main() -> int:
     cfg = HaloConfig(n=args.n, neighbors=args.neighbors, fuse=args.fuse, order=args.order,
                      transport=args.transport, rank_grid=grid, stencil=args.stencil,
                      relay=args.relay, hostsplit=args.hostsplit,
-                     hostsplit_chunks=args.hostsplit_chunks)
+                     hostsplit_chunks=args.hostsplit_chunks, wide_puts=args.wide_puts,
+                     wide_put_blocks=args.wide_put_blocks)
 
     # the JSON line: every field known up front, so that the deadline can print it partially
     out = {
@@ -602,6 +610,7 @@ def main() -> int:
             "relay_offered": halo.uses_relay(),
             "hostsplit_offered": halo.uses_hostsplit(),
             "hostsplit_chunks": cfg.hostsplit_chunks if halo.uses_hostsplit() else None,
+            "wide_puts_offered": halo.uses_wide_puts(),
             "cpus_bound": len(cpus) or None,
             "rccl_socket_ifname": os.environ.get("NCCL_SOCKET_IFNAME") if world > 1 else None,
             "xgmi_topology": topo,
@@ -626,6 +635,7 @@ def main() -> int:
                             "hostsplit": args.hostsplit,
                             "hostsplit_fracs": ",".join(str(f) for f in cfg.hostsplit_fracs),
                             "hostsplit_chunks": cfg.hostsplit_chunks,
+                            "wide_puts": args.wide_puts, "wide_put_blocks": args.wide_put_blocks,
                             "stencil": bool(args.stencil), "rank_grid": args.rank_grid},
                    "schedule": json.loads(best.json(True))}
             with open(args.save_best, "w") as f:

@@ -39,7 +39,8 @@ def _build_workload(a, ctrl, device, setup):
                     relay_fracs=tuple(float(f) for f in a.relay_fracs.split(",")),
                     hostsplit=a.hostsplit,
                     hostsplit_fracs=tuple(float(f) for f in a.hostsplit_fracs.split(",")),
-                    hostsplit_chunks=a.hostsplit_chunks, rank_grid=grid)
+                    hostsplit_chunks=a.hostsplit_chunks, rank_grid=grid,
+                    wide_puts=a.wide_puts, wide_put_blocks=a.wide_put_blocks)
     sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport,
                     matrix=a.spmv_matrix, library=a.spmv_library)
     if a.workload == "halo":
@@ -180,7 +181,8 @@ def cmd_search(a) -> int:
 # (the same keys, with the same meaning, as `tz-search --save-best` writes)
 _WORKLOAD_KEYS = ("workload", "noop_width", "streams", "halo_n", "nq", "ghost", "neighbors",
                   "order", "fuse", "transport", "relay", "relay_fracs", "hostsplit",
-                  "hostsplit_fracs", "hostsplit_chunks", "stencil", "rank_grid",
+                  "hostsplit_fracs", "hostsplit_chunks", "wide_puts", "wide_put_blocks",
+                  "stencil", "rank_grid",
                   "spmv_m", "spmv_matrix", "spmv_form", "spmv_transport", "spmv_library",
                   "cu_partition", "stream_priorities")
 
@@ -410,6 +412,11 @@ def _parser() -> argparse.ArgumentParser:
                    help="host shares offered to the search (comma-separated)")
     s.add_argument("--hostsplit-chunks", type=int, default=1,
                    help="host share pipelined in this many chunks (1: store, then DMA)")
+    s.add_argument("--wide-puts", default="auto", choices=["auto", "on", "off"],
+                   help="halo, ipc: offer kernel puts with --wide-put-blocks workgroups per box "
+                        "beside the default (auto: when peers sit on other devices)")
+    s.add_argument("--wide-put-blocks", type=int, default=256,
+                   help="workgroups per box of the wide put")
     s.add_argument("--stencil", action="store_true",
                    help="halo: add the 7-point stencil (interior beside / shell after the exchange)")
     s.add_argument("--rank-grid", default="", help="halo rank grid PXxPYxPZ (default: prime factors)")

@@ -913,6 +913,8 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("hostsplit", &HaloArgs::hostsplit)
       .def_readwrite("hostsplit_fracs", &HaloArgs::hostsplit_fracs)
       .def_readwrite("hostsplit_chunks", &HaloArgs::hostsplit_chunks)
+      .def_readwrite("wide_puts", &HaloArgs::wide_puts)
+      .def_readwrite("wide_put_blocks", &HaloArgs::wide_put_blocks)
       .def_readwrite("device", &HaloArgs::device)
       .def("json", [](const HaloArgs &a) { return a.json().dump(); });
   py::class_<HaloExchange, std::shared_ptr<HaloExchange>>(m, "HaloExchange")
@@ -965,6 +967,7 @@ PYBIND11_MODULE(_tz, m) {
       .def("uses_ipc", &HaloExchange::uses_ipc)
       .def("uses_relay", &HaloExchange::uses_relay)
       .def("uses_hostsplit", &HaloExchange::uses_hostsplit)
+      .def("uses_wide_puts", &HaloExchange::uses_wide_puts)
       .def("hostsplit_parts", &HaloExchange::hs_parts, py::arg("frac"))
       .def("relay_faces", &HaloExchange::relay_faces)
       .def("link_probe", [](HaloExchange &h, int dir, const std::string &via, int iters, Ctrl *c) {
@@ -972,7 +975,9 @@ PYBIND11_MODULE(_tz, m) {
            }, py::arg("dir"), py::arg("via"), py::arg("iters"), py::arg("ctrl"),
            py::call_guard<py::gil_scoped_release>())
       .def("ipc_mode", &HaloExchange::ipc_mode)
-      .def("put_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.put_group(d, P(s)); })
+      .def("put_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s, int maxBlocks) {
+             h.put_group(d, P(s), maxBlocks);
+           }, py::arg("dirs"), py::arg("stream"), py::arg("max_blocks") = 0)
       .def("wait_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.wait_group(d, P(s)); })
       .def("ipc_errors", &HaloExchange::ipc_errors, py::call_guard<py::gil_scoped_release>())
       .def("pipelined_dirs", &HaloExchange::pipelined_dirs)

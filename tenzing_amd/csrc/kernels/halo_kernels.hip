@@ -637,13 +637,18 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
   TZ_HIP_LAUNCH_CHECK();
 }
 
+// workgroups per box of a signalling put: the launch's own cap, else the global one
+static int put_cap(const MoveSignal &sig) {
+  return sig.max_blocks > 0 ? sig.max_blocks : box_tuning().put_max_blocks;
+}
+
 void box_move_many_signal(const MoveDesc *moves, int n, const MoveSignal &sig, void *stream) {
   if (n <= 0) return;
   if (n > kMaxBoxes) throw std::runtime_error("box_move_many_signal: too many boxes");
   if (!sig.done) throw std::runtime_error("box_move_many_signal: null block counters");
   uint32_t total = 0;
   std::vector<int> keep;
-  const DevBatch b = make_move_batch(moves, n, total, keep, box_tuning().put_max_blocks);
+  const DevBatch b = make_move_batch(moves, n, total, keep, put_cap(sig));
   if (b.n != n) throw std::runtime_error("box_move_many_signal: empty box (nothing to signal)");
   DevSignal ds{};
   ds.done = sig.done;
@@ -677,7 +682,7 @@ void box_pack_many_signal(double *grid, const BoxDesc *boxes, int n, const MoveS
     b.d[b.n] = d;
     b.block_start[b.n] = total;
     ds.flag[b.n] = sig.flag[i];
-    total += blocks_for(d, box_tuning().put_max_blocks);
+    total += blocks_for(d, put_cap(sig));
     ++b.n;
   }
   b.block_start[b.n] = total;

@@ -90,6 +90,8 @@ struct MoveSignal {
   /// system-scope release store. Boxes not in `store_mask` add 1 as usual.
   unsigned long long *count = nullptr;
   uint64_t store_mask = 0;
+  /// workgroups per box at most (0: BoxTuning::put_max_blocks)
+  int max_blocks = 0;
 };
 void box_move_many_signal(const MoveDesc *d, int n, const MoveSignal &sig, void *stream);
 /// pack boxes of `grid` into their (possibly peer-mapped) dense buffers and signal each box's

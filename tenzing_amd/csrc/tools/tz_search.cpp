@@ -63,6 +63,7 @@ void usage() {
          "  [--spmv-library adaptive|lrb|rowsplit|''] [--cu-partition] [--stencil] [--max-seqs N]\n"
          "  [--relay auto|off|force] [--relay-fracs F1,F2]\n"
          "  [--hostsplit auto|off|force] [--hostsplit-fracs F1,F2,...] [--hostsplit-chunks N]\n"
+         "  [--wide-puts auto|on|off] [--wide-put-blocks N]\n"
          "  [--ctrl auto|tcp|mpi|self] [--mpi-lib PATH] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--seed-schedule PATH] [--watchdog S]\n"
@@ -253,6 +254,8 @@ int main(int argc, char **argv) {
         }
       }
       h.hostsplit_chunks = std::stoi(opt("hostsplit-chunks", "1"));
+      h.wide_puts = opt("wide-puts", "auto");
+      h.wide_put_blocks = int(optn("wide-put-blocks", 256));
       TZ_CHECK(h.order == "xyzq" || h.order == "qxyz", "--order must be xyzq or qxyz");
       h.rank = rank;
       h.size = size;

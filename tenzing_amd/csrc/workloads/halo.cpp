@@ -41,6 +41,8 @@ Json HaloArgs::json() const {
   for (double v : hostsplit_fracs) hf.push_back(v);
   j["hostsplit_fracs"] = hf;
   j["hostsplit_chunks"] = hostsplit_chunks;
+  j["wide_puts"] = wide_puts;
+  j["wide_put_blocks"] = wide_put_blocks;
   return j;
 }
 
@@ -62,6 +64,10 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.pitch_pad >= 0 && a_.pitch_pad % 16 == 0, "pitch_pad must be a multiple of 16");
   TZ_CHECK(a_.ghost_align == 0 || a_.ghost_align == 8 || a_.ghost_align == 16,
            "ghost_align must be 0, 8 or 16");
+  TZ_CHECK(a_.wide_puts == "auto" || a_.wide_puts == "on" || a_.wide_puts == "off",
+           "wide_puts must be auto, on or off");
+  TZ_CHECK(a_.wide_put_blocks >= 1 && a_.wide_put_blocks <= 4096,
+           "wide_put_blocks must be in [1, 4096]");
 
   // rank grid: prime factors (descending) multiply the currently smallest dimension, ties to
   // the later dimension (reference halo_run_strategy.hpp:80-98: 2 -> 1x1x2, 4 -> 1x2x2)
@@ -451,6 +457,7 @@ void HaloExchange::setup(Ctrl *ctrl) {
     ctrl->barrier();
     ipc_preflight(ctrl);
     if (ipcReady_ && useCopy_ && !ipcGrid_) copy_preflight(ctrl);
+    if (ipcReady_) wide_put_preflight(ctrl);
     if (relay_ && ipcReady_) relay_preflight(ctrl);
     if (hsReady_ && ipcReady_) hostsplit_preflight(ctrl);
   }
@@ -517,6 +524,9 @@ std::map<std::string, std::string> HaloExchange::transport_report() const {
     else if (!copyWhy_[k].empty()) r[copyNames[k]] = copyWhy_[k];
     else r[copyNames[k]] = "not offered";
   }
+  if (uses_wide_puts() && ready()) r["wide_put"] = "ok (" + std::to_string(a_.wide_put_blocks) + " workgroups per box)";
+  else if (!wideWhy_.empty()) r["wide_put"] = wideWhy_;
+  else r["wide_put"] = "not offered";
   if (uses_relay() && ready()) r["relay"] = "ok";
   else if (relay_) r["relay"] = relayWhy_.empty() ? "unavailable" : relayWhy_;
   else r["relay"] = "not offered";

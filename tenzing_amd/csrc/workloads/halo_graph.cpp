@@ -74,19 +74,20 @@ private:
 };
 
 /// ipc transport: pack-free put of one direction into the neighbour's grid + arrival signal
+/// (`cap` > 0: a wide put, at most `cap` workgroups per box)
 class HaloPut : public GpuOp {
 public:
-  HaloPut(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
-  std::string name() const override { return "he_put_" + h_->dir(i_).name(); }
-  std::string kind() const override { return "HaloPut"; }
+  HaloPut(std::shared_ptr<const HaloExchange> h, int i, int cap = 0) : h_(std::move(h)), i_(i), cap_(cap) {}
+  std::string name() const override { return (cap_ ? "he_putw_" : "he_put_") + h_->dir(i_).name(); }
+  std::string kind() const override { return cap_ ? "HaloWidePut" : "HaloPut"; }
   double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
   // peer stores over one xGMI link (~60 GB/s effective)
   double cost_us() const override { return 4.0 + bytes() / 2.0 / 6.0e4; }
-  void launch(void *s, Executor &) const override { h_->put_group({i_}, s); }
+  void launch(void *s, Executor &) const override { h_->put_group({i_}, s, cap_); }
 
 private:
   std::shared_ptr<const HaloExchange> h_;
-  int i_;
+  int i_, cap_;
 };
 
 /// stencil over an interior region (stencil mode)
@@ -134,18 +135,20 @@ public:
   // UnpackRelease: unpack IPC receive buffers, then hand them back to the senders (credits)
   // CopyPut: pack locally, copy-engine (SDMA) copy into the peer's receive buffer, signal
   // MemcpyPut: the same with the runtime's choice of copy engine (hipMemcpyDeviceToDevice)
-  enum Stage { Pack, Shift, Unpack, Direct, Put, UnpackRelease, CopyPut, MemcpyPut };
-  HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag)
-      : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)) {}
+  // WidePut: Put with at most `cap` workgroups per box (HaloArgs::wide_puts)
+  enum Stage { Pack, Shift, Unpack, Direct, Put, UnpackRelease, CopyPut, MemcpyPut, WidePut };
+  HaloStageGroup(std::shared_ptr<const HaloExchange> h, Stage st, std::vector<int> dirs, std::string tag,
+                 int cap = 0)
+      : h_(std::move(h)), st_(st), dirs_(std::move(dirs)), tag_(std::move(tag)), cap_(cap) {}
   std::string name() const override {
     static const char *pre[] = {"he_pack_", "he_shift_", "he_unpack_", "he_direct_", "he_put_",
-                                "he_unpack_", "he_copyput_", "he_mcput_"};
+                                "he_unpack_", "he_copyput_", "he_mcput_", "he_putw_"};
     return pre[st_] + tag_;
   }
   std::string kind() const override {
     static const char *k[] = {"HaloPackGroup", "HaloShiftGroup", "HaloUnpackGroup",
                               "HaloDirectGroup", "HaloPutGroup", "HaloUnpackGroup",
-                              "HaloCopyPutGroup", "HaloMemcpyPutGroup"};
+                              "HaloCopyPutGroup", "HaloMemcpyPutGroup", "HaloWidePutGroup"};
     return k[st_];
   }
   double bytes() const override {
@@ -165,6 +168,7 @@ public:
     else if (st_ == Unpack) h_->unpack_group(dirs_, s);
     else if (st_ == Direct) h_->direct_group(dirs_, s);
     else if (st_ == Put) h_->put_group(dirs_, s);
+    else if (st_ == WidePut) h_->put_group(dirs_, s, cap_);
     else if (st_ == CopyPut) h_->copy_put_group(dirs_, s, /*sdma=*/true);
     else if (st_ == MemcpyPut) h_->copy_put_group(dirs_, s, /*sdma=*/false);
     else h_->ipc_unpack_group(dirs_, s);
@@ -175,6 +179,7 @@ private:
   Stage st_;
   std::vector<int> dirs_;
   std::string tag_;
+  int cap_;
 };
 
 /// relay routing stages (HaloArgs::relay): one op each, for every direction at once
@@ -373,6 +378,7 @@ void HaloExchange::add_chains(Graph &g, const std::vector<int> &dirs, int via) {
       OpPtr d;
       if (direct_[i]) d = std::make_shared<HaloDirect>(self, i);
       else if (via == kViaPut) d = std::make_shared<HaloPut>(self, i);
+      else if (via == kViaPutWide) d = std::make_shared<HaloPut>(self, i, a_.wide_put_blocks);
       else d = std::make_shared<HaloStageGroup>(
                self, via == kViaCopy ? HaloStageGroup::CopyPut : HaloStageGroup::MemcpyPut,
                std::vector<int>{i}, dirs_[i].name());
@@ -403,10 +409,12 @@ void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::
   }
   if (remote.empty()) return;
   if (via != kViaPipe) {
-    auto d = std::make_shared<HaloStageGroup>(
-        self, via == kViaPut ? HaloStageGroup::Put
-              : (via == kViaCopy ? HaloStageGroup::CopyPut : HaloStageGroup::MemcpyPut),
-        remote, tag);
+    const HaloStageGroup::Stage st =
+        via == kViaPut ? HaloStageGroup::Put
+        : via == kViaPutWide ? HaloStageGroup::WidePut
+        : (via == kViaCopy ? HaloStageGroup::CopyPut : HaloStageGroup::MemcpyPut);
+    auto d = std::make_shared<HaloStageGroup>(self, st, remote, tag,
+                                              via == kViaPutWide ? a_.wide_put_blocks : 0);
     g.start_then(d);
     g.then_finish(d);
     return;
@@ -514,9 +522,10 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via
 void HaloExchange::add_ipc_part(Graph &g, const std::vector<int> &remote, int via) {
   // puts wait only for the credit of the previous iteration, so each rank's puts all complete;
   // the arrival wait runs after them (one spinning kernel per rank, never ahead of its own
-  // puts). The copy-engine variants' op names carry "cp_" / "mc_" (unique in the expanded graph).
+  // puts). The copy-engine and wide variants' op names carry "cp_" / "mc_" / "w_" (unique in the
+  // expanded graph).
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
-  const std::string v = via == kViaCopy ? "cp_" : (via == kViaMemcpy ? "mc_" : "");
+  const std::string v = via == kViaCopy ? "cp_" : via == kViaMemcpy ? "mc_" : via == kViaPutWide ? "w_" : "";
   auto puts = std::make_shared<Graph>();
   add_structure(*puts, remote, via, v.empty() ? "ipc_" : v);
   auto c = std::make_shared<StaticCompoundOp>("he_" + v + "puts", puts);
@@ -608,6 +617,11 @@ void HaloExchange::add_exchange(Graph &g) {
     auto gr = std::make_shared<Graph>();
     add_ipc_part(*gr, remote, kViaPut);
     alts.push_back(std::make_shared<StaticCompoundOp>("he_via_ipc", gr));
+  }
+  if (ipc && uses_wide_puts()) {
+    auto gr = std::make_shared<Graph>();
+    add_ipc_part(*gr, remote, kViaPutWide);
+    alts.push_back(std::make_shared<StaticCompoundOp>("he_via_ipcw", gr));
   }
   // (each copy-engine variant only if it passed its preflight; mixed puts use the SDMA one)
   if (copy && copyOk_[1]) {

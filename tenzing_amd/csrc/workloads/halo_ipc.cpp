@@ -128,6 +128,75 @@ void HaloExchange::copy_preflight(Ctrl *ctrl) {
   init_grid();
 }
 
+void HaloExchange::wide_put_preflight(Ctrl *ctrl) {
+  // Offered or not, agreed first (the search needs the same graph on every rank): "auto" offers
+  // the wide variant when any rank's peers live on another device, where the puts cross xGMI
+  // links; ranks sharing one GPU store into their own HBM and gain nothing from it.
+  double offer = 0;
+  if (a_.wide_puts == "on") {
+    offer = 1;
+  } else if (a_.wide_puts == "auto") {
+    int dev = 0;
+    TZ_HIP(hipGetDevice(&dev));
+    for (const auto &[q, d] : ipc_peer_devices())
+      if (d >= 0 && d != dev) offer = 1;
+  }
+  ctrl->allreduce_max(&offer, 1);
+  widePuts_ = false;
+  if (offer == 0) return;
+  if (a_.wide_put_blocks == kern::box_tuning().put_max_blocks) {
+    wideWhy_ = "not offered: the same cap as the default put";
+    return;
+  }
+  // then one verified exchange with the wide launches, like copy_preflight
+  std::vector<int> local, remote;
+  for (int i = 0; i < ndirs(); ++i) {
+    if (direct_[i]) local.push_back(i);
+    else if (ipc_[i]) remote.push_back(i);
+  }
+  const double keep = ipcTimeoutS_;
+  ipcTimeoutS_ = std::min(ipcTimeoutS_, preflight_wait_s());
+  double bad = 0;
+  std::string why;
+  init_grid(nullptr, 3);
+  TZ_HIP(hipDeviceSynchronize());
+  ctrl->barrier();
+  try {
+    if (!local.empty()) direct_group(local, nullptr);
+    put_group(remote, nullptr, a_.wide_put_blocks);
+    wait_group(remote, nullptr);
+    if (!ipcGrid_) ipc_unpack_group(remote, nullptr);
+    TZ_HIP(hipDeviceSynchronize());
+  } catch (const std::exception &ex) {
+    bad = 1;
+    why = std::string("wide_put preflight: ") + ex.what();
+  }
+  ctrl->barrier(); // peers may still be putting into my ghosts until they synced
+  if (bad == 0) {
+    try {
+      const int e = ipc_errors();
+      const uint64_t cells = check_grid();
+      if (e || cells)
+        why = "wide_put preflight: " + std::to_string(e) + " wait timeout(s), " +
+              std::to_string(cells) + " wrong cells";
+      bad = why.empty() ? 0 : 1;
+    } catch (const std::exception &ex) {
+      bad = 1;
+      why = std::string("wide_put preflight check: ") + ex.what();
+    }
+  }
+  ctrl->allreduce_max(&bad, 1);
+  ipcTimeoutS_ = keep;
+  if (bad != 0) {
+    wideWhy_ = why.empty() ? "preflight failed on another rank" : why;
+    TZ_LOG(Warn, "wide_put variant disabled: " << wideWhy_);
+    reset_ipc_counters(ctrl);
+  } else {
+    widePuts_ = true;
+  }
+  init_grid();
+}
+
 std::string HaloExchange::setup_ipc(Ctrl *ctrl) {
   // Collective: every rank makes the same control-plane calls (one allgather) whatever fails
   // locally, and reports failure as a string, so a rank that cannot export or map never leaves
@@ -256,12 +325,13 @@ std::map<int, int> HaloExchange::ipc_peer_devices() const {
   return out;
 }
 
-void HaloExchange::put_group(const std::vector<int> &dirs, void *stream) const {
+void HaloExchange::put_group(const std::vector<int> &dirs, void *stream, int max_blocks) const {
   TZ_CHECK(ready() && ipcReady_, "ipc transport not set up");
   TZ_CHECK(!dirs.empty() && dirs.size() <= size_t(kern::kMaxBoxes), "bad put group");
   std::vector<kern::MoveDesc> ms;
   std::vector<kern::BoxDesc> bs;
   kern::MoveSignal sig;
+  sig.max_blocks = max_blocks;
   // block counters: one slot range per group, keyed by its first direction (groups of one
   // schedule are disjoint, so concurrently running puts never share counters)
   sig.done = done_.as<unsigned int>() + size_t(dirs.front()) * kern::kMaxBoxes;
@@ -485,6 +555,9 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
   // dimension has 2 ranks), by kernel puts, copy engines, or one of each on two streams
   const bool pair = via.rfind("pair_", 0) == 0;
   const std::string how = pair ? via.substr(5) : via;
+  // "put_wide": the kernel put with HaloArgs::wide_put_blocks workgroups per box
+  const bool isPut = how == "put" || how == "put_wide";
+  const int cap = how == "put_wide" ? a_.wide_put_blocks : 0;
   const std::vector<int> d = pair ? std::vector<int>{dir, opp_[dir]} : std::vector<int>{dir};
   hipStream_t s = nullptr, s2 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
@@ -501,10 +574,10 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
     TZ_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
   }
   auto once = [&] {
-    if (pair && (how == "put" || how == "sdma" || how == "mixed")) {
+    if (pair && (isPut || how == "sdma" || how == "mixed")) {
       TZ_CHECK(ipcReady_ && ipc_[d[0]] && ipc_[d[1]], "ipc transport not available");
-      if (how == "put") {
-        put_group(d, s);
+      if (isPut) {
+        put_group(d, s, cap);
       } else if (how == "sdma") {
         copy_put_group(d, s);
       } else { // + face by CU stores on s, - face by the copy engines on s2, concurrently
@@ -518,10 +591,10 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
       wait_group(d, s);
       if (!ipcGrid_) ipc_unpack_group(d, s);
     } else if (pair) {
-      TZ_THROW("pair probes take put, sdma or mixed (got " << how << ")");
-    } else if (via == "put" || via == "sdma" || via == "memcpy") {
+      TZ_THROW("pair probes take put, put_wide, sdma or mixed (got " << how << ")");
+    } else if (isPut || via == "sdma" || via == "memcpy") {
       TZ_CHECK(ipcReady_ && ipc_[dir], "ipc transport not available");
-      if (via == "put") put_group(d, s);
+      if (isPut) put_group(d, s, cap);
       else copy_put_group(d, s, via == "sdma");
       wait_group(d, s);
       if (!ipcGrid_) ipc_unpack_group(d, s);
@@ -531,14 +604,13 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
       shift_group(d, s, 0);
       unpack_group(d, s);
     } else {
-      TZ_THROW("link probe transport must be put, sdma, memcpy or rccl (got " << via << ")");
+      TZ_THROW("link probe transport must be put, put_wide, sdma, memcpy or rccl (got " << via << ")");
     }
   };
   // agree collectively that every rank can run the probe before any transfer is issued
   std::string err;
   const bool ipcOk = ipcReady_ && ipc_[dir] && (!pair || ipc_[opp_[dir]]);
-  if ((how == "put" || how == "sdma" || how == "mixed") &&
-      !(ipcOk && (how == "put" || (useCopy_ && !ipcGrid_))))
+  if ((isPut || how == "sdma" || how == "mixed") && !(ipcOk && (isPut || (useCopy_ && !ipcGrid_))))
     err = via + " unavailable";
   if (via == "rccl" && !(useRccl_ && pipe_[dir])) err = "rccl unavailable";
   double bad = err.empty() ? 0.0 : 1.0;

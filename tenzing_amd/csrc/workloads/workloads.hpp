@@ -212,6 +212,13 @@ struct HaloArgs {
   // stores, then one DMA): 4 chunks measured 7-17 % slower on 2 loopback ranks, whose PCIe
   // link sees the same store / read-back mix as one GPU's link on a node (profiles/r3_hs_chunks)
   int hostsplit_chunks = 1;
+  // wide kernel puts: the IPC put kernels with `wide_put_blocks` workgroups per box instead of
+  // the global cap (TZ_PUT_MAX_BLOCKS, 64), offered to the search as a transport alternative.
+  // One loopback GPU has no link to fill, so 64 won there; whether more workgroups in flight
+  // fill an xGMI link better is the node's to measure. "auto": offered when a peer's memory
+  // sits on another device (agreed by every rank); "on": always (tests); "off"
+  std::string wide_puts = "auto";
+  int wide_put_blocks = 256;
   int device = -1;
   Json json() const;
 };
@@ -323,7 +330,8 @@ public:
   }
   /// ipc transport: put my slabs facing `dirs` into the neighbours' ghost regions and signal
   /// their arrival counters (one launch)
-  void put_group(const std::vector<int> &dirs, void *stream) const;
+  /// (`max_blocks`: workgroups per box at most, 0 = the global cap)
+  void put_group(const std::vector<int> &dirs, void *stream, int max_blocks = 0) const;
   /// ipc transport, copy-engine variant ("buffers" mode): pack locally, hipMemcpyAsync into the
   /// neighbours' receive buffers, then signal their arrival counters. `sdma`: force the SDMA
   /// engines (no CUs); otherwise the runtime picks the copy engine
@@ -361,6 +369,11 @@ public:
   /// of the direct senders and of the forwarders
   void relay_unpack(const std::vector<int> &dirs, const std::vector<int> &faces, double frac,
                     void *stream) const;
+  /// wide kernel puts (see HaloArgs::wide_puts) are offered: agreed and preflighted at setup;
+  /// for graph-only builds when wide_puts is "on"
+  bool uses_wide_puts() const {
+    return useIpc_ && (ready() ? ipcReady_ && widePuts_ : a_.wide_puts == "on");
+  }
   /// the face directions among the remote ones (what relay routing splits)
   std::vector<int> relay_faces() const;
   /// host split (HaloArgs::hostsplit) is available: ipc buffers mode, shared host memory mapped
@@ -389,7 +402,8 @@ public:
   int hs_parts(double frac) const;
   /// Link probe (collective): every rank moves its slab facing direction `dir` to its
   /// neighbour there, `iters` times, through `via` ("put": kernel stores into the peer's
-  /// memory, "sdma": copy engines, "rccl": pack + RCCL send/recv + unpack), one transfer at a
+  /// memory, "put_wide": the same with HaloArgs::wide_put_blocks workgroups per box, "sdma":
+  /// copy engines, "rccl": pack + RCCL send/recv + unpack), one transfer at a
   /// time on one stream. Each transfer crosses one xGMI link per rank, so this measures what one
   /// link carries with that transport. "pair_put" / "pair_sdma" / "pair_mixed" move both faces
   /// of the axis at once (kernel puts, copy engines, or the + face by kernel and the - face by
@@ -404,8 +418,8 @@ public:
 private:
   // graph builders; remote directions go through `via`: pack/transfer/unpack (kViaPipe), IPC
   // puts (kViaPut), copy-engine puts on the SDMA engines (kViaCopy) or with the runtime's copy
-  // engine (kViaMemcpy)
-  static constexpr int kViaPipe = 0, kViaPut = 1, kViaCopy = 2, kViaMemcpy = 3;
+  // engine (kViaMemcpy), wide kernel puts (kViaPutWide)
+  static constexpr int kViaPipe = 0, kViaPut = 1, kViaCopy = 2, kViaMemcpy = 3, kViaPutWide = 4;
   void add_chains(Graph &g, const std::vector<int> &dirs, int via);
   void add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag, int via);
   void add_structure(Graph &g, const std::vector<int> &dirs, int via,
@@ -466,6 +480,12 @@ private:
   /// one verified exchange per copy-engine put variant before the search may use it (the
   /// kernel-put preflight does not exercise the copy engines' peer path); collective
   void copy_preflight(Ctrl *ctrl);
+  // wide kernel puts: offered (HaloArgs::wide_puts, agreed) and their preflight passed
+  bool widePuts_ = false;
+  std::string wideWhy_;
+  /// decide whether wide puts are offered (collective) and verify them with one exchange of
+  /// their own; a failure drops only that variant
+  void wide_put_preflight(Ctrl *ctrl);
   // copy-engine puts can spread every copy over this many streams (one SDMA engine each; env
   // TZ_COPY_ENGINES). One engine moves ~60 GB/s, and independent copies on 2 / 4 streams reach
   // 120 / 235 GB/s. Forking the chunks from the op's stream and joining them back through events

@@ -40,6 +40,10 @@ class HaloConfig:
     hostsplit: str = "auto"
     hostsplit_fracs: tuple = (0.1, 0.2, 0.3, 0.4)  # host shares offered (ChoiceOp)
     hostsplit_chunks: int = 1  # host share pipelined in this many chunks
+    # IPC kernel puts with more workgroups per box, offered beside the default put: "auto"
+    # (when peers sit on other devices), "on", "off"
+    wide_puts: str = "auto"
+    wide_put_blocks: int = 256
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":
         a = _tz.HaloArgs()
@@ -59,6 +63,8 @@ class HaloConfig:
         a.hostsplit = self.hostsplit
         a.hostsplit_fracs = [float(f) for f in self.hostsplit_fracs]
         a.hostsplit_chunks = int(self.hostsplit_chunks)
+        a.wide_puts = self.wide_puts
+        a.wide_put_blocks = int(self.wide_put_blocks)
         if self.rank_grid:
             a.px, a.py, a.pz = (int(v) for v in self.rank_grid)
         a.rank, a.size, a.device = rank, size, device

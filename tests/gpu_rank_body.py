@@ -43,6 +43,7 @@ def main():
                                             transport=os.environ.get("TZ_TEST_TRANSPORT", "ipc"),
                                             fuse=fuse, stencil=stencil, relay=relay,
                                             hostsplit=hostsplit,
+                                            wide_puts=os.environ.get("TZ_TEST_WIDE", "auto"),
                                             comms=int(os.environ.get("TZ_TEST_COMMS", "0")),
                                             hostsplit_chunks=int(os.environ.get("TZ_TEST_HS_CHUNKS", "1"))),
                                ctrl, dev)
@@ -104,7 +105,8 @@ def main():
                                     relay=any(o.name.startswith("he_rl") for o in seq.ops()),
                                     relay_sdma=any(o.name.endswith("_fwdcp") for o in seq.ops()),
                                     hostsplit=any(o.name.startswith("he_hs") for o in seq.ops()),
-                                    mixed=any(o.name == "he_copyput_mx" for o in seq.ops())))
+                                    mixed=any(o.name == "he_copyput_mx" for o in seq.ops()),
+                                    wide=any(o.name.startswith("he_putw_") for o in seq.ops())))
             if os.environ.get("TZ_TEST_NO_MCTS"):
                 continue
             # a short collective search over ipc schedules

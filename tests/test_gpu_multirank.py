@@ -166,6 +166,22 @@ def test_copy_puts_over_two_engines_loopback(gpu):
             assert run["bad1"] == run["bad2"] == run["bad3"] == 0 and run["err"] == 0, run
 
 
+@pytest.mark.parametrize("grid_mode", ["1", "0"])
+def test_wide_puts_loopback(gpu, grid_mode):
+    """wide kernel puts (256 workgroups per box, forced on: loopback ranks share one GPU, where
+    "auto" does not offer them): preflighted at setup, then exact eager and as hipGraphs over
+    repeated exchanges, in grid and buffers mode"""
+    extra = {"TZ_IPC_GRID": grid_mode, "TZ_TEST_WIDE": "on", "TZ_TEST_FUSES": "none,choice",
+             "TZ_TEST_REQUIRE": "he_putw_", "TZ_TEST_SEEDS": "2", "TZ_TEST_NO_MCTS": "1"}
+    res = _launch("ipc_halo", 2, extra_env=extra)
+    for r in res:
+        assert r["transports"]["wide_put"].startswith("ok"), r["transports"]
+        assert "he_via_ipcw" in r["graph_ops"]
+        assert r["runs"] and all(run["wide"] for run in r["runs"]), r["runs"]
+        for run in r["runs"]:
+            assert run["bad1"] == run["bad2"] == run["bad3"] == 0 and run["err"] == 0, run
+
+
 def test_relay_routing_loopback(gpu):
     """the 2x2x2 grid with every remote direction through relay routing (a share of each face
     via the corner peer, forwarded over its edge-diagonal link): every ghost right on all 8
@@ -259,6 +275,10 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     p = j["link_probe"]
     # kernel puts always; copy-engine puts need receive buffers; RCCL is refused in loopback
     assert p["GBps"]["put"] > 0 and "rccl" not in p["GBps"]
+    # the wide kernel put is probed everywhere but offered to the search only where peers sit on
+    # other devices ("auto")
+    assert p["GBps"]["put_wide"] > 0 and p["pair_GBps"]["put_wide"] > 0
+    assert j["wide_puts_offered"] is False
     assert (p["GBps"]["sdma"] is not None) == (mode == "buffers")
     assert (p["GBps"]["memcpy"] is not None) == (mode == "buffers")
     # both z faces at once (2 ranks: one peer): kernel puts always, copy engines and the

@@ -368,3 +368,53 @@ def test_host_share_chunk_count_is_the_same_for_every_face(tz):
     assert h.hostsplit_parts(0.1) == 3 and h.hostsplit_parts(0.2) == 4
     a.hostsplit_chunks = 1
     assert tz.HaloExchange(a).hostsplit_parts(0.2) == 1
+
+
+@pytest.mark.parametrize("fuse", ["none", "all", "groups", "choice"])
+@pytest.mark.parametrize("grid_mode", ["1", "0"])
+def test_wide_puts_are_a_transport_alternative(tz, monkeypatch, fuse, grid_mode):
+    """wide_puts="on": the IPC put again with more workgroups per box, as its own he_remote
+    alternative ("he_via_ipcw"); its ops carry "he_putw_" / "w_" and never mix with the
+    default put's. Graph-only builds offer it only when asked ("auto" decides at setup)."""
+    from tenzing_amd.search import choice_alternatives, greedy_schedule
+
+    monkeypatch.setenv("TZ_IPC_GRID", grid_mode)
+    a = tz.HaloArgs()
+    a.nx = a.ny = a.nz = 16
+    a.neighbors, a.fuse, a.rank, a.size, a.hostsplit, a.relay = 26, fuse, 0, 8, "off", "off"
+    h0 = tz.HaloExchange(a)
+    g0 = tz.Graph()
+    h0.add_to_graph(g0)
+    assert not h0.uses_wide_puts()
+    assert "he_via_ipcw" not in choice_alternatives(g0, "he_remote")
+    a.wide_puts = "on"
+    h = tz.HaloExchange(a)
+    g = tz.Graph()
+    h.add_to_graph(g)
+    assert h.uses_wide_puts()
+    assert "he_via_ipcw" in choice_alternatives(g, "he_remote")
+    p = tz.Platform(3)
+    s = greedy_schedule(g, p, {"he_remote": "he_via_ipcw"})
+    names = [o.name for o in s.ops() if isinstance(o, tz._tz.BoundGpuOp)]
+    wide = [n for n in names if n.startswith("he_putw_")]
+    assert wide and not any(n.startswith("he_put_") for n in names)
+    w = names.index("he_wait_w_remote")
+    assert max(names.index(n) for n in wide) < w
+    if fuse == "none":
+        assert len(wide) == 26
+    assert tz.verify(s, tz.resolve_graph(g, s), 3) == []
+    kinds = {o.kind for o in s.ops()}
+    assert kinds & {"HaloWidePut", "HaloWidePutGroup"}
+
+
+def test_wide_put_args_are_checked(tz):
+    a = tz.HaloArgs()
+    a.nx = a.ny = a.nz = 16
+    a.wide_puts = "sometimes"
+    with pytest.raises(Exception, match="wide_puts"):
+        tz.HaloExchange(a)
+    a.wide_puts, a.wide_put_blocks = "on", 0
+    with pytest.raises(Exception, match="wide_put_blocks"):
+        tz.HaloExchange(a)
+    a.wide_put_blocks = 128
+    assert '"wide_put_blocks":128' in a.json().replace(" ", "")

@@ -75,10 +75,10 @@ def rccl_positions(seq):
     return [p for p, op in enumerate(seq.ops()) if op.order_domain == "rccl"]
 
 
-def _halo(tz, size, transport="auto", fuse="choice"):
+def _halo(tz, size, transport="auto", fuse="choice", wide_puts="auto"):
     a = tz.HaloArgs()
     a.nx = a.ny = a.nz = 16
-    a.neighbors, a.transport, a.fuse = 26, transport, fuse
+    a.neighbors, a.transport, a.fuse, a.wide_puts = 26, transport, fuse, wide_puts
     a.rank, a.size = 0, size
     h = tz.HaloExchange(a)
     g = tz.Graph()
@@ -297,12 +297,14 @@ def test_one_seed_per_transport(tz, monkeypatch):
     from tenzing_amd.search import choice_alternatives, greedy_schedule
 
     monkeypatch.setenv("TZ_IPC_GRID", "0")
-    h, g = _halo(tz, 8)
+    h, g = _halo(tz, 8, wide_puts="on")
     alts = choice_alternatives(g, "he_remote")
-    assert {"he_via_rccl", "he_via_ipc", "he_via_sdma", "he_via_memcpy", "he_via_mixed"} <= set(alts)
+    assert {"he_via_rccl", "he_via_ipc", "he_via_ipcw", "he_via_sdma", "he_via_memcpy",
+            "he_via_mixed"} <= set(alts)
     assert any(a.startswith("he_via_relay") for a in alts)
     p = tz.Platform(4)
-    key = {"he_via_rccl": "he_shift_", "he_via_ipc": "he_put_", "he_via_sdma": "he_copyput_",
+    key = {"he_via_rccl": "he_shift_", "he_via_ipc": "he_put_", "he_via_ipcw": "he_putw_",
+           "he_via_sdma": "he_copyput_",
            "he_via_memcpy": "he_mcput_", "he_via_mixed": "he_wait_mx", "he_via_hs10": "he_hs10", "he_via_hs20": "he_hs20",
            "he_via_hs30": "he_hs30", "he_via_hs40": "he_hs40"}
     seeds = []
