@@ -132,12 +132,22 @@ void HaloExchange::wide_put_preflight(Ctrl *ctrl) {
   // Offered or not, agreed first (the search needs the same graph on every rank): "auto" offers
   // the wide variant when any rank's peers live on another device, where the puts cross xGMI
   // links; ranks sharing one GPU store into their own HBM and gain nothing from it.
+  // Which device a peer sits on: its PCI bus id (allgathered; every rank makes this call), and
+  // the device the runtime reports for the peer memory mapped here (which may name the importing
+  // device even for another GPU's memory, so the bus id decides as well).
+  int dev = 0;
+  TZ_HIP(hipGetDevice(&dev));
+  char bus[64] = {};
+  if (hipDeviceGetPCIBusId(bus, int(sizeof(bus)), dev) != hipSuccess) bus[0] = 0;
+  const std::vector<std::string> buses = ctrl->allgather(std::string(bus));
   double offer = 0;
   if (a_.wide_puts == "on") {
     offer = 1;
   } else if (a_.wide_puts == "auto") {
-    int dev = 0;
-    TZ_HIP(hipGetDevice(&dev));
+    for (int i = 0; i < ndirs(); ++i)
+      if (ipc_[i] && size_t(nbr_[i]) < buses.size() && !buses[size_t(nbr_[i])].empty() &&
+          buses[size_t(nbr_[i])] != std::string(bus))
+        offer = 1;
     for (const auto &[q, d] : ipc_peer_devices())
       if (d >= 0 && d != dev) offer = 1;
   }
