@@ -968,6 +968,9 @@ PYBIND11_MODULE(_tz, m) {
       .def("uses_relay", &HaloExchange::uses_relay)
       .def("uses_hostsplit", &HaloExchange::uses_hostsplit)
       .def("uses_wide_puts", &HaloExchange::uses_wide_puts)
+      .def_static("wide_puts_offered", &HaloExchange::wide_puts_offered, py::arg("mode"),
+                  py::arg("my_bus"), py::arg("peer_buses"), py::arg("my_device"),
+                  py::arg("mapped_devices"))
       .def("hostsplit_parts", &HaloExchange::hs_parts, py::arg("frac"))
       .def("relay_faces", &HaloExchange::relay_faces)
       .def("link_probe", [](HaloExchange &h, int dir, const std::string &via, int iters, Ctrl *c) {

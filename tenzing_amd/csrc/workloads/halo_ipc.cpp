@@ -128,6 +128,18 @@ void HaloExchange::copy_preflight(Ctrl *ctrl) {
   init_grid();
 }
 
+bool HaloExchange::wide_puts_offered(const std::string &mode, const std::string &myBus,
+                                     const std::vector<std::string> &peerBuses, int myDevice,
+                                     const std::vector<int> &mappedDevices) {
+  if (mode == "on") return true;
+  if (mode != "auto") return false;
+  for (const std::string &b : peerBuses)
+    if (!b.empty() && !myBus.empty() && b != myBus) return true;
+  for (int d : mappedDevices)
+    if (d >= 0 && d != myDevice) return true;
+  return false;
+}
+
 void HaloExchange::wide_put_preflight(Ctrl *ctrl) {
   // Offered or not, agreed first (the search needs the same graph on every rank): "auto" offers
   // the wide variant when any rank's peers live on another device, where the puts cross xGMI
@@ -140,17 +152,12 @@ void HaloExchange::wide_put_preflight(Ctrl *ctrl) {
   char bus[64] = {};
   if (hipDeviceGetPCIBusId(bus, int(sizeof(bus)), dev) != hipSuccess) bus[0] = 0;
   const std::vector<std::string> buses = ctrl->allgather(std::string(bus));
-  double offer = 0;
-  if (a_.wide_puts == "on") {
-    offer = 1;
-  } else if (a_.wide_puts == "auto") {
-    for (int i = 0; i < ndirs(); ++i)
-      if (ipc_[i] && size_t(nbr_[i]) < buses.size() && !buses[size_t(nbr_[i])].empty() &&
-          buses[size_t(nbr_[i])] != std::string(bus))
-        offer = 1;
-    for (const auto &[q, d] : ipc_peer_devices())
-      if (d >= 0 && d != dev) offer = 1;
-  }
+  std::vector<std::string> peerBuses;
+  for (int i = 0; i < ndirs(); ++i)
+    if (ipc_[i] && size_t(nbr_[i]) < buses.size()) peerBuses.push_back(buses[size_t(nbr_[i])]);
+  std::vector<int> mapped;
+  for (const auto &[q, d] : ipc_peer_devices()) mapped.push_back(d);
+  double offer = wide_puts_offered(a_.wide_puts, bus, peerBuses, dev, mapped) ? 1 : 0;
   ctrl->allreduce_max(&offer, 1);
   widePuts_ = false;
   if (offer == 0) return;

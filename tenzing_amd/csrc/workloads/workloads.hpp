@@ -374,6 +374,13 @@ public:
   bool uses_wide_puts() const {
     return useIpc_ && (ready() ? ipcReady_ && widePuts_ : a_.wide_puts == "on");
   }
+  /// this rank's wide-put offer (before the agreement, which takes the max over ranks): "on"
+  /// always, "off" never, "auto" when a peer of an IPC direction has another PCI bus id than
+  /// mine, or the runtime maps a peer's memory on another device than mine (empty bus ids and
+  /// negative devices are unknown and decide nothing)
+  static bool wide_puts_offered(const std::string &mode, const std::string &myBus,
+                                const std::vector<std::string> &peerBuses, int myDevice,
+                                const std::vector<int> &mappedDevices);
   /// the face directions among the remote ones (what relay routing splits)
   std::vector<int> relay_faces() const;
   /// host split (HaloArgs::hostsplit) is available: ipc buffers mode, shared host memory mapped

@@ -418,3 +418,21 @@ def test_wide_put_args_are_checked(tz):
         tz.HaloExchange(a)
     a.wide_put_blocks = 128
     assert '"wide_put_blocks":128' in a.json().replace(" ", "")
+
+
+def test_wide_put_offer_on_a_fake_topology(tz):
+    """the per-rank decision behind wide_puts="auto": peers on other GPUs (another PCI bus id, or
+    peer memory the runtime maps on another device) offer the wide put; loopback ranks (every
+    peer on my bus / device) do not; unknown facts decide nothing"""
+    offered = tz._tz.HaloExchange.wide_puts_offered
+    me = "0000:05:00.0"
+    # an 8-GPU node: the IPC peers sit on other buses, whatever the mapping reports
+    assert offered("auto", me, ["0000:15:00.0", "0000:65:00.0"], 0, [0, 0])
+    # ... or only the mapping knows (bus ids unavailable)
+    assert offered("auto", "", ["", ""], 0, [3])
+    # loopback: all on my GPU
+    assert not offered("auto", me, [me, me.upper().lower()], 0, [0, 0])
+    assert not offered("auto", me, ["", me], 0, [-1])
+    # forced either way
+    assert offered("on", me, [me], 0, [0])
+    assert not offered("off", me, ["0000:15:00.0"], 0, [1])
