@@ -21,7 +21,7 @@ if [ -z "${SKIP_N1:-}" ]; then
   fi
 fi
 port=29810
-for n in ${NS:-2 4 8}; do
+for n in ${NS:-2 4}; do
   port=$((port+1))
   timeout -k 10 ${NT:-560} python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
     --master-port $port bench.py --gpus $n --steps 20 --warmup 5 ${BENCH_ARGS:-} \

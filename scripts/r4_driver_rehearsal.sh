@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4. The driver's commands on one GPU: N=1 bench (+ a rocprofv3 kernel-stats pass), then the
 # multi-rank command with N loopback ranks (all on this GPU; flow and robustness, not xGMI speed).
+# N=8 is the driver's own case (its 8-GPU node) and is not run here by default.
 # Every step has its own time limit; a crash, abort or time limit stops the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -22,7 +23,7 @@ if [ -z "${SKIP_N1:-}" ]; then
   fi
 fi
 port=29810
-for n in ${NS:-2 4 8}; do
+for n in ${NS:-2 4}; do
   port=$((port+1))
   timeout -k 10 ${NT:-560} python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
     --master-port $port bench.py --gpus $n --steps 20 --warmup 5 ${BENCH_ARGS:-} \
