@@ -93,6 +93,16 @@ def link_probe(tz, halo, ctrl, iters, rccl=False):
                 pair[how] = None
                 if ctrl.rank == 0:
                     print(f"bench.py: link probe pair_{how}: {e}", file=sys.stderr)
+    # the kernel put's width over the same link: workgroups per box (the default put runs 64,
+    # the wide put 256); on a node this says which width fills an xGMI link
+    by_cap = {}
+    for cap in (16, 64, 256, 1024):
+        try:
+            by_cap[str(cap)] = face / halo.link_probe(i, f"put_cap{cap}", iters, ctrl) / 1e9
+        except Exception as e:  # noqa: BLE001  (collective: every rank skips together)
+            by_cap[str(cap)] = None
+            if ctrl.rank == 0:
+                print(f"bench.py: link probe put_cap{cap}: {e}", file=sys.stderr)
     # the other axes' face links too (kernel puts): are the links of one node alike?
     by_axis = {"z": rates.get("put")}
     for name, d in (("x", (1, 0, 0)), ("y", (0, 1, 0))):
@@ -112,6 +122,7 @@ def link_probe(tz, halo, ctrl, iters, rccl=False):
     busiest = max(per_peer.values()) if per_peer else 0.0
     best = max([r for r in list(rates.values()) + list(pair.values()) if r], default=None)
     return {"face_MB": face / 1e6, "GBps": rates, "pair_GBps": pair, "put_GBps_by_axis": by_axis,
+            "put_GBps_by_blocks_per_box": by_cap,
             "busiest_link_MB": busiest / 1e6,
             "busiest_link_at_probe_rate_ms": (busiest / (best * 1e9) * 1e3) if best else None}
 

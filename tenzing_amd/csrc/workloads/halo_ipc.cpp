@@ -572,9 +572,15 @@ double HaloExchange::link_probe(int dir, const std::string &via, int iters, Ctrl
   // dimension has 2 ranks), by kernel puts, copy engines, or one of each on two streams
   const bool pair = via.rfind("pair_", 0) == 0;
   const std::string how = pair ? via.substr(5) : via;
-  // "put_wide": the kernel put with HaloArgs::wide_put_blocks workgroups per box
-  const bool isPut = how == "put" || how == "put_wide";
-  const int cap = how == "put_wide" ? a_.wide_put_blocks : 0;
+  // "put_wide": the kernel put with HaloArgs::wide_put_blocks workgroups per box; "put_cap<N>":
+  // with N workgroups per box (a sweep of the put width over one link)
+  const bool capped = how.rfind("put_cap", 0) == 0;
+  const bool isPut = how == "put" || how == "put_wide" || capped;
+  int cap = how == "put_wide" ? a_.wide_put_blocks : 0;
+  if (capped) {
+    cap = std::atoi(how.c_str() + 7);
+    TZ_CHECK(cap >= 1 && cap <= 4096, "put_cap<N> needs 1 <= N <= 4096 (got " << how << ")");
+  }
   const std::vector<int> d = pair ? std::vector<int>{dir, opp_[dir]} : std::vector<int>{dir};
   hipStream_t s = nullptr, s2 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;

@@ -409,7 +409,8 @@ public:
   int hs_parts(double frac) const;
   /// Link probe (collective): every rank moves its slab facing direction `dir` to its
   /// neighbour there, `iters` times, through `via` ("put": kernel stores into the peer's
-  /// memory, "put_wide": the same with HaloArgs::wide_put_blocks workgroups per box, "sdma":
+  /// memory, "put_wide": the same with HaloArgs::wide_put_blocks workgroups per box,
+  /// "put_cap<N>": with N workgroups per box, "sdma":
   /// copy engines, "rccl": pack + RCCL send/recv + unpack), one transfer at a
   /// time on one stream. Each transfer crosses one xGMI link per rank, so this measures what one
   /// link carries with that transport. "pair_put" / "pair_sdma" / "pair_mixed" move both faces

@@ -279,6 +279,8 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     # other devices ("auto")
     assert p["GBps"]["put_wide"] > 0 and p["pair_GBps"]["put_wide"] > 0
     assert j["wide_puts_offered"] is False
+    assert set(p["put_GBps_by_blocks_per_box"]) == {"16", "64", "256", "1024"}
+    assert all(v > 0 for v in p["put_GBps_by_blocks_per_box"].values()), p
     assert (p["GBps"]["sdma"] is not None) == (mode == "buffers")
     assert (p["GBps"]["memcpy"] is not None) == (mode == "buffers")
     # both z faces at once (2 ranks: one peer): kernel puts always, copy engines and the
