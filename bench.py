@@ -568,6 +568,14 @@ def main() -> int:
     probe = None
     if world > 1 and args.link_probe_iters > 0:
         probe = link_probe(tz, halo, ctrl, args.link_probe_iters, args.link_probe_rccl)
+    # every ordered pair of ranks (not only the halo's neighbours), every rank sending at once:
+    # the fabric the search ran on, e.g. whether all pairs are one xGMI hop
+    matrix = None
+    if world > 1 and args.link_probe_iters > 0:
+        try:
+            matrix = tz._tz.link_matrix(ctrl, 32 << 20, 10)
+        except Exception as e:  # noqa: BLE001
+            matrix = {"why": str(e)}
 
     topo = None
     if rank == 0 and world > 1:
@@ -630,6 +638,7 @@ def main() -> int:
             "graph_capture": tz._tz.graph_capture_info(),
             "timed_graph_node_types": graph_nodes,
             "link_probe": probe,
+            "link_matrix": matrix,
             "elapsed_s": round(time.time() - T_START, 1),
         })
         if deadline is not None:

@@ -807,6 +807,21 @@ PYBIND11_MODULE(_tz, m) {
   });
   m.def("node_identity", []() { return py::bytes(node_identity()); },
         "this machine as exchanged with IPC handles (host name | boot id, fixed size)");
+  m.def("link_matrix", [](Ctrl &c, size_t bytes, int iters) {
+          LinkMatrix lm;
+          {
+            py::gil_scoped_release r;
+            lm = link_matrix(c, bytes, iters);
+          }
+          py::dict d;
+          d["put_GBps"] = lm.put;
+          d["sdma_GBps"] = lm.sdma;
+          d["bytes"] = lm.bytes;
+          d["iters"] = lm.iters;
+          d["why"] = lm.why;
+          return d;
+        }, py::arg("ctrl"), py::arg("bytes") = size_t(32) << 20, py::arg("iters") = 10,
+        "collective all-pairs link probe: GB/s rank r -> q by kernel put and SDMA, all ranks at once");
   m.def("make_rccl_comms", &make_rccl_comms, py::arg("ctrl"), py::arg("device"), py::arg("n"),
         "n communicators over the same ranks (one per logical stream), one broadcast of ids");
 

@@ -156,6 +156,18 @@ private:
 constexpr size_t kNodeIdBytes = 96;
 std::string node_identity();
 
+/// All-pairs link probe (link_matrix.cpp): put[r][q] / sdma[r][q] = GB/s rank r moved into rank
+/// q's IPC-mapped buffer by the halo's kernel put / the SDMA engines, every rank sending at once
+/// (round s: r -> (r + s) % P); -1 where not measured; `why` says why nothing was ("" = ok)
+struct LinkMatrix {
+  std::vector<std::vector<double>> put, sdma;
+  double bytes = 0;
+  int iters = 0;
+  std::string why;
+};
+/// collective over `ctrl`: `bytes` per transfer (a multiple of 32 KiB), `iters` per round
+LinkMatrix link_matrix(Ctrl &ctrl, size_t bytes, int iters);
+
 // ------------------------------------------------------------------ halo exchange
 
 struct HaloArgs {

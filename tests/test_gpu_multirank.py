@@ -280,6 +280,12 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     assert p["GBps"]["put_wide"] > 0 and p["pair_GBps"]["put_wide"] > 0
     assert j["wide_puts_offered"] is False
     assert set(p["put_GBps_by_blocks_per_box"]) == {"16", "64", "256", "1024"}
+    # all pairs, both engines: 2 x 2 with the diagonal unmeasured
+    lm = j["link_matrix"]
+    assert lm["why"] == "", lm
+    for key in ("put_GBps", "sdma_GBps"):
+        m = lm[key]
+        assert len(m) == 2 and m[0][0] == m[1][1] == -1 and m[0][1] > 0 and m[1][0] > 0, lm
     assert all(v > 0 for v in p["put_GBps_by_blocks_per_box"].values()), p
     assert (p["GBps"]["sdma"] is not None) == (mode == "buffers")
     assert (p["GBps"]["memcpy"] is not None) == (mode == "buffers")

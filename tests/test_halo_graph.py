@@ -436,3 +436,12 @@ def test_wide_put_offer_on_a_fake_topology(tz):
     # forced either way
     assert offered("on", me, [me], 0, [0])
     assert not offered("off", me, ["0000:15:00.0"], 0, [1])
+
+
+def test_link_matrix_needs_pairs_and_whole_rows(tz):
+    """the all-pairs link probe: one rank has no pairs (nothing touches a GPU); transfer sizes
+    must be whole 32 KiB rows"""
+    lm = tz._tz.link_matrix(tz._tz.SelfCtrl(), 1 << 20, 2)
+    assert lm["why"] == "one rank: no pairs" and lm["put_GBps"] == [[-1.0]]
+    with pytest.raises(Exception, match="multiple of 32768"):
+        tz._tz.link_matrix(tz._tz.SelfCtrl(), 1000, 2)
