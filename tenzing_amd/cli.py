@@ -333,6 +333,21 @@ def cmd_env(a) -> int:
     return 0
 
 
+def cmd_links(a) -> int:
+    """The fabric between the ranks of this launch (one process per GPU, started like bench.py):
+    the all-pairs link matrix and each peer's device facts, as one JSON line from rank 0."""
+    import tenzing_amd as tz
+    from tenzing_amd.parallel import init
+    from tenzing_amd.parallel.topology import peer_device_facts
+
+    ctrl, dev = init()
+    lm = tz._tz.link_matrix(ctrl, int(a.mib) << 20, a.iters)
+    facts = peer_device_facts(ctrl, dev, range(ctrl.size))
+    if ctrl.rank == 0:
+        print(json.dumps({"ranks": ctrl.size, "link_matrix": lm, "peer_devices": facts}), flush=True)
+    return 0 if ctrl.size == 1 or not lm["why"] else 1
+
+
 def main(argv=None) -> int:
     a = _parser().parse_args(argv)
     return a.fn(a)
@@ -436,6 +451,10 @@ def _parser() -> argparse.ArgumentParser:
     e = sub.add_parser("env")
     e.add_argument("--topology", action="store_true")
     e.set_defaults(fn=cmd_env)
+    k = sub.add_parser("links", help="all-pairs link matrix of the launched ranks (collective)")
+    k.add_argument("--mib", type=int, default=32, help="MiB per transfer")
+    k.add_argument("--iters", type=int, default=10, help="transfers per pair and engine")
+    k.set_defaults(fn=cmd_links)
     u = sub.add_parser("run", help="run a schedule saved by `search --save-best` (no search)")
     u.add_argument("schedule")
     u.add_argument("--iters", type=int, default=1000)

@@ -50,6 +50,13 @@ def test_native_cli_sim(tmp_path):
     assert json.loads(lines[0])["mcts__Opts"]["nIters"] == 20 and len(lines) == 21
 
 
+def test_links_single_process():
+    """`links` in one process: no pairs to measure, no GPU touched, still one JSON line"""
+    j = json.loads(_py("links", "--mib", "1", "--iters", "1").strip().splitlines()[-1])
+    assert j["ranks"] == 1 and j["link_matrix"]["why"] == "one rank: no pairs"
+    assert j["peer_devices"]["summary"] == "no peers"
+
+
 def test_env_report():
     out = _py("env")
     j = json.loads(out)

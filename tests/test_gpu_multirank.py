@@ -342,6 +342,42 @@ def test_native_cli_two_ranks_under_mpiexec(gpu):
     assert j["ranks"] == 2 and j["candidates"] == 6
 
 
+def test_links_cli_three_ranks_loopback(gpu, tmp_path):
+    """`python -m tenzing_amd links` on 3 ranks started the torchrun way (RANK / WORLD_SIZE /
+    MASTER_*): the all-pairs matrix covers all 6 ordered pairs by kernel put and SDMA, and the
+    peer facts say loopback (every peer on this rank's GPU)"""
+    port = _free_port()
+    procs, logs = [], []
+    for r in range(3):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="3", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TZ_CTRL_TIMEOUT_S="60")
+        path = tmp_path / f"links{r}.log"
+        logs.append(str(path))
+        with open(path, "w") as f:
+            procs.append(subprocess.Popen([sys.executable, "-m", "tenzing_amd", "links", "--mib", "8",
+                                           "--iters", "3"], cwd=ROOT, env=env, stdout=f,
+                                          stderr=subprocess.STDOUT, text=True))
+    try:
+        for p in procs:
+            p.wait(timeout=120)
+    except subprocess.TimeoutExpired:
+        pytest.fail("links: no exit within 120 s\n" + _tails(logs))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert all(p.returncode == 0 for p in procs), _tails(logs)
+    with open(logs[0]) as f:
+        j = json.loads([x for x in f.read().splitlines() if x.startswith('{"ranks"')][-1])
+    lm = j["link_matrix"]
+    assert j["ranks"] == 3 and lm["why"] == "" and lm["iters"] == 3, j
+    for key in ("put_GBps", "sdma_GBps"):
+        m = lm[key]
+        assert all((m[r][q] > 0) == (r != q) for r in range(3) for q in range(3)), lm
+    assert all(f["same_device"] for f in j["peer_devices"]["peers"].values()), j["peer_devices"]
+
+
 @pytest.mark.parametrize("world,case", [(2, "spmv"), (4, "spmv"), (8, "spmv"), (2, "fused")])
 def test_spmv_ipc_loopback(gpu, world, case):
     """distributed SpMV (and SpMV + halo in one graph, BASELINE config 5) on several ranks of
