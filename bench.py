@@ -574,6 +574,8 @@ def main() -> int:
     if world > 1 and args.link_probe_iters > 0:
         try:
             matrix = tz._tz.link_matrix(ctrl, 32 << 20, 10)
+            from tenzing_amd.parallel.topology import matrix_summary
+            matrix["summary"] = {k: matrix_summary(matrix[k + "_GBps"]) for k in ("put", "sdma")}
         except Exception as e:  # noqa: BLE001
             matrix = {"why": str(e)}
 

@@ -67,3 +67,19 @@ def summarize(facts: dict) -> str:
     if bad_map:
         s += f"; {bad_map} IPC mapping(s) report an unexpected device"
     return s
+
+
+def matrix_summary(m) -> dict | None:
+    """Off-diagonal summary of a link matrix (``link_matrix``'s ``put_GBps`` / ``sdma_GBps``):
+    how many ordered pairs were measured and how evenly they carry (``spread`` = max / min). On
+    an 8-GPU node with one xGMI hop between every pair the spread stays near 1; a pair routed
+    through another GPU, or a link shared with other traffic, stands out as the minimum."""
+    vals = sorted(v for r, row in enumerate(m or []) for q, v in enumerate(row) if r != q and v > 0)
+    if not vals:
+        return None
+    n = len(vals)
+    med = vals[n // 2] if n % 2 else 0.5 * (vals[n // 2 - 1] + vals[n // 2])
+    worst = min(((r, q) for r, row in enumerate(m) for q, v in enumerate(row) if r != q and v > 0),
+                key=lambda rq: m[rq[0]][rq[1]])
+    return {"pairs": n, "min": vals[0], "median": med, "max": vals[-1],
+            "spread": vals[-1] / vals[0], "slowest_pair": list(worst)}

@@ -310,3 +310,23 @@ def test_graph_capture_info_defaults():
     j = json.loads(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True,
                                   text=True, timeout=120).stdout.strip().splitlines()[-1])
     assert j["mode"] == "child" and j["forced"] and j["rccl_mode"] == "child" and j["pad_streams"] == 0
+
+
+def test_link_matrix_summary_finds_the_slow_pair():
+    """the record's link-matrix summary on a fake 8-GPU node: 56 ordered pairs, one of them
+    (3 -> 5) at half speed, as a pair routed over two hops would be"""
+    import importlib.util
+
+    # the module alone (no package import: this file's tests stay torch-free)
+    spec = importlib.util.spec_from_file_location(
+        "tz_topology", os.path.join(ROOT, "tenzing_amd", "parallel", "topology.py"))
+    topo = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(topo)
+    matrix_summary = topo.matrix_summary
+
+    m = [[-1.0 if r == q else 70.0 for q in range(8)] for r in range(8)]
+    m[3][5] = 35.0
+    s = matrix_summary(m)
+    assert s["pairs"] == 56 and s["min"] == 35.0 and s["max"] == 70.0 and s["median"] == 70.0
+    assert s["slowest_pair"] == [3, 5] and s["spread"] == 2.0
+    assert matrix_summary([[-1.0]]) is None
