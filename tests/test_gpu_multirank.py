@@ -286,6 +286,7 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     for key in ("put_GBps", "sdma_GBps"):
         m = lm[key]
         assert len(m) == 2 and m[0][0] == m[1][1] == -1 and m[0][1] > 0 and m[1][0] > 0, lm
+    assert lm["summary"]["put"]["pairs"] == 2 and lm["summary"]["sdma"]["spread"] >= 1.0, lm
     assert all(v > 0 for v in p["put_GBps_by_blocks_per_box"].values()), p
     assert (p["GBps"]["sdma"] is not None) == (mode == "buffers")
     assert (p["GBps"]["memcpy"] is not None) == (mode == "buffers")
