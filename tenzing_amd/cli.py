@@ -223,6 +223,10 @@ def load_schedule(doc: dict, ctrl, device: int, setup: bool):
     import tenzing_amd as tz
 
     w = _saved_args(doc["args"])
+    # a schedule that uses the wide put needs it offered again, wherever it runs now ("auto"
+    # decides by the devices of this launch)
+    if hasattr(w, "wide_puts") and "he_putw_" in json.dumps(doc["schedule"]):
+        w.wide_puts = "on"
     g, wl = _build_workload(w, ctrl, device, setup)
     seq = tz.OpIndex(g).sequence_from_json(json.dumps(doc["schedule"]))
     bad = tz.verify(seq, tz.resolve_graph(g, seq), w.streams)

@@ -255,3 +255,27 @@ def test_native_cli_two_ranks_port_rendezvous():
     assert best and best[0]["ranks"] == 2 and best[0]["candidates"] == 6
     assert sum(ln.startswith("0|") for ln in outs[0][0].splitlines()) == 1
     assert not any(ln.startswith("0|") for ln in outs[1][0].splitlines())
+
+
+def test_saved_wide_put_schedule_loads_where_auto_would_not_offer_it():
+    """a schedule searched on a node, where "auto" offered the wide put, loads anywhere: the
+    saved options say "auto", the schedule's he_putw_ ops turn the wide put on again"""
+    import tenzing_amd as tz
+    from tenzing_amd.cli import load_schedule
+    from tenzing_amd.models import HaloConfig, build_halo
+    from tenzing_amd.search import greedy_schedule
+
+    class EightRanks:  # graph-only builds read the rank and the size
+        rank, size = 0, 8
+
+    cfg = HaloConfig(n=16, neighbors=26, fuse="all", transport="auto", wide_puts="on",
+                     relay="off", hostsplit="off")
+    _, g = build_halo(cfg, EightRanks(), setup=False)
+    s = greedy_schedule(g, tz.Platform(2), {"he_remote": "he_via_ipcw"})
+    assert any(o.name.startswith("he_putw_") for o in s.ops())
+    doc = {"ranks": 8, "args": {"workload": "halo", "streams": 2, "halo_n": 16, "neighbors": 26,
+                                "fuse": "all", "transport": "auto", "relay": "off",
+                                "hostsplit": "off", "wide_puts": "auto"},
+           "schedule": json.loads(s.json(True))}
+    w, g2, wl, seq = load_schedule(doc, EightRanks(), -1, False)
+    assert w.wide_puts == "on" and any(o.name.startswith("he_putw_") for o in seq.ops())
