@@ -138,6 +138,9 @@ int main(int argc, char **argv) {
       ss << f.rdbuf();
       saved = Json::parse(ss.str());
       load_saved_args(saved.at("args"), a);
+      // a schedule that uses the wide put needs it offered again wherever it runs now
+      if (saved.contains("schedule") && saved.at("schedule").dump().find("he_putw_") != std::string::npos)
+        a.kv["wide-puts"] = "on";
       if (!a.flag("mode") && saved.contains("mode")) a.kv["mode"] = saved.at("mode").as_string();
       TZ_CHECK(!a.flag("sim"), "--run needs a GPU");
     }
