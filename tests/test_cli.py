@@ -279,3 +279,18 @@ def test_saved_wide_put_schedule_loads_where_auto_would_not_offer_it():
            "schedule": json.loads(s.json(True))}
     w, g2, wl, seq = load_schedule(doc, EightRanks(), -1, False)
     assert w.wide_puts == "on" and any(o.name.startswith("he_putw_") for o in seq.ops())
+
+
+def test_bench_names_the_transport_of_a_schedule():
+    """bench.py's transport label per schedule (op-name prefixes): kernel puts of either width,
+    copy engines, the mix, relay and host-split shares"""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.remote_via(["he_direct_self", "he_put_ipc_all"]) == "ipc"
+    assert bench.remote_via(["he_direct_self", "he_putw_w_all", "he_wait_w_remote"]) == "ipc_wide"
+    assert bench.remote_via(["he_put_mx", "he_copyput_mx"]) == "mixed"
+    assert bench.remote_via(["he_rl20_putd", "he_rl20_putc"]) == "relay20"
+    assert bench.remote_via(["he_hs30_putd", "he_hs30_puth"]) == "hostsplit30"
+    assert bench.remote_via(["he_direct_all"]) is None
+    assert bench.schedule_via(["he_direct_a", "he_putw_x"]) == ["direct", "ipc_wide"]
