@@ -224,6 +224,23 @@ def main() -> int:
                          "this + --watchdog-k x n x its expected iteration time, then its device "
                          "waits and RCCL communicators are aborted and the candidate is skipped")
     ap.add_argument("--watchdog-k", type=float, default=50.0)
+    ap.add_argument("--ghost-align", type=int, default=16,
+                    help="x ghost runs aligned to 16 (line) / 8 (sector) elements, 0 = interior "
+                         "rows sector-aligned, -1 = x=0 at the pitched row start (reference)")
+    ap.add_argument("--subrecords", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline: the reference's XYZQ layout and BASELINE configs 2 "
+                         "(SpMV) and 5 (SpMV + halo), each searched briefly, verified and timed "
+                         "(auto: on one rank only)")
+    ap.add_argument("--post-budget-s", type=float, default=150.0,
+                    help="once the headline is final: wall-clock budget of the sub-records and "
+                         "diagnostics after it; past it the complete line is printed and the run "
+                         "exits 0")
+    ap.add_argument("--link-matrix-wait-s", type=float, default=20.0,
+                    help="several ranks: the all-pairs link matrix gives up on a transfer that "
+                         "has not completed within this (the record then says so)")
+    ap.add_argument("--branch-probe", default="on", choices=["on", "off"],
+                    help="probe whether 3 independent branches of a hipGraph run at once with "
+                         "this runtime's stream padding (else try other paddings); recorded")
     args = ap.parse_args()
 
     # one node (every rank local): RCCL's bootstrap over the loopback interface, which always
@@ -266,7 +283,7 @@ def main() -> int:
                      transport=args.transport, rank_grid=grid, stencil=args.stencil,
                      relay=args.relay, hostsplit=args.hostsplit,
                      hostsplit_chunks=args.hostsplit_chunks, wide_puts=args.wide_puts,
-                     wide_put_blocks=args.wide_put_blocks)
+                     wide_put_blocks=args.wide_put_blocks, ghost_align=args.ghost_align)
 
     # the JSON line: every field known up front, so that the deadline can print it partially
     out = {
@@ -317,9 +334,21 @@ def main() -> int:
     halo, graph = build_halo(cfg, ctrl, device)
     out["config"]["rank_grid"] = list(halo.rank_grid())
     mode = tz.ExecMode.Graph if args.search_mode == "graph" else tz.ExecMode.Eager
-    rt = tz.HipRuntime(device=device, n_streams=args.streams, mode=mode,
-                       watchdog_s=args.watchdog_s, watchdog_k=args.watchdog_k,
-                       graph_unroll=args.search_graph_unroll if args.search_mode == "graph" else 1)
+
+    def make_rt(pad=None, n_streams=args.streams):
+        return tz.HipRuntime(device=device, n_streams=n_streams, mode=mode,
+                             watchdog_s=args.watchdog_s, watchdog_k=args.watchdog_k,
+                             graph_unroll=args.search_graph_unroll if args.search_mode == "graph" else 1,
+                             pad_streams=-1 if pad is None else pad)
+
+    branch = None
+    if args.branch_probe == "on" and args.streams >= 3:
+        # the search ranks candidates as hipGraphs: check on this box that HIP's graph executor
+        # runs independent branches at once with this padding (else try others)
+        from tenzing_amd.utils.benchkit import branch_probe, choose_pad
+        rt, branch = choose_pad(make_rt, lambda r: branch_probe(tz, r), [None, 8, 12, 4])
+    else:
+        rt = make_rt()
     bench = tz.EmpiricalBenchmarker(rt, ctrl)
     setup_s = time.time() - t_setup
     transports = halo.transport_report()
@@ -511,30 +540,10 @@ def main() -> int:
     ctrl.barrier()
     report(phase="timing", verified_bad_cells=int(bad), verify_rejected=rejected or None)
 
+    from tenzing_amd.utils.benchkit import timed_replay
+
     def timed(m):
-        rt.set_mode(m)
-        # every rank must agree on the mode (a failed graph build on one rank would otherwise
-        # leave the others blocked in a collective)
-        ok = 1.0
-        try:
-            rt.prepare(best)
-            ok = 1.0 if rt.effective_mode == m else 0.0
-        except Exception as e:  # noqa: BLE001
-            print(f"bench.py: rank {rank}: {m} preparation failed: {e}", file=sys.stderr)
-            ok = 0.0
-        if ctrl.allreduce_max([1.0 - ok])[0] > 0:
-            rt.set_mode(tz.ExecMode.Eager)
-            rt.prepare(best)
-            return None, tz.ExecMode.Eager
-        rt.run(args.warmup)
-        rt.device_sync()
-        ctrl.barrier()
-        t0 = time.perf_counter()
-        rt.run(args.steps)
-        rt.device_sync()
-        ctrl.barrier()
-        dt = time.perf_counter() - t0
-        return ctrl.allreduce_max([dt])[0], rt.effective_mode
+        return timed_replay(tz, rt, ctrl, best, m, args.steps, args.warmup)
 
     t_eager, _ = timed(tz.ExecMode.Eager)
     report(value=t_eager / args.steps * 1e3, ms_per_step=t_eager / args.steps * 1e3,
@@ -560,89 +569,126 @@ def main() -> int:
     t = t_graph if use_graph else t_eager
     ms = t / args.steps * 1e3
     names = [o.name for o in best.ops()]
-    report(value=ms, ms_per_step=ms, value_source="timed replay of the best schedule",
-           phase="link_probe", verified_bad_cells=int(bad))
+    bytes_total = halo.exchange_bytes() * world
+    n_local = sum(1 for i in range(halo.ndirs()) if halo.is_direct(i))
+    out.update({
+        "value": ms,
+        "ms_per_step": ms,
+        "value_source": "timed replay of the best schedule",
+        "partial": False,
+        "phase": "done",
+        "search_wall_s": search_wall,
+        "mcts_candidates": payload["n_sims"],
+        "mcts_skipped": payload["failed"],
+        "mcts_raced": bench.raced,
+        "mcts_tree_nodes": payload["tree"],
+        "search_mode": "hipgraph" if mode == tz.ExecMode.Graph else "eager",
+        "search_best_pct10_ms": best_pct10 * 1e3,
+        "seeded_pct10_ms": payload["seeded"] or None,
+        "rerank": rerank,
+        "eager_ms_per_step": t_eager / args.steps * 1e3,
+        "graph_ms_per_step": (t_graph / args.steps * 1e3) if graph_ok else None,
+        "timed_mode": "hipgraph" if use_graph else "eager",
+        "graph_unroll": args.graph_unroll,
+        "halo_bytes_per_iter_total": bytes_total,
+        "halo_GBps_total": bytes_total / (ms * 1e-3) / 1e9,
+        "schedule_ops": len(best),
+        "schedule_sync_ops": best.count_sync_ops(),
+        "verified_bad_cells": int(bad),
+        "verified_bad_cells_after_timing": int(bad_after),
+        "verify_rejected": rejected or None,
+        "setup_s": setup_s,
+        "transport": halo.transport(),
+        "transports_available": transports,
+        "rccl_nranks": halo.rccl_nranks() or None,
+        "schedule_transport": "+".join(schedule_via(names)),
+        "transport_by_group": {"local": {"dirs": n_local, "via": "direct" if n_local else None},
+                               "remote": {"dirs": halo.ndirs() - n_local,
+                                          "via": remote_via(names)}},
+        "dead_domains": list(res.dead_domains),
+        "pruned_dead": res.pruned_dead,
+        "watchdog": {"floor_s": args.watchdog_s, "k": args.watchdog_k,
+                     "fired": rt.watchdog_fired},
+        "search_wait_timeouts": search_timeouts,
+        "stencil_mode": (("split" if "st_interior" in names else "after")
+                         if args.stencil else None),
+        "ipc_mode": halo.ipc_mode() or None,
+        "relay_offered": halo.uses_relay(),
+        "hostsplit_offered": halo.uses_hostsplit(),
+        "hostsplit_chunks": cfg.hostsplit_chunks if halo.uses_hostsplit() else None,
+        "wide_puts_offered": halo.uses_wide_puts(),
+        "cpus_bound": len(cpus) or None,
+        "rccl_socket_ifname": os.environ.get("NCCL_SOCKET_IFNAME") if world > 1 else None,
+        "peer_devices": peers,
+        "runtime": runtime_libraries(),
+        "graph_capture": tz._tz.graph_capture_info(),
+        "graph_branch_probe": branch,
+        "pad_streams": rt.pad_streams,
+        "timed_graph_node_types": graph_nodes,
+    })
+    # The headline is final. Everything after it is optional and bounded: from here the deadline
+    # prints this (complete) line and exits 0 if the sub-records or diagnostics do not finish
+    # within --post-budget-s, so a stall there (e.g. the first cross-device transfer of a link
+    # probe) cannot turn a finished measurement into a partial one.
+    post = {"budget_s": args.post_budget_s, "done": [], "running": None}
+    out["post_timing"] = post
 
+    def post_phase(name):
+        post["running"] = name
+        report()
+        stall = os.environ.get("TZ_BENCH_STALL", "")  # tests: hang in this phase
+        if stall == name:
+            time.sleep(1e6)
+
+    def post_done(name, **kw):
+        post["done"].append(name)
+        post["running"] = None
+        report(**kw)
+
+    if deadline is not None:
+        report()
+        deadline.tighten(max(5.0, min(args.post_budget_s, deadline.remaining - 10.0)), 0)
+
+    stuck = False
     # per-link bandwidth of each transport (context for the multi-GPU number: an exchange can
     # not beat the bytes its busiest link carries divided by what one link moves)
-    probe = None
     if world > 1 and args.link_probe_iters > 0:
+        post_phase("link_probe")
         probe = link_probe(tz, halo, ctrl, args.link_probe_iters, args.link_probe_rccl)
-    # every ordered pair of ranks (not only the halo's neighbours), every rank sending at once:
-    # the fabric the search ran on, e.g. whether all pairs are one xGMI hop
-    matrix = None
-    if world > 1 and args.link_probe_iters > 0:
+        post_done("link_probe", link_probe=probe)
+        # every ordered pair of ranks (not only the halo's neighbours), every rank sending at
+        # once: the fabric the search ran on, e.g. whether all pairs are one xGMI hop
+        post_phase("link_matrix")
         try:
-            matrix = tz._tz.link_matrix(ctrl, 32 << 20, 10)
+            matrix = tz._tz.link_matrix(ctrl, 32 << 20, 10, args.link_matrix_wait_s)
+            stuck = bool(matrix.get("stuck"))
             from tenzing_amd.parallel.topology import matrix_summary
             matrix["summary"] = {k: matrix_summary(matrix[k + "_GBps"]) for k in ("put", "sdma")}
         except Exception as e:  # noqa: BLE001
             matrix = {"why": str(e)}
-
-    topo = None
+        post_done("link_matrix", link_matrix=matrix)
     if rank == 0 and world > 1:
+        post_phase("topology")
         from tenzing_amd.utils.env import xgmi_topology_summary
-        topo = xgmi_topology_summary()
+        post_done("topology", xgmi_topology=xgmi_topology_summary())
+
+    subrecords = args.subrecords == "on" or (args.subrecords == "auto" and world == 1)
+    if subrecords and not stuck:
+        # the reference driver's layout and the other BASELINE configs, each in this same run
+        del bench
+        rt = None  # the headline's runtime and streams go before the sub-records' are made
+        halo = None
+        for name, fn in (("reference_layout", _reference_layout), ("baseline_configs", _baseline_configs)):
+            post_phase(name)
+            try:
+                val = fn(tz, args, ctrl, device, branch)
+            except Exception as e:  # noqa: BLE001 (a sub-record never costs the headline)
+                val = {"error": f"{type(e).__name__}: {e}"}
+            out[name] = val
+            post_done(name)
+
+    out["elapsed_s"] = round(time.time() - T_START, 1)
     if rank == 0:
-        bytes_total = halo.exchange_bytes() * world
-        n_local = sum(1 for i in range(halo.ndirs()) if halo.is_direct(i))
-        out.update({
-            "value": ms,
-            "ms_per_step": ms,
-            "value_source": "timed replay of the best schedule",
-            "partial": False,
-            "phase": "done",
-            "search_wall_s": search_wall,
-            "mcts_candidates": payload["n_sims"],
-            "mcts_skipped": payload["failed"],
-            "mcts_raced": bench.raced,
-            "mcts_tree_nodes": payload["tree"],
-            "search_mode": "hipgraph" if mode == tz.ExecMode.Graph else "eager",
-            "search_best_pct10_ms": best_pct10 * 1e3,
-            "seeded_pct10_ms": payload["seeded"] or None,
-            "rerank": rerank,
-            "eager_ms_per_step": t_eager / args.steps * 1e3,
-            "graph_ms_per_step": (t_graph / args.steps * 1e3) if graph_ok else None,
-            "timed_mode": "hipgraph" if use_graph else "eager",
-            "graph_unroll": args.graph_unroll,
-            "halo_bytes_per_iter_total": bytes_total,
-            "halo_GBps_total": bytes_total / (ms * 1e-3) / 1e9,
-            "schedule_ops": len(best),
-            "schedule_sync_ops": best.count_sync_ops(),
-            "verified_bad_cells": int(bad),
-            "verified_bad_cells_after_timing": int(bad_after),
-            "verify_rejected": rejected or None,
-            "setup_s": setup_s,
-            "transport": halo.transport(),
-            "transports_available": transports,
-            "rccl_nranks": halo.rccl_nranks() or None,
-            "schedule_transport": "+".join(schedule_via(names)),
-            "transport_by_group": {"local": {"dirs": n_local, "via": "direct" if n_local else None},
-                                   "remote": {"dirs": halo.ndirs() - n_local,
-                                              "via": remote_via(names)}},
-            "dead_domains": list(res.dead_domains),
-            "pruned_dead": res.pruned_dead,
-            "watchdog": {"floor_s": args.watchdog_s, "k": args.watchdog_k,
-                         "fired": rt.watchdog_fired},
-            "search_wait_timeouts": search_timeouts,
-            "stencil_mode": (("split" if "st_interior" in names else "after")
-                             if args.stencil else None),
-            "ipc_mode": halo.ipc_mode() or None,
-            "relay_offered": halo.uses_relay(),
-            "hostsplit_offered": halo.uses_hostsplit(),
-            "hostsplit_chunks": cfg.hostsplit_chunks if halo.uses_hostsplit() else None,
-            "wide_puts_offered": halo.uses_wide_puts(),
-            "cpus_bound": len(cpus) or None,
-            "rccl_socket_ifname": os.environ.get("NCCL_SOCKET_IFNAME") if world > 1 else None,
-            "xgmi_topology": topo,
-            "peer_devices": peers,
-            "runtime": runtime_libraries(),
-            "graph_capture": tz._tz.graph_capture_info(),
-            "timed_graph_node_types": graph_nodes,
-            "link_probe": probe,
-            "link_matrix": matrix,
-            "elapsed_s": round(time.time() - T_START, 1),
-        })
         if deadline is not None:
             deadline.cancel()
         print(json.dumps(out), flush=True)
@@ -664,7 +710,115 @@ def main() -> int:
                 json.dump(doc, f, indent=1)
     elif deadline is not None:
         deadline.cancel()
+    if stuck:
+        # a diagnostic transfer never completed: the device may never drain, so the runtime's
+        # teardown at exit could hang; the result is out, leave without it
+        sys.stdout.flush()
+        os._exit(0 if bad == 0 else 3)
     return 0 if bad == 0 else 3
+
+
+def _sub_runtime(tz, args, device, branch, n_streams):
+    """a runtime for a sub-record: graph-mode search, the headline's watchdog and padding"""
+    pad = branch["pad_streams"] if branch and branch.get("pad_streams") else -1
+    return tz.HipRuntime(device=device, n_streams=n_streams, mode=tz.ExecMode.Graph,
+                         watchdog_s=args.watchdog_s, watchdog_k=args.watchdog_k,
+                         graph_unroll=args.search_graph_unroll, pad_streams=max(pad, n_streams))
+
+
+def _halo_verify(tz, rt, ctrl, halo):
+    """verify(seq): one exchange of seq from a fresh grid of a new value generation, bad cells
+    summed over ranks; verify(None): the grid as it stands (after the timed iterations)"""
+    gen = [0]
+
+    def verify(seq):
+        if seq is not None:
+            gen[0] = gen[0] % 3 + 1
+            halo.init_grid(gen=gen[0])
+            rt.device_sync()
+            rt.prepare(seq)
+            rt.run(1)
+        rt.device_sync()
+        return ctrl.allreduce_sum([float(halo.check_grid())])[0]
+    return verify
+
+
+def _reference_layout(tz, args, ctrl, device, branch):
+    """The headline problem in the reference driver's storage: XYZQ (x fastest, one quantity per
+    3-D block) with x = 0 at the start of the pitched row and the row pitch rounded up to 128 B
+    (tenzing-mcts/examples/halo_run_strategy.hpp:42-49, 63-64: 528 doubles for 518 cells).
+    Searched, verified and timed like the headline."""
+    from tenzing_amd.models import HaloConfig, build_halo
+    from tenzing_amd.utils.benchkit import search_record
+
+    cfg = HaloConfig(n=args.n, neighbors=args.neighbors, fuse=args.fuse, order="xyzq",
+                     transport=args.transport, ghost_align=-1)
+    halo, graph = build_halo(cfg, ctrl, device)
+    rt = _sub_runtime(tz, args, device, branch, args.streams)
+    rec = search_record(tz, ctrl, rt, graph, args.streams, _halo_verify(tz, rt, ctrl, halo),
+                        args.steps, args.warmup, seed=args.seed)
+    rec["config"] = {"model": f"3D {'27' if args.neighbors == 26 else '7'}-point halo-exchange "
+                              f"{args.n}^3 x {cfg.nq}q ghost {cfg.ghost}",
+                     "storage_order": "xyzq", "x_origin": "row start (reference)",
+                     "layout": halo.layout(), "streams": args.streams,
+                     "halo_bytes_per_iter": halo.exchange_bytes()}
+    del rt
+    return rec
+
+
+def _baseline_configs(tz, args, ctrl, device, branch):
+    """BASELINE.json configs 2 and 5 on this GPU, each searched briefly (MCTS, hipGraph
+    candidates), verified and timed like the headline:
+      spmv_c2:  CSR SpMV, m = 150,000, nnz = 10 m, band m / ranks, f32, 2 streams
+                (tenzing-dfs/examples/spmv.cu:86-117, tenzing-mcts/examples/spmv_run_strategy.cuh:44-68;
+                BASELINE.md: 0.0094 ms, DFS over hipGraph candidates)
+      fused_c5: that SpMV + the 26-neighbour 512^3 halo in one graph, 4 streams
+                (0.0544 ms)"""
+    from tenzing_amd.models import HaloConfig, SpmvConfig, build_fused, build_spmv
+    from tenzing_amd.utils.benchkit import search_record
+
+    recs = {}
+    steps, warmup = max(args.steps, 20), max(args.warmup, 5)
+
+    def spmv_verify(rt, s):
+        def verify(seq):
+            if seq is not None:
+                s.reset_y()
+                rt.device_sync()
+                rt.prepare(seq)
+                rt.run(1)
+            rt.device_sync()
+            err = ctrl.allreduce_max([s.check()])[0]
+            return 0 if err < 1e-4 else 1
+        return verify
+
+    sc = SpmvConfig(m=150_000)
+    s, g = build_spmv(sc, ctrl, device)
+    rt = _sub_runtime(tz, args, device, branch, 2)
+    rec = search_record(tz, ctrl, rt, g, 2, spmv_verify(rt, s), steps, warmup, mcts_iters=60,
+                        search_unroll=8, seed=args.seed)
+    rec["config"] = {"m": sc.m, "nnz": s.local_nnz() + s.remote_nnz(), "streams": 2,
+                     "dtype": "fp32", "baseline_ms": 0.0094}
+    recs["spmv_c2"] = rec
+    del rt, s, g
+
+    hc = HaloConfig(n=args.n, neighbors=26, order="qxyz")
+    h, s, g = build_fused(hc, SpmvConfig(m=150_000), ctrl, device)
+    rt = _sub_runtime(tz, args, device, branch, 4)
+    hv, sv = _halo_verify(tz, rt, ctrl, h), spmv_verify(rt, s)
+
+    def both(seq):
+        if seq is not None:
+            s.reset_y()
+        b = hv(seq)
+        return b + sv(None)
+    rec = search_record(tz, ctrl, rt, g, 4, both, steps, warmup, mcts_iters=60, search_unroll=8,
+                        seed=args.seed)
+    rec["config"] = {"halo": f"{args.n}^3 x 3q ghost 3, 26 neighbours, qxyz", "spmv_m": 150_000,
+                     "streams": 4, "baseline_ms": 0.0544}
+    recs["fused_c5"] = rec
+    del rt
+    return recs
 
 
 _STATE = {}  # what a failure report needs: the JSON line so far, the rank, the deadline

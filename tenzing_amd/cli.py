@@ -228,6 +228,12 @@ def load_schedule(doc: dict, ctrl, device: int, setup: bool):
     if hasattr(w, "wide_puts") and "he_putw_" in json.dumps(doc["schedule"]):
         w.wide_puts = "on"
     g, wl = _build_workload(w, ctrl, device, setup)
+    if setup and "halo" in wl and "he_putw_" in json.dumps(doc["schedule"]) \
+            and not wl["halo"].uses_wide_puts():
+        raise SystemExit("the saved schedule uses wide IPC puts (he_putw_*), which this launch "
+                         "does not offer: " + wl["halo"].transport_report()["wide_put"] +
+                         " (e.g. TZ_PUT_MAX_BLOCKS equal to --wide-put-blocks, or its preflight "
+                         "failed on this node)")
     seq = tz.OpIndex(g).sequence_from_json(json.dumps(doc["schedule"]))
     bad = tz.verify(seq, tz.resolve_graph(g, seq), w.streams)
     if bad:

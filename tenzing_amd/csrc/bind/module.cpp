@@ -560,7 +560,11 @@ PYBIND11_MODULE(_tz, m) {
            "rank 0 listens on the first free port of port..port+nports-1, the others connect "
            "(handshake-checked): no store, no torch")
       .def("rendezvous_file", &TcpCtrl::rendezvous_file, py::arg("path"), py::arg("host") = "127.0.0.1",
-           py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>());
+           py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>())
+      .def("ensure_timeout", &TcpCtrl::ensure_timeout, py::arg("seconds"),
+           "raise the peer sockets' receive timeout to at least this (never lowered)")
+      .def_property_readonly("timeout", &TcpCtrl::timeout,
+                             "the peer sockets' receive timeout in seconds (0 = none)");
   py::class_<MpiCtrl, Ctrl, std::shared_ptr<MpiCtrl>>(m, "MpiCtrl")
       .def(py::init<const std::string &>(), py::arg("lib") = "", py::call_guard<py::gil_scoped_release>())
       .def_static("launched", &MpiCtrl::launched)
@@ -635,6 +639,8 @@ PYBIND11_MODULE(_tz, m) {
       .def(py::init<double, int>(), py::arg("seconds"), py::arg("exit_code") = 5)
       .def("set_report", &RunDeadline::set_report, py::arg("line"))
       .def("cancel", &RunDeadline::cancel)
+      .def("tighten", &RunDeadline::tighten, py::arg("seconds"), py::arg("exit_code"),
+           "expire at the latest `seconds` from now, exiting with `exit_code`")
       .def_property_readonly("remaining", &RunDeadline::remaining)
       .def_property_readonly("armed", &RunDeadline::armed);
   m.def("exit_with_report", [](int code, const std::string &why) { exit_with_report(code, why); },
@@ -677,8 +683,9 @@ PYBIND11_MODULE(_tz, m) {
   py::enum_<ExecMode>(m, "ExecMode").value("Eager", ExecMode::Eager).value("Graph", ExecMode::Graph);
   py::class_<HipRuntime, ExecutorRunner>(m, "HipRuntime", py::multiple_inheritance())
       .def(py::init([](int device, int n, std::vector<int> prio, bool cu, ExecMode mode, double wd,
-                       int unroll, double wk) {
+                       int unroll, double wk, int pad) {
         HipRuntimeOpts o;
+        o.pad_streams = pad;
         o.device = device;
         o.n_streams = n;
         o.priorities = prio;
@@ -690,7 +697,9 @@ PYBIND11_MODULE(_tz, m) {
         return new HipRuntime(o);
       }), py::arg("device") = -1, py::arg("n_streams") = 2, py::arg("priorities") = std::vector<int>{},
          py::arg("cu_partition") = false, py::arg("mode") = ExecMode::Eager, py::arg("watchdog_s") = 0.0,
-         py::arg("graph_unroll") = 1, py::arg("watchdog_k") = 50.0)
+         py::arg("graph_unroll") = 1, py::arg("watchdog_k") = 50.0, py::arg("pad_streams") = -1)
+      .def_property_readonly("pad_streams", &HipRuntime::pad_streams,
+                             "streams this runtime owns at least (schedule streams + never-used spares)")
       .def("set_graph_unroll", &HipRuntime::set_graph_unroll)
       .def_property_readonly("graph_unroll", &HipRuntime::graph_unroll)
       .def("set_mode", &HipRuntime::set_mode)
@@ -807,11 +816,11 @@ PYBIND11_MODULE(_tz, m) {
   });
   m.def("node_identity", []() { return py::bytes(node_identity()); },
         "this machine as exchanged with IPC handles (host name | boot id, fixed size)");
-  m.def("link_matrix", [](Ctrl &c, size_t bytes, int iters) {
+  m.def("link_matrix", [](Ctrl &c, size_t bytes, int iters, double wait_limit_s) {
           LinkMatrix lm;
           {
             py::gil_scoped_release r;
-            lm = link_matrix(c, bytes, iters);
+            lm = link_matrix(c, bytes, iters, wait_limit_s);
           }
           py::dict d;
           d["put_GBps"] = lm.put;
@@ -819,8 +828,10 @@ PYBIND11_MODULE(_tz, m) {
           d["bytes"] = lm.bytes;
           d["iters"] = lm.iters;
           d["why"] = lm.why;
+          d["stuck"] = lm.stuck;
           return d;
         }, py::arg("ctrl"), py::arg("bytes") = size_t(32) << 20, py::arg("iters") = 10,
+        py::arg("wait_limit_s") = 30.0,
         "collective all-pairs link probe: GB/s rank r -> q by kernel put and SDMA, all ranks at once");
   m.def("make_rccl_comms", &make_rccl_comms, py::arg("ctrl"), py::arg("device"), py::arg("n"),
         "n communicators over the same ranks (one per logical stream), one broadcast of ids");
@@ -954,6 +965,15 @@ PYBIND11_MODULE(_tz, m) {
                   },
                   py::arg("box"), py::arg("parts"))
       .def("grid_elems", &HaloExchange::grid_elems)
+      .def("layout", [](const HaloExchange &h) {
+             const kern::HaloGeom g = h.geom();
+             py::dict d;
+             d["order"] = g.order == 0 ? "xyzq" : "qxyz";
+             d["x_offset_cells"] = g.xoff;   // padding before x = 0 (the first ghost cell)
+             d["row_pitch_elems"] = g.sy;    // doubles per pitched row
+             d["grid_bytes"] = double(h.grid_elems()) * 8.0;
+             return d;
+           }, "storage layout: order, x padding before the first ghost cell, row pitch")
       .def("exchange_bytes", &HaloExchange::exchange_bytes)
       .def("setup", [](HaloExchange &h, Ctrl *c) { h.setup(c); }, py::arg("ctrl") = nullptr,
            py::call_guard<py::gil_scoped_release>())
@@ -1015,6 +1035,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("m", &SpmvArgs::m)
       .def_readwrite("bw", &SpmvArgs::bw)
       .def_readwrite("nnz", &SpmvArgs::nnz)
+      .def_readonly("nnz_actual", &SpmvArgs::nnz_actual)
       .def_readwrite("seed", &SpmvArgs::seed)
       .def_readwrite("rank", &SpmvArgs::rank)
       .def_readwrite("size", &SpmvArgs::size)
@@ -1038,6 +1059,9 @@ PYBIND11_MODULE(_tz, m) {
       .def("transport", &DistSpmv::transport)
       .def("uses_ipc", &DistSpmv::uses_ipc)
       .def("uses_rccl", &DistSpmv::uses_rccl)
+      .def("rccl_graph_ok", &DistSpmv::rccl_graph_ok, "RCCL exchanges may be captured into hipGraphs")
+      .def("rccl_capture_note", &DistSpmv::rccl_capture_note,
+           "how the RCCL exchange is compiled into hipGraphs (its preflight's verdict), or why not")
       .def("ipc_errors", &DistSpmv::ipc_errors, py::call_guard<py::gil_scoped_release>())
       .def("setup", [](DistSpmv &s, Ctrl *c) { s.setup(c); }, py::arg("ctrl") = nullptr,
            py::call_guard<py::gil_scoped_release>())

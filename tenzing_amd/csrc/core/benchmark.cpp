@@ -58,6 +58,10 @@ EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, d
                                                                 bool deviceTimer) {
   Measurement m{std::max<int64_t>(1, nHint), 0};
   while (true) {
+    // the control plane waits in the max-reduction below for the slowest rank's run: never give
+    // up on it before that run's own watchdog would
+    const double budget = runner_.run_budget(m.n);
+    if (budget > 0) ctrl_.ensure_timeout(budget + 60.0);
     ctrl_.barrier();
     const double t0 = wtime();
     // a run-time failure (launch error, watchdog, op check) may hit one rank only: it travels

@@ -79,6 +79,13 @@ public:
   /// batch sizes that run without a remainder (a compiled graph of K unrolled iterations: K),
   /// so a measurement times the same launches as a long run does
   virtual int64_t batch_multiple() const { return 1; }
+  /// the longest a run of `n` iterations may take before the runner gives up on it (its
+  /// watchdog budget plus grace), 0 if unbounded: every rank's collectives around a run must
+  /// wait at least that long for the slowest rank
+  virtual double run_budget(int64_t n) const {
+    (void)n;
+    return 0.0;
+  }
 
 private:
   std::vector<Sequence> many_;

@@ -9,6 +9,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/select.h>
 #include <sys/socket.h>
 #include <sys/time.h>
@@ -97,12 +98,24 @@ void nodelay(int fd) {
   int one = 1;
   ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
 }
-/// receive timeout of a joined peer socket: env TZ_CTRL_TIMEOUT_S (default 900 s: above any
-/// search step, below "forever"; 0 = none)
-void peer_timeout(int fd) {
+/// the other end of `fd` has closed it (readable at end of file, or reset): a peer that left
+bool peer_closed(int fd) {
+  pollfd p{fd, POLLIN, 0};
+  if (::poll(&p, 1, 0) <= 0) return false; // nothing pending: still open
+  if (p.revents & (POLLHUP | POLLERR | POLLNVAL)) return true;
+  char c;
+  const ssize_t r = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+  return r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK);
+}
+/// default receive timeout of a joined peer socket: env TZ_CTRL_TIMEOUT_S (default 900 s: above
+/// any search step, below "forever"; 0 = none). Runs whose watchdog budget is longer raise it
+/// (TcpCtrl::ensure_timeout, called by the benchmarker before every run)
+double default_peer_timeout() {
   double t = 900.0;
   if (const char *v = std::getenv("TZ_CTRL_TIMEOUT_S")) t = std::atof(v);
-  if (t <= 0) return;
+  return t > 0 ? t : 0.0;
+}
+void set_rcv_timeout(int fd, double t) {
   timeval tv{};
   tv.tv_sec = long(t);
   tv.tv_usec = long((t - double(tv.tv_sec)) * 1e6);
@@ -164,8 +177,10 @@ int TcpCtrl::connect_acked(const std::string &host, int port, std::string &why) 
   }
   nodelay(fd);
   // rank 0 acknowledges a peer at once; a listener that does not (another program that holds
-  // the port) is left, not waited on forever
-  timeval ack{5, 0};
+  // the port) is left, not waited on forever. Rank 0 may first have to drop a backlog of stray
+  // connections (up to 1 s each), so the wait is generous; a peer that gives up anyway comes
+  // back and rank 0 replaces its closed connection
+  timeval ack{15, 0};
   ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &ack, sizeof(ack));
   uint32_t a = 0;
   try {
@@ -186,7 +201,19 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
   if (rank_ == 0) {
     TZ_CHECK(listenFd_ >= 0, "rank 0 must listen() before connect()");
     const double t0 = wtime();
-    for (int joined = 1; joined < size_;) {
+    for (int joined = 1;;) {
+      if (joined == size_) {
+        // every rank joined; a peer that has since closed its connection (it gave up waiting
+        // for the acknowledgement and will come back) is waited for again
+        for (int i = 1; i < size_; ++i)
+          if (peers_[i] >= 0 && peer_closed(peers_[i])) {
+            ::close(peers_[i]);
+            peers_[i] = -1;
+            --joined;
+            TZ_LOG(Info, "ctrl rendezvous: rank " << i << " left before the release; waiting for it again");
+          }
+        if (joined == size_) break;
+      }
       // bounded: a rank that never comes must not leave rank 0 blocked in accept() forever
       timeval tv{};
       const double left = timeoutS - (wtime() - t0);
@@ -222,20 +249,35 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
                          << (h.magic != kHello ? "without the handshake" : "of another job"));
         continue;
       }
-      if (h.size != size_ || h.rank <= 0 || h.rank >= size_ || peers_[h.rank] >= 0) {
+      if (h.size != size_ || h.rank <= 0 || h.rank >= size_) {
         ::close(fd);
         TZ_THROW("ctrl rendezvous: peer says rank " << h.rank << " of " << h.size << " (this job: "
-                                                    << size_ << " ranks; a duplicate rank or a "
-                                                                "rank of another job?)");
+                                                    << size_ << " ranks; a rank of another job?)");
+      }
+      if (peers_[h.rank] >= 0) {
+        // the same rank again: a peer that gave up waiting for its acknowledgement (this loop
+        // was held up by stray connections) closed the old connection and came back -- take
+        // the new one; while the old one is still open, the new one is a stray and is dropped
+        if (!peer_closed(peers_[h.rank])) {
+          ::close(fd);
+          TZ_LOG(Warn, "ctrl rendezvous: dropped a second connection of rank " << h.rank
+                                                                                 << " (its first is open)");
+          continue;
+        }
+        ::close(peers_[h.rank]);
+        peers_[h.rank] = -1;
+        --joined;
+        TZ_LOG(Info, "ctrl rendezvous: rank " << h.rank << " reconnected");
       }
       peers_[h.rank] = fd;
       send_all(fd, &kAck, sizeof(kAck));
       ++joined;
     }
     // release everyone
+    timeoutS_ = default_peer_timeout();
     for (int i = 1; i < size_; ++i) {
       send_all(peers_[i], &kWelcome, sizeof(kWelcome));
-      peer_timeout(peers_[i]);
+      if (timeoutS_ > 0) set_rcv_timeout(peers_[i], timeoutS_);
     }
     return;
   }
@@ -264,8 +306,16 @@ void TcpCtrl::connect(const std::string &host, int port, double timeoutS) {
   TZ_CHECK(w == kWelcome, "ctrl rendezvous: " << host << ":" << port << " is not this job's rank 0");
   timeval none{0, 0};
   ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
-  peer_timeout(fd);
+  timeoutS_ = default_peer_timeout();
+  if (timeoutS_ > 0) set_rcv_timeout(fd, timeoutS_);
   peers_[0] = fd;
+}
+
+void TcpCtrl::ensure_timeout(double seconds) {
+  if (timeoutS_ <= 0 || seconds <= timeoutS_) return; // no timeout at all, or long enough
+  timeoutS_ = seconds;
+  for (int fd : peers_)
+    if (fd >= 0) set_rcv_timeout(fd, timeoutS_);
 }
 
 void TcpCtrl::rendezvous(const std::string &host, int port, double timeoutS, int nports) {

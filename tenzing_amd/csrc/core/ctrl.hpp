@@ -37,6 +37,9 @@ public:
     return v;
   }
   int64_t bcast_int(int64_t v, int root);
+  /// a collective may wait at least `seconds` for the other ranks before it declares one of them
+  /// gone (control planes with a receive timeout raise it; never lowered)
+  virtual void ensure_timeout(double seconds) { (void)seconds; }
 };
 
 class SelfCtrl : public Ctrl {
@@ -80,9 +83,14 @@ public:
   std::vector<std::string> allgather(const std::string &mine) override;
   std::vector<std::string> alltoallv(const std::vector<std::string> &out) override;
   using Ctrl::allreduce_max;
+  /// raise every peer socket's receive timeout to `seconds` if it is lower (0 = none: stays)
+  void ensure_timeout(double seconds) override;
+  /// the peer sockets' receive timeout in seconds (0 = none)
+  double timeout() const { return timeoutS_; }
 
 private:
   void allreduce(double *v, size_t n, bool isMax);
+  double timeoutS_ = 0; // receive timeout of the joined peer sockets (0 = none)
   /// one connection attempt to host:port with the handshake; the fd, or -1 (`why` updated)
   int connect_acked(const std::string &host, int port, std::string &why) const;
   int connectPorts_ = 1; // candidate ports connect() cycles through (rendezvous)

@@ -31,9 +31,17 @@ public:
   /// waiter: the wait ended. True if the watchdog had claimed it: the state is then kDraining
   /// until drained(); false otherwise (the state is back to 0)
   bool finish() {
-    if (d_.exchange(0) != kClaimed) return false;
-    d_.store(kDraining);
-    return true;
+    // claimed -> draining in one step: the watchdog never sees 0 in between, so a drain that
+    // then hangs still counts as a pending abort (its grace exit stays armed)
+    double c = kClaimed;
+    if (d_.compare_exchange_strong(c, kDraining)) return true;
+    // not claimed: back to 0, unless the watchdog claims it right now (then drain after all)
+    double d = d_.load();
+    while (d != kClaimed) {
+      if (d_.compare_exchange_weak(d, 0)) return false;
+    }
+    c = kClaimed;
+    return d_.compare_exchange_strong(c, kDraining);
   }
   /// waiter: the aborted wait has drained
   void drained() { d_.store(0); }

@@ -1148,7 +1148,9 @@ struct RunDeadline::Impl {
   std::condition_variable cv;
   std::string report;
   bool done = false;
-  double end = 0;
+  double end = 0;                                // wtime() of expiry (remaining())
+  std::chrono::steady_clock::time_point until;   // the same instant, for the waiting thread
+  uint64_t gen = 0;                              // bumped by tighten(): re-wait
   int code = 5;
   std::thread th;
 };
@@ -1208,27 +1210,51 @@ void exit_with_report(int code, const std::string &why) {
 
 RunDeadline::RunDeadline(double seconds, int exitCode) : p_(std::make_unique<Impl>()) {
   p_->end = wtime() + seconds;
+  p_->until = std::chrono::steady_clock::now() +
+              std::chrono::microseconds(int64_t(std::max(0.0, seconds) * 1e6));
   p_->code = exitCode;
   Impl *p = p_.get();
   g_armedDeadline = p;
   p_->th = std::thread([p, seconds] {
     std::unique_lock<std::mutex> lk(p->mu);
-    const auto until = std::chrono::steady_clock::now() +
-                       std::chrono::microseconds(int64_t(std::max(0.0, seconds) * 1e6));
-    if (p->cv.wait_until(lk, until, [p] { return p->done; })) return;
+    for (;;) {
+      const uint64_t gen = p->gen;
+      const auto until = p->until;
+      if (p->cv.wait_until(lk, until, [p, gen] { return p->done || p->gen != gen; })) {
+        if (p->done) return;
+        continue; // tightened: wait for the new instant
+      }
+      break;
+    }
     // expired: report and leave; no locks other threads might hold, no stdio buffers
     p->done = true; // (a fatal exit racing this one must not print the line again)
     std::string line = p->report;
     if (!line.empty() && line.back() != '\n') line += '\n';
     write_all(1, line);
-    char msg[160];
+    char msg[200];
     const int n = std::snprintf(msg, sizeof(msg),
-                                "[tz] run deadline of %.0f s reached: %s; exiting with status %d\n",
-                                seconds, p->report.empty() ? "nothing to report" : "partial result printed",
+                                "[tz] run deadline reached (%.0f s from the start): %s; exiting with status %d\n",
+                                seconds, p->report.empty() ? "nothing to report" : "report printed",
                                 p->code);
     if (n > 0) (void)!::write(2, msg, size_t(std::min<int>(n, int(sizeof(msg) - 1))));
     std::_Exit(p->code);
   });
+}
+
+void RunDeadline::tighten(double seconds, int exitCode) {
+  {
+    std::lock_guard<std::mutex> lk(p_->mu);
+    if (p_->done) return;
+    const double end = wtime() + std::max(0.0, seconds);
+    if (end < p_->end) {
+      p_->end = end;
+      p_->until = std::chrono::steady_clock::now() +
+                  std::chrono::microseconds(int64_t(std::max(0.0, seconds) * 1e6));
+    }
+    p_->code = exitCode;
+    ++p_->gen;
+  }
+  p_->cv.notify_all();
 }
 
 RunDeadline::~RunDeadline() {

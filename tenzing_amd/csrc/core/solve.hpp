@@ -174,6 +174,10 @@ public:
   void set_report(const std::string &line);
   /// disarm (the program finished in time)
   void cancel();
+  /// expire at the latest `seconds` from now (never later than already set) and exit with
+  /// `exit_code` then: e.g. once a result is final, a bounded budget for the optional work after
+  /// it, whose expiry prints the (complete) report and exits 0
+  void tighten(double seconds, int exit_code);
   double remaining() const;
   bool armed() const;
 

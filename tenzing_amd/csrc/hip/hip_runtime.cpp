@@ -82,7 +82,8 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
   // independent 200 us kernels: 447 us per launch; with 4-8 streams owned: 241-244 us; a host
   // node then a kernel beside two kernels: 319 -> 241 us). 6: the RCCL probe between two
   // loopback ranks also stays at its unpadded time (profiles/r4_pad/)
-  for (int i = opts.n_streams; i < pad_streams(); ++i) {
+  pad_ = opts.pad_streams >= 0 ? opts.pad_streams : tz::pad_streams();
+  for (int i = opts.n_streams; i < pad_; ++i) {
     hipStream_t s = nullptr;
     TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     spare_.push_back(s);
@@ -439,7 +440,12 @@ CaptureMode rccl_capture_mode() {
   return capture_mode_forced() ? capture_mode() : CaptureMode(g_rcclCapture.load());
 }
 
-void set_rccl_capture_mode(CaptureMode m) { g_rcclCapture = int(m); }
+std::atomic<bool> g_rcclCaptureSettled{false};
+void set_rccl_capture_mode(CaptureMode m) {
+  g_rcclCapture = int(m);
+  g_rcclCaptureSettled = true;
+}
+bool rccl_capture_settled() { return g_rcclCaptureSettled.load(); }
 
 const char *capture_mode_name(CaptureMode m) {
   return m == CaptureMode::Child ? "child" : "schedule";

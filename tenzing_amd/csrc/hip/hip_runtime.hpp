@@ -51,6 +51,7 @@ struct HipRuntimeOpts {
   double watchdog_k = 50;      // ... plus this many times the expected time of the run
   int graph_unroll = 1;        // iterations per hipGraph launch in Graph mode
   bool spin_sync = true;       // host syncs busy-poll (env TZ_SPIN_SYNC=0/1 overrides)
+  int pad_streams = -1;        // streams owned at least (spares never used); -1: pad_streams()
 };
 
 // ExecutorRunner first: the Python bindings expose HipRuntime through that base
@@ -63,6 +64,12 @@ public:
 
   // Executor
   int num_streams() const override { return int(streams_.size()); }
+  int pad_streams() const { return std::max(pad_, int(streams_.size())); }
+  /// the watchdog's budget for n iterations plus its grace before the process exit (0: no
+  /// watchdog, unbounded)
+  double run_budget(int64_t n) const override {
+    return watchdogS_ > 0 ? watchdog_budget(n) + std::max(10.0, watchdogS_) : 0.0;
+  }
   void launch(const GpuOp &op, int stream) override;
   void event_record(int event, int stream) override;
   void stream_wait_event(int stream, int event) override;
@@ -147,6 +154,7 @@ private:
   ExecMode mode_;
   std::vector<void *> streams_;
   std::vector<void *> spare_;    // never used: hardware-queue padding (TZ_PAD_STREAMS)
+  int pad_ = 0;                  // streams owned at least (schedule streams + spares)
   std::vector<void *> events_;   // schedule events
   std::vector<void *> internal_; // StreamWait helpers
   void *timerEv_[2] = {nullptr, nullptr};
@@ -209,6 +217,9 @@ bool capture_mode_forced();
 /// on every rank (Schedule first, Child as the fallback); Schedule until a preflight sets it
 CaptureMode rccl_capture_mode();
 void set_rccl_capture_mode(CaptureMode m);
+/// a workload's RCCL preflight has verified (and set) the capture mode: a later workload's
+/// preflight must verify that same mode, not pick another (the mode is per process)
+bool rccl_capture_settled();
 const char *capture_mode_name(CaptureMode m);
 
 /// Builds one hipGraph from ops enqueued on a fixed set of streams (hipStream_t as void*;

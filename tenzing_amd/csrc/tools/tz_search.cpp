@@ -327,6 +327,12 @@ int main(int argc, char **argv) {
     if (a.flag("run")) {
       // a saved schedule: rebuilt by op name, proven race-free on the graph it executes,
       // checked once from a fresh state, then timed (max over ranks)
+      if (halo && !halo->uses_wide_puts() &&
+          saved.at("schedule").dump().find("he_putw_") != std::string::npos)
+        TZ_THROW("the saved schedule uses wide IPC puts (he_putw_*), which this launch does not "
+                 "offer: " << halo->transport_report().at("wide_put")
+                           << " (e.g. TZ_PUT_MAX_BLOCKS equal to --wide-put-blocks, or its preflight "
+                              "failed on this node)");
       const Sequence seq = OpIndex(*g).sequence_from_json(saved.at("schedule"));
       const auto bad = verify(seq, *resolve_graph(*g, seq), streams);
       TZ_CHECK(bad.empty(), "schedule is not race-free on this graph: " << bad.front().desc());

@@ -785,6 +785,37 @@ TEST(deadline_claim_run_ends_at_its_deadline) {
   std::printf("  deadline race: %d of 20000 ends claimed by the watchdog, all reported\n", claimed);
 }
 
+TEST(deadline_claim_abort_pending_through_finish) {
+  // between a claimed wait's end and its drain, a watchdog sweep must always see the
+  // abort pending (never the 0 of a finished wait), or a drain that hangs loses its grace exit
+  std::atomic<int> seen0{0}, sweeps{0};
+  for (int it = 0; it < 2000; ++it) {
+    DeadlineClaim c;
+    c.arm(1.0);
+    CHECK(c.try_claim(2.0));
+    std::atomic<bool> stop{false}, running{false};
+    std::thread wd([&] {
+      while (!stop.load()) {
+        ++sweeps;
+        if (!c.abort_pending()) ++seen0;
+        running = true;
+      }
+    });
+    while (!running.load()) {
+    }
+    const bool aborted = c.finish();
+    CHECK(aborted);
+    CHECK(c.abort_pending() && c.value() == DeadlineClaim::kDraining);
+    stop = true;
+    wd.join();
+    c.drained();
+    CHECK(!c.abort_pending());
+  }
+  CHECK(seen0 == 0);
+  CHECK(sweeps > 0);
+  std::printf("  %d watchdog sweeps during claimed finishes, none saw the wait as ended\n", sweeps.load());
+}
+
 TEST(runs_test_behaviour) {
   std::vector<double> alt, trend;
   for (int i = 0; i < 40; ++i) {

@@ -62,8 +62,8 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.order == "xyzq" || a_.order == "qxyz", "order must be xyzq or qxyz");
   TZ_CHECK(a_.rank >= 0 && a_.rank < a_.size, "bad rank");
   TZ_CHECK(a_.pitch_pad >= 0 && a_.pitch_pad % 16 == 0, "pitch_pad must be a multiple of 16");
-  TZ_CHECK(a_.ghost_align == 0 || a_.ghost_align == 8 || a_.ghost_align == 16,
-           "ghost_align must be 0, 8 or 16");
+  TZ_CHECK(a_.ghost_align == -1 || a_.ghost_align == 0 || a_.ghost_align == 8 || a_.ghost_align == 16,
+           "ghost_align must be -1 (x = 0 at the row start), 0, 8 or 16");
   TZ_CHECK(a_.wide_puts == "auto" || a_.wide_puts == "on" || a_.wide_puts == "off",
            "wide_puts must be auto, on or off");
   TZ_CHECK(a_.wide_put_blocks >= 1 && a_.wide_put_blocks <= 4096,
@@ -107,8 +107,10 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   if (a_.order == "xyzq") {
     // interior rows (and so the inner ends of the x ghost runs) start on a 64-B sector, or on
     // a ghost_align boundary
+    // (ghost_align -1: no padding, x = 0 at the start of the pitched row, as the reference
+    // driver lays it out: halo_run_strategy.hpp:49, 63-64)
     const int64_t al = a_.ghost_align > 8 ? a_.ghost_align : 8;
-    xoff_ = (al - a_.ghost % al) % al;
+    xoff_ = a_.ghost_align < 0 ? 0 : (al - a_.ghost % al) % al;
     pitch_ = round_up(xoff_ + X, 16) + a_.pitch_pad; // rows are whole 128-B lines
     sy_ = pitch_;
     sz_ = pitch_ * Y;
@@ -136,7 +138,7 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
         bestCost = cost;
       }
     }
-    xoff_ = best < 0 ? 0 : best;
+    xoff_ = best < 0 || a_.ghost_align < 0 ? 0 : best;
     if (a_.ghost_align > 0) {
       // instead: the smallest padding that puts the inner ends of both x ghost runs on
       // ghost_align boundaries (ghost-low ends, ghost-high starts there when q*n is a multiple

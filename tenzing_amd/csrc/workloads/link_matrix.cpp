@@ -10,7 +10,10 @@
 // Reference: none (the reference relies on CUDA-aware MPI and never measures its fabric).
 #include "workloads.hpp"
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "core/util.hpp"
 #include "hip/hip_runtime.hpp"
@@ -19,7 +22,28 @@
 
 namespace tz {
 
-LinkMatrix link_matrix(Ctrl &ctrl, size_t bytes, int iters) {
+namespace {
+// wait for `e` for at most `limit_s` (polling; hipEventSynchronize has no bound): false if it did
+// not complete in time. Env TZ_LINK_MATRIX_STALL=1 (tests) treats every wait as one that never
+// completes.
+bool wait_event_bounded(hipEvent_t e, double limit_s) {
+  static const bool stall = [] {
+    const char *v = std::getenv("TZ_LINK_MATRIX_STALL");
+    return v && std::atoi(v) != 0;
+  }();
+  const double end = wtime() + limit_s;
+  for (;;) {
+    const hipError_t q = stall ? hipErrorNotReady : hipEventQuery(e);
+    if (q == hipSuccess) return true;
+    if (q != hipErrorNotReady) TZ_HIP(q);
+    if (wtime() > end) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+} // namespace
+
+LinkMatrix link_matrix(Ctrl &ctrl, size_t bytes, int iters, double wait_limit_s) {
+  TZ_CHECK(wait_limit_s > 0, "wait_limit_s must be positive");
   const int P = ctrl.size(), R = ctrl.rank();
   TZ_CHECK(iters >= 1, "iters must be positive");
   constexpr size_t kRow = 4096; // elements per row of the put's box (32 KiB)
@@ -99,7 +123,11 @@ LinkMatrix link_matrix(Ctrl &ctrl, size_t bytes, int iters) {
     err = std::string("probe: ") + e.what();
   }
   // the same barriers on every rank whatever fails locally: a rank that failed only skips its
-  // transfers
+  // transfers. Every device wait is bounded: a transfer that has not completed in time (a link
+  // that stalls) fails this rank's probe, and its buffers, mappings and stream are then left as
+  // they are (releasing them would wait for the stuck transfer) -- the caller gets a result
+  // that says why instead of a hang
+  bool stuck = false;
   for (int kind = 0; kind < 2; ++kind) {
     for (int shift = 1; shift < P; ++shift) {
       const int q = (R + shift) % P;
@@ -128,7 +156,12 @@ LinkMatrix link_matrix(Ctrl &ctrl, size_t bytes, int iters) {
           }
         }
         TZ_HIP(hipEventRecord(e1, s));
-        TZ_HIP(hipEventSynchronize(e1));
+        if (!wait_event_bounded(e1, wait_limit_s)) {
+          stuck = true;
+          err = "probe: " + std::string(kind == 0 ? "kernel put" : "SDMA copy") + " to rank " +
+                std::to_string(q) + " did not complete within " + std::to_string(wait_limit_s) + " s";
+          continue;
+        }
         float ms = 0;
         TZ_HIP(hipEventElapsedTime(&ms, e0, e1));
         row[size_t(kind * P + q)] = ms > 0 ? double(bytes) * iters / (double(ms) * 1e-3) / 1e9 : -1.0;
@@ -138,12 +171,23 @@ LinkMatrix link_matrix(Ctrl &ctrl, size_t bytes, int iters) {
     }
   }
   // every rank has stopped writing into its peers before any buffer is unmapped or freed
-  if (s) (void)hipStreamSynchronize(s);
-  ctrl.barrier();
-  if (e0) (void)hipEventDestroy(e0);
-  if (e1) (void)hipEventDestroy(e1);
-  if (s) (void)hipStreamDestroy(s);
-  close_all();
+  if (s && !stuck) (void)hipStreamSynchronize(s);
+  double anyStuck = stuck ? 1.0 : 0.0;
+  ctrl.allreduce_max(&anyStuck, 1);
+  out.stuck = anyStuck != 0.0;
+  if (out.stuck) {
+    // a transfer somewhere has not completed: it may still write into any rank's buffer, so
+    // nothing is unmapped, freed or destroyed (a process exit reclaims it)
+    src.leak();
+    dst.leak();
+    done.leak();
+    flag.leak();
+  } else {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (s) (void)hipStreamDestroy(s);
+    close_all();
+  }
   std::string enc(reinterpret_cast<const char *>(row.data()), row.size() * sizeof(double));
   const std::vector<std::string> rows = ctrl.allgather(err.empty() ? enc : std::string());
   for (int r = 0; r < P; ++r) {

@@ -26,6 +26,7 @@ Json SpmvArgs::json() const {
   j["m"] = m;
   j["bw"] = bw;
   j["nnz"] = nnz;
+  j["nnz_actual"] = nnz_actual;
   j["seed"] = int64_t(seed);
   j["rank"] = rank;
   j["size"] = size;
@@ -39,18 +40,32 @@ Json SpmvArgs::json() const {
 }
 
 CsrHost random_band_matrix(int64_t n, int64_t bw, int64_t nnz, uint64_t seed) {
-  TZ_CHECK(n > 0 && bw > 0 && nnz >= 0, "bad band matrix parameters");
+  // The reference's generator (include/tenzing/spmv/csr_mat.hpp:334-370): a row uniformly at
+  // random, a column uniformly in [r - bw, r + bw] (draws outside the matrix are dropped, not
+  // clamped, so the first and last columns are not over-weighted), duplicates removed, and
+  // refilled until exactly nnz distinct entries exist. Values here are uniform in [-1, 1)
+  // (the reference stores 1.0) so that a wrong column shows in the numerical check.
+  TZ_CHECK(n > 0 && bw >= 0 && nnz >= 0, "bad band matrix parameters");
+  int64_t capacity = 0; // entries inside the band
+  for (int64_t r = 0; r < n && capacity < nnz; ++r)
+    capacity += std::min(n - 1, r + bw) - std::max<int64_t>(0, r - bw) + 1;
+  TZ_CHECK(nnz <= capacity, "nnz " << nnz << " exceeds the " << capacity << " entries of an " << n
+                                    << " x " << n << " band of half-width " << bw);
   std::mt19937_64 rng(seed);
+  const uint64_t width = uint64_t(2 * bw + 1);
   std::vector<int64_t> keys;
   keys.reserve(size_t(nnz));
-  for (int64_t k = 0; k < nnz; ++k) {
-    const int64_t r = int64_t(rng() % uint64_t(n));
-    const int64_t lo = std::max<int64_t>(0, r - bw + 1), hi = std::min<int64_t>(n - 1, r + bw - 1);
-    const int64_t c = lo + int64_t(rng() % uint64_t(hi - lo + 1));
-    keys.push_back(r * n + c);
+  while (int64_t(keys.size()) < nnz) {
+    const int64_t need = nnz - int64_t(keys.size());
+    for (int64_t k = 0; k < need; ++k) {
+      const int64_t r = int64_t(rng() % uint64_t(n));
+      const int64_t c = r - bw + int64_t(rng() % width);
+      if (c < 0 || c >= n) continue;
+      keys.push_back(r * n + c);
+    }
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
   }
-  std::sort(keys.begin(), keys.end());
-  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
   CsrHost A;
   A.rows = A.cols = n;
   A.rowPtr.assign(size_t(n + 1), 0);
@@ -221,6 +236,7 @@ public:
   std::string kind() const override { return "SpmvExchange"; }
   double cost_us() const override { return s_->num_peers() ? 10.0 + 4.0 * double(s_->send_elems()) / 5.0e4 : 0.5; }
   std::string order_domain() const override { return s_->uses_rccl() ? "rccl" : ""; }
+  bool capturable() const override { return !s_->uses_rccl() || s_->rccl_graph_ok(); }
   void launch(void *st, Executor &) const override { s_->exchange(st); }
 
 private:
@@ -305,6 +321,7 @@ DistSpmv::DistSpmv(SpmvArgs a) : a_(std::move(a)) {
     if (a_.nnz <= 0) a_.nnz = 10 * a_.m;
     A = random_band_matrix(a_.m, a_.bw, a_.nnz, a_.seed);
   }
+  a_.nnz_actual = A.nnz();
   const int64_t n = a_.m;
   TZ_CHECK(n >= a_.size, "fewer matrix rows (" << n << ") than ranks (" << a_.size << ")");
   std::tie(r0_, r1_) = row_partition(n, a_.rank, a_.size);
@@ -455,6 +472,7 @@ void DistSpmv::setup(Ctrl *ctrl) {
         failed = why.empty() ? 0.0 : 1.0;
         ctrl->allreduce_max(&failed, 1);
         if (failed != 0.0) why = "preflight: " + (why.empty() ? std::string("failed on another rank") : why);
+        else rccl_graph_preflight(*ctrl);
       }
       if (failed != 0.0) {
         if (comm_ && !comm_->aborted()) comm_->abort();
@@ -658,6 +676,116 @@ std::string DistSpmv::rccl_preflight_local() {
   }
   (void)hipStreamDestroy(s);
   return why;
+}
+
+void DistSpmv::rccl_graph_preflight(Ctrl &ctrl) {
+  // The exchange as the runtime compiles candidates (GraphBuilder: scatter, then the grouped
+  // RCCL exchange), launched twice with a different local x each time, so that a graph that
+  // delivers the previous launch's data fails the check. The capture mode is per process: once
+  // a workload's preflight has settled it (the halo's, in a fused graph), only that mode is
+  // verified here; otherwise whole-schedule capture first, then child capture. No mode works:
+  // RCCL exchanges stay out of hipGraphs (their candidates run eagerly). Every rank in step.
+  double limit = 20.0;
+  if (const char *v = std::getenv("TZ_RCCL_PREFLIGHT_S")) limit = std::atof(v);
+  const std::string failEnv = std::getenv("TZ_FAIL_TRANSPORTS") ? std::getenv("TZ_FAIL_TRANSPORTS") : "";
+  const bool simGraph = ("," + failEnv + ",").find(",rccl_graph_schedule,") != std::string::npos;
+  std::vector<CaptureMode> modes;
+  if (capture_mode_forced() || rccl_capture_settled()) modes = {rccl_capture_mode()};
+  else modes = {CaptureMode::Schedule, CaptureMode::Child};
+  hipStream_t s = nullptr;
+  TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  auto wait = [&]() {
+    const double t0 = wtime();
+    while (true) {
+      const hipError_t r = hipStreamQuery(s);
+      if (r == hipSuccess) return true;
+      if (r != hipErrorNotReady) TZ_HIP(r);
+      if (wtime() - t0 > limit) return false;
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+  };
+  auto upload_x = [&](int gen) {
+    std::vector<float> x(xLocal_.size());
+    for (size_t i = 0; i < x.size(); ++i) x[i] = xLocal_[i] + float(gen);
+    if (!x.empty()) dX_.upload(x.data(), x.size() * 4);
+  };
+  std::vector<std::string> tried;
+  bool chosen = false, hung = false;
+  for (CaptureMode mode : modes) {
+    std::string wrong;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    try {
+      {
+        GraphBuilder gb({s}, mode);
+        gb.add(0, {}, [&](void *cs) {
+          scatter(cs);
+          exchange(cs);
+        });
+        graph = static_cast<hipGraph_t>(gb.finish());
+      }
+      TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      for (int gen = 1; gen <= 2 && wrong.empty() && !hung; ++gen) {
+        upload_x(gen);
+        TZ_HIP(hipMemsetAsync(dXr_.get(), 0, dXr_.bytes(), s));
+        TZ_HIP(hipGraphLaunch(exec, s));
+        if (!wait()) {
+          hung = true;
+          break;
+        }
+        std::vector<float> xr(remoteCols_.size());
+        if (!xr.empty()) dXr_.download(xr.data(), xr.size() * 4);
+        size_t bad = 0;
+        for (size_t i = 0; i < xr.size(); ++i) bad += xr[i] != x_value(remoteCols_[i]) + float(gen);
+        if (simGraph && mode == CaptureMode::Schedule) bad += 1; // tests: force the fallback
+        if (bad) wrong = "launch " + std::to_string(gen) + ": " + std::to_string(bad) + " wrong remote x entries";
+      }
+    } catch (const std::exception &e) {
+      wrong = e.what(); // a capture or instantiation error: RCCL stays for eager runs
+      if (!wait()) hung = true;
+    }
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    double flags[2] = {hung ? 1.0 : 0.0, wrong.empty() ? 0.0 : 1.0};
+    ctrl.allreduce_max(flags, 2);
+    if (flags[0] != 0.0) {
+      hung = true;
+      break;
+    }
+    if (flags[1] == 0.0) {
+      if (!rccl_capture_settled() && !capture_mode_forced()) set_rccl_capture_mode(mode);
+      rcclCaptureNote_ = std::string(capture_mode_name(mode)) + " capture";
+      if (!tried.empty()) rcclCaptureNote_ += " (" + tried.front() + ")";
+      chosen = true;
+      break;
+    }
+    tried.push_back(std::string(capture_mode_name(mode)) + " capture: " +
+                    (wrong.empty() ? "wrong data on another rank" : wrong));
+  }
+  if (hung) {
+    // a captured exchange that never completes: release spinning kernels and abort the
+    // communicator as the eager preflight does; RCCL is then gone for this workload
+    kern::set_abort(true);
+    auto c = comm_;
+    std::thread([c] { c->abort(); }).detach();
+    if (!wait())
+      exit_with_report(6, "RCCL graph preflight (spmv): the device did not drain after the "
+                          "communicator abort");
+    kern::set_abort(false);
+    TZ_CHECK(a_.transport == "auto" && useIpc_ && ipcReady_,
+             "SpMV RCCL transport: a captured exchange hung and there is no IPC fallback");
+    comm_.reset();
+    useRccl_ = false;
+    rcclCaptureNote_ = "hipGraph exchange hung (communicator aborted)";
+    TZ_LOG(Warn, "SpMV RCCL transport dropped: " << rcclCaptureNote_);
+  } else if (!chosen) {
+    rcclGraphOk_ = false;
+    rcclCaptureNote_ = "eager only";
+    for (const std::string &t : tried) rcclCaptureNote_ += "; " + t;
+    TZ_LOG(Warn, "SpMV RCCL exchanges run eagerly only: " << rcclCaptureNote_);
+  }
+  upload_x(0);
+  (void)hipStreamDestroy(s);
 }
 
 void DistSpmv::ipc_preflight(Ctrl *ctrl) {

@@ -62,6 +62,12 @@ public:
   size_t bytes() const { return bytes_; }
   void upload(const void *src, size_t bytes);
   void download(void *dst, size_t bytes) const;
+  /// give the memory up without freeing it (a device that may still be writing into it, e.g.
+  /// after a transfer that did not complete in time: freeing would wait for it)
+  void leak() {
+    p_ = nullptr;
+    bytes_ = 0;
+  }
 
 private:
   void *p_ = nullptr;
@@ -164,9 +170,11 @@ struct LinkMatrix {
   double bytes = 0;
   int iters = 0;
   std::string why;
+  bool stuck = false; // a transfer did not complete within the wait limit (on some rank)
 };
-/// collective over `ctrl`: `bytes` per transfer (a multiple of 32 KiB), `iters` per round
-LinkMatrix link_matrix(Ctrl &ctrl, size_t bytes, int iters);
+/// collective over `ctrl`: `bytes` per transfer (a multiple of 32 KiB), `iters` per round; every
+/// device wait gives up after `wait_limit_s` (the result then says why, and `stuck` is set)
+LinkMatrix link_matrix(Ctrl &ctrl, size_t bytes, int iters, double wait_limit_s = 30.0);
 
 // ------------------------------------------------------------------ halo exchange
 
@@ -598,6 +606,7 @@ struct SpmvArgs {
   int64_t m = 150000;
   int64_t bw = 0;  // 0 = m / size (reference spmv_run_strategy.cuh:67)
   int64_t nnz = 0; // 0 = 10 * m
+  int64_t nnz_actual = 0; // set by DistSpmv: the entries of the matrix it built or read
   uint64_t seed = 1;
   int rank = 0, size = 1;
   int device = -1;
@@ -660,6 +669,11 @@ public:
   /// return the senders' credits (their next put may overwrite my remote-x buffer)
   void release(void *stream) const;
   bool uses_rccl() const { return useRccl_; }
+  /// RCCL exchanges may be captured into hipGraphs (their preflight verified the process's
+  /// capture mode); otherwise candidates with them run eagerly
+  bool rccl_graph_ok() const { return rcclGraphOk_; }
+  /// how the RCCL exchange is compiled into hipGraphs, or why it is not ("" = no RCCL)
+  std::string rccl_capture_note() const { return rcclCaptureNote_; }
   bool uses_ipc() const { return useIpc_ && ipcReady_; }
   /// "rccl", "ipc", "rccl+ipc" (search chooses) or "none" (one rank)
   std::string transport() const;
@@ -686,7 +700,13 @@ private:
   void ipc_preflight(Ctrl *ctrl);
   /// one verified RCCL exchange under a bounded wait; "" on success, else why not
   std::string rccl_preflight_local();
+  /// the RCCL exchange compiled into hipGraphs as the runtime compiles candidates, in the
+  /// process's capture mode (or, if no workload has settled it yet, whole-schedule capture
+  /// first, then child capture): collective; sets rcclGraphOk_ / rcclCaptureNote_
+  void rccl_graph_preflight(Ctrl &ctrl);
   bool useRccl_ = false, useIpc_ = false, ipcReady_ = false;
+  bool rcclGraphOk_ = true;
+  std::string rcclCaptureNote_;
   void *flags_ = nullptr; // [arrivals from rank q | credits from rank q] (uncached, exported)
   DeviceBuffer expected_, sent_, done_, err_;
   std::vector<void *> peerXr_, peerFlags_, opened_;

@@ -1,0 +1,202 @@
+"""Pieces of ``bench.py`` that are worth testing on their own.
+
+* ``branch_probe`` / ``choose_pad``: does HIP's graph executor run three independent branches of
+  a captured schedule at once on this box, with this runtime's stream padding? (round 4 found a
+  3-branch graph serializing unless the process owns spare streams: 449 vs 232 us,
+  ``profiles/r4_capture/README.md:42-57``). The bench probes the runtime it is about to search
+  with, retries other paddings if the branches serialize, and records what it found.
+* ``timed_replay``: the timing contract of every number the bench reports (W untimed warm-up
+  iterations, then K timed ones bracketed by barrier + device sync, max over ranks).
+* ``search_record``: a short search of another workload, its winner verified and timed the same
+  way as the headline -- the bench's sub-records (the reference's XYZQ halo layout, BASELINE
+  configs 2 and 5) so that the driver's own run observes them.
+
+Reference: the drivers time with MPI_Wtime around MPI_Barrier'd batches, max over ranks
+(src/benchmarker.cpp:83-119); tenzing-mcts/examples/spmv_run_strategy.cuh:44-68 and
+halo_run_strategy.hpp:42-49 give the sub-record configurations.
+"""
+from __future__ import annotations
+
+import time
+
+BRANCH_PREFIX = "branch_probe"
+
+
+def _busy_graph(tz, branches: int, us: float):
+    g = tz.Graph()
+    for i in range(branches):
+        op = tz.BusyKernelOp(f"{BRANCH_PREFIX}{i}", us)
+        g.start_then(op)
+        g.then_finish(op)
+    return g
+
+
+def branch_probe(tz, rt, branches: int = 3, us: float = 50.0, iters: int = 10):
+    """Microseconds per hipGraph launch of ``branches`` independent ``us``-long single-workgroup
+    kernels, one per stream of ``rt`` (compiled the way the runtime compiles every schedule), and
+    of one such kernel alone. ``ratio`` = all / one: about 1 when the branches run at once,
+    about ``branches`` when they serialize. The runtime's mode and unroll are restored; None if
+    the runtime cannot build the graph."""
+    from ..search import greedy_schedule
+
+    if rt.num_streams() < branches:
+        return None
+    mode, unroll = rt.mode, rt.graph_unroll
+    rt.set_mode(tz.ExecMode.Graph)
+    rt.set_graph_unroll(1)
+
+    def per_launch(k):
+        g = _busy_graph(tz, k, us)
+        seq = greedy_schedule(g, tz.Platform(rt.num_streams(), symmetric_streams=False),
+                              stream_for=lambda n: int(n[len(BRANCH_PREFIX):]))
+        rt.prepare(seq)
+        if rt.effective_mode != tz.ExecMode.Graph:
+            return None
+        rt.run(3)
+        rt.device_sync()
+        t0 = time.perf_counter()
+        rt.run(iters)
+        rt.device_sync()
+        return (time.perf_counter() - t0) / iters * 1e6
+
+    try:
+        one = per_launch(1)
+        many = per_launch(branches)
+    finally:
+        rt.set_mode(mode)
+        rt.set_graph_unroll(unroll)
+    if not one or not many:
+        return None
+    return {"branches": branches, "kernel_us": us, "one_us": round(one, 1),
+            "all_us": round(many, 1), "ratio": round(many / one, 3)}
+
+
+def choose_pad(make_rt, probe, pads, threshold: float = 1.5):
+    """Runtime whose graph branches run concurrently: ``make_rt(pad)`` builds a runtime with that
+    stream padding (None: the default), ``probe(rt)`` returns its branch probe (a dict with
+    ``ratio``, or None). The first padding whose ratio is at most ``threshold`` is kept;
+    otherwise the one with the lowest ratio (built again if it is not the last one probed).
+
+    Returns (runtime, record); the record lists every probe in order and the padding chosen."""
+    tried = []
+    best = None  # (ratio, pad)
+    rt = None
+    for pad in pads:
+        rt = None  # the previous runtime (and its streams) goes before the next is made
+        rt = make_rt(pad)
+        r = probe(rt)
+        used = rt.pad_streams if hasattr(rt, "pad_streams") else pad
+        tried.append({"pad_streams": used, "probe": r})
+        ratio = r["ratio"] if r else None
+        if ratio is not None and ratio <= threshold:
+            return rt, {"pad_streams": used, "serialized": False, "tried": tried,
+                        "threshold": threshold}
+        if ratio is not None and (best is None or ratio < best[0]):
+            best = (ratio, pad, used)
+    if best is None:  # the probe could not run at all: keep the last runtime, say so
+        return rt, {"pad_streams": tried[-1]["pad_streams"] if tried else None,
+                    "serialized": None, "tried": tried, "threshold": threshold}
+    if best[1] != pads[-1]:
+        rt = None
+        rt = make_rt(best[1])
+    return rt, {"pad_streams": best[2], "serialized": True, "tried": tried,
+                "threshold": threshold}
+
+
+def timed_replay(tz, rt, ctrl, seq, mode, steps: int, warmup: int):
+    """(seconds for ``steps`` iterations of ``seq`` in ``mode``, max over ranks, or None if the
+    mode could not be prepared on some rank; the mode that ran). ``warmup`` untimed iterations
+    first; the timed ones are bracketed by device sync + barrier on both sides."""
+    rt.set_mode(mode)
+    ok = 1.0
+    try:
+        rt.prepare(seq)
+        ok = 1.0 if rt.effective_mode == mode else 0.0
+    except Exception:  # noqa: BLE001 (agreed below: every rank falls back together)
+        ok = 0.0
+    if ctrl.allreduce_max([1.0 - ok])[0] > 0:
+        rt.set_mode(tz.ExecMode.Eager)
+        rt.prepare(seq)
+        return None, tz.ExecMode.Eager
+    rt.run(warmup)
+    rt.device_sync()
+    ctrl.barrier()
+    t0 = time.perf_counter()
+    rt.run(steps)
+    rt.device_sync()
+    ctrl.barrier()
+    dt = time.perf_counter() - t0
+    return ctrl.allreduce_max([dt])[0], rt.effective_mode
+
+
+def search_record(tz, ctrl, rt, graph, streams: int, verify, steps: int, warmup: int,
+                  mcts_iters: int = 40, bench_iters: int = 6, target_secs: float = 0.002,
+                  search_unroll: int = 10, graph_unroll: int = 20, seed: int = 0,
+                  time_budget_s: float = 30.0, strategy: str = "FastMin", rerank: int = 4):
+    """Search ``graph`` briefly (MCTS, hipGraph candidates, racing and settling as the headline),
+    re-rank the ``rerank`` best distinct candidates interleaved, verify the winner with
+    ``verify(seq) -> bad count`` (the next finalist if it fails), then time it eagerly and as a
+    hipGraph exactly as the headline is timed. Returns the sub-record dict."""
+    t_start = time.time()
+    plat = tz.Platform(streams)
+    rt.set_mode(tz.ExecMode.Graph)
+    rt.set_graph_unroll(search_unroll)
+    bench = tz.EmpiricalBenchmarker(rt, ctrl)
+    o = tz.MctsOpts()
+    o.n_iters = mcts_iters
+    o.time_budget_s = time_budget_s
+    o.strategy = strategy
+    o.seed = seed
+    o.bench = tz.BenchOpts(n_iters=bench_iters, max_retries=3, target_secs=target_secs,
+                           race_ratio=1.25, settle_ratio=0.03)
+    res = tz.mcts_explore(graph, plat, bench, ctrl, o)
+    rec = {"mcts_candidates": len(res.sims), "mcts_skipped": res.failed,
+           "search_wall_s": round(res.wall_s, 3)}
+    if not res.sims:
+        rec["error"] = "the search measured no candidate"
+        return rec
+    order = sorted(range(len(res.sims)), key=lambda i: res.sims[i].res.pct10)
+    top, keys = [], set()
+    for i in order:
+        k = res.sims[i].seq.canonical_key()
+        if k not in keys:
+            keys.add(k)
+            top.append(i)
+        if len(top) >= max(1, rerank):
+            break
+    cands = [res.sims[i].seq for i in top]
+    rec["search_best_pct10_ms"] = res.sims[top[0]].res.pct10 * 1e3
+    ranked = list(range(len(cands)))
+    if len(cands) > 1:
+        rr = bench.benchmark_many(cands, tz.BenchOpts(n_iters=bench_iters, max_retries=1,
+                                                      target_secs=target_secs), seed)
+        ranked = sorted(range(len(rr)), key=lambda i: rr[i].pct10)
+        rec["rerank_pct10_ms"] = [round(r.pct10 * 1e3, 5) for r in rr]
+    rt.set_mode(tz.ExecMode.Eager)
+    best, bad, rejected = None, None, 0
+    for k in ranked:
+        b = verify(cands[k])
+        if b == 0:
+            best, bad = cands[k], 0
+            break
+        rejected += 1
+    if best is None:
+        best, bad = cands[ranked[0]], int(verify(cands[ranked[0]]))
+    rec["verified_bad"] = int(bad)
+    rec["verify_rejected"] = rejected
+    t_e, _ = timed_replay(tz, rt, ctrl, best, tz.ExecMode.Eager, steps, warmup)
+    rt.set_graph_unroll(graph_unroll)
+    t_g, eff = timed_replay(tz, rt, ctrl, best, tz.ExecMode.Graph, steps, warmup)
+    graph_ok = t_g is not None and eff == tz.ExecMode.Graph
+    use_graph = graph_ok and t_g < t_e
+    t = t_g if use_graph else t_e
+    rec.update({"ms_per_step": t / steps * 1e3, "timed_mode": "hipgraph" if use_graph else "eager",
+                "eager_ms_per_step": t_e / steps * 1e3,
+                "graph_ms_per_step": (t_g / steps * 1e3) if graph_ok else None,
+                "schedule_ops": len(best), "steps": steps, "warmup": warmup,
+                "wall_s": round(time.time() - t_start, 2)})
+    # correctness after the timed iterations too (the sub-record's workload decides what a
+    # bad result is)
+    after = verify(None)
+    rec["verified_bad_after_timing"] = int(after)
+    return rec

@@ -132,6 +132,8 @@ def main():
             halo, sp, g = build_fused(HaloConfig(n=32, neighbors=26, order="qxyz", fuse="choice"),
                                       SpmvConfig(m=m), ctrl, dev)
         out["transport"] = sp.transport()
+        out["rccl_capture"] = sp.rccl_capture_note()
+        out["rccl_graph_ok"] = sp.rccl_graph_ok()
         rt = tz.HipRuntime(device=dev, n_streams=3, watchdog_s=60.0)
         res = []
         for mode in (tz.ExecMode.Eager, tz.ExecMode.Graph):

@@ -1,0 +1,106 @@
+"""bench.py's testable pieces on the CPU: the stream-padding choice driven by the graph-branch
+probe (fake runtimes and a fake timer), and the run deadline's post-headline budget (a stall
+after the result is final still prints the complete line and exits 0)."""
+import json
+import os
+import subprocess
+import sys
+
+from tenzing_amd.utils.benchkit import choose_pad
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class FakeRt:
+    made = []
+
+    def __init__(self, pad):
+        self.pad_streams = 6 if pad is None else pad
+        FakeRt.made.append(self.pad_streams)
+
+
+def fake_probe(ratios):
+    """the probe's ratio per padding (None: the probe could not run)"""
+    def probe(rt):
+        r = ratios[rt.pad_streams]
+        return None if r is None else {"ratio": r, "one_us": 55.0, "all_us": 55.0 * r}
+    return probe
+
+
+def test_choose_pad_keeps_the_default_when_branches_run_at_once():
+    FakeRt.made = []
+    rt, rec = choose_pad(FakeRt, fake_probe({6: 1.1, 8: 1.0}), [None, 8, 12])
+    assert rt.pad_streams == 6 and rec["pad_streams"] == 6 and rec["serialized"] is False
+    assert FakeRt.made == [6] and len(rec["tried"]) == 1
+
+
+def test_choose_pad_retries_until_a_padding_runs_branches_at_once():
+    FakeRt.made = []
+    rt, rec = choose_pad(FakeRt, fake_probe({6: 2.05, 8: 1.9, 12: 1.15, 4: 1.0}), [None, 8, 12, 4])
+    assert rt.pad_streams == 12 and rec["serialized"] is False
+    assert [t["pad_streams"] for t in rec["tried"]] == [6, 8, 12]
+    assert FakeRt.made == [6, 8, 12]
+
+
+def test_choose_pad_falls_back_to_the_least_serialized():
+    FakeRt.made = []
+    rt, rec = choose_pad(FakeRt, fake_probe({6: 2.0, 8: 1.7, 12: 1.9, 4: 2.1}), [None, 8, 12, 4])
+    # none within the threshold: the lowest ratio (8) is rebuilt and recorded as serialized
+    assert rt.pad_streams == 8 and rec["pad_streams"] == 8 and rec["serialized"] is True
+    assert FakeRt.made == [6, 8, 12, 4, 8]
+
+
+def test_choose_pad_when_the_probe_cannot_run():
+    FakeRt.made = []
+    rt, rec = choose_pad(FakeRt, fake_probe({6: None, 8: None}), [None, 8])
+    assert rec["serialized"] is None and rt.pad_streams == 8 and FakeRt.made == [6, 8]
+
+
+def _run(code, timeout=60):
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                          timeout=timeout, cwd=ROOT)
+
+
+def test_deadline_tighten_prints_the_final_line_and_exits_0():
+    """the bench's post-headline phase: the report is the complete (non-partial) line, the
+    deadline is tightened to the post budget with exit status 0, and a diagnostic then stalls:
+    the line is printed once and the process exits 0 within the budget"""
+    code = ("import json, time, tenzing_amd as tz\n"
+            "d = tz.RunDeadline(300.0, 5)\n"
+            "d.set_report(json.dumps({'metric': 'm', 'value': 0.1, 'partial': True}))\n"
+            "d.set_report(json.dumps({'metric': 'm', 'value': 0.2, 'partial': False,\n"
+            "                         'post_timing': {'running': 'link_matrix'}}))\n"
+            "d.tighten(1.0, 0)\n"
+            "time.sleep(60)\n")
+    r = _run(code)
+    assert r.returncode == 0, (r.stdout, r.stderr)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    j = json.loads(lines[0])
+    assert j["partial"] is False and j["value"] == 0.2
+    assert j["post_timing"]["running"] == "link_matrix"
+    assert "run deadline" in r.stderr and "status 0" in r.stderr
+
+
+def test_deadline_tighten_never_extends():
+    """tighten() can only bring the deadline closer: a later instant keeps the earlier one (its
+    exit status is still replaced)"""
+    code = ("import time, tenzing_amd as tz\n"
+            "d = tz.RunDeadline(1.0, 5)\n"
+            "d.set_report('{\"v\": 1}')\n"
+            "d.tighten(100.0, 7)\n"
+            "assert d.remaining < 1.5\n"
+            "time.sleep(30)\n")
+    r = _run(code)
+    assert r.returncode == 7, (r.stdout, r.stderr)
+
+
+def test_deadline_cancel_after_tighten():
+    code = ("import time, tenzing_amd as tz\n"
+            "d = tz.RunDeadline(30.0, 5)\n"
+            "d.tighten(0.5, 0)\n"
+            "d.cancel()\n"
+            "time.sleep(1.2)\n"
+            "print('alive')\n")
+    r = _run(code)
+    assert r.returncode == 0 and "alive" in r.stdout, (r.stdout, r.stderr)

@@ -330,3 +330,83 @@ def test_link_matrix_summary_finds_the_slow_pair():
     assert s["pairs"] == 56 and s["min"] == 35.0 and s["max"] == 70.0 and s["median"] == 70.0
     assert s["slowest_pair"] == [3, 5] and s["spread"] == 2.0
     assert matrix_summary([[-1.0]]) is None
+
+
+def test_timeout_is_raised_for_long_runs():
+    """a run whose watchdog budget is longer than the control plane's receive timeout raises it
+    (the benchmarker calls ensure_timeout before every run): a peer that is slow but within that
+    budget is waited for, not declared gone"""
+    port = _free_port()
+    body = r"""
+import os, sys, time
+sys.path.insert(0, os.environ["TZ_ROOT"])
+from tenzing_amd.parallel import init_ctrl
+c = init_ctrl(timeout_s=60)
+c.ensure_timeout(1.0)   # never lowers
+assert abs(c.timeout - 1.5) < 1e-9, c.timeout
+c.ensure_timeout(8.0)
+if c.rank == 1:
+    time.sleep(3)
+t0 = time.time()
+c.barrier()
+print("OK %.1f %.1f" % (time.time() - t0, c.timeout))
+"""
+    env = dict(os.environ, TZ_NO_TORCH="1", TZ_ROOT=ROOT, MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), WORLD_SIZE="2", TZ_CTRL_TIMEOUT_S="1.5")
+    ps = [subprocess.Popen([sys.executable, "-c", body], env=dict(env, RANK=str(r)),
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in (0, 1)]
+    try:
+        outs = [p.communicate(timeout=60) for p in ps]
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in ps), outs
+    line = [x for x in outs[0][0].splitlines() if x.startswith("OK")][-1]
+    assert float(line.split()[1]) > 2.0 and float(line.split()[2]) == 8.0, line
+
+
+def test_rank_that_reconnects_replaces_its_closed_connection():
+    """a peer that gave up waiting for its acknowledgement and came back with the same rank is
+    taken again (its first connection, now closed, is replaced) instead of failing the whole
+    rendezvous as a duplicate rank (3 ranks: rank 0 is still waiting for rank 2 when rank 1
+    comes back)"""
+    import struct
+    import time
+
+    port = _free_port()
+    body = r"""
+import os, sys
+sys.path.insert(0, os.environ["TZ_ROOT"])
+import tenzing_amd as tz
+c = tz._tz.TcpCtrl(int(os.environ["RANK"]), 3)
+c.rendezvous("127.0.0.1", int(os.environ["MASTER_PORT"]), 30.0, 1)
+print("JOINED", c.allreduce_max([float(c.rank)])[0])
+"""
+    env = dict(os.environ, TZ_NO_TORCH="1", TZ_ROOT=ROOT, MASTER_PORT=str(port))
+    ps = [subprocess.Popen([sys.executable, "-c", body], env=dict(env, RANK="0"),
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)]
+    try:
+        # the first, abandoned connection of rank 1: handshake, acknowledged, then closed
+        deadline = time.time() + 30
+        while True:
+            try:
+                s = socket.create_connection(("127.0.0.1", port), timeout=5)
+                break
+            except OSError:
+                if time.time() > deadline:
+                    raise
+                time.sleep(0.1)
+        s.sendall(struct.pack("<Iiii", 0x545A4331, 3, 1, port))
+        assert struct.unpack("<I", s.recv(4))[0] == 0x545A4143
+        s.close()
+        for r in (1, 2):
+            ps.append(subprocess.Popen([sys.executable, "-c", body], env=dict(env, RANK=str(r)),
+                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+        outs = [p.communicate(timeout=60) for p in ps]
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in ps), outs
+    assert all("JOINED 2.0" in o[0] for o in outs), outs

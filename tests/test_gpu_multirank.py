@@ -541,14 +541,56 @@ def test_bench_rccl_across_ranks_loopback(gpu):
 
 
 @rccl_loopback
-def test_spmv_rccl_across_ranks_loopback(gpu):
+@pytest.mark.parametrize("fail_schedule", [False, True])
+def test_spmv_rccl_across_ranks_loopback(gpu, fail_schedule):
     """the distributed SpMV's x halo through RCCL between real ranks (TZ_RCCL_LOOPBACK=1):
-    every schedule's y checked against the host reference, eagerly and as hipGraphs, then a
-    collective search"""
-    res = _launch("spmv", 2, extra_env={"TZ_RCCL_LOOPBACK": "1", "TZ_TEST_SPMV_TRANSPORT": "rccl"})
+    its preflight verifies the exchange compiled into hipGraphs (whole-schedule capture, or
+    child capture when the former is forced to deliver wrong data), then every schedule's y is
+    checked against the host reference, eagerly and as hipGraphs, then a collective search"""
+    env = {"TZ_RCCL_LOOPBACK": "1", "TZ_TEST_SPMV_TRANSPORT": "rccl"}
+    if fail_schedule:
+        env["TZ_FAIL_TRANSPORTS"] = "rccl_graph_schedule"
+    res = _launch("spmv", 2, extra_env=env)
     for r in res:
         assert r["transport"] == "rccl", r["transport"]
+        assert r["rccl_graph_ok"], r["rccl_capture"]
+        if fail_schedule:
+            assert r["rccl_capture"].startswith("child capture (schedule capture: "), r["rccl_capture"]
+        else:
+            assert r["rccl_capture"] == "schedule capture", r["rccl_capture"]
         assert r["mcts"] == (6 if r["rank"] == 0 else 0)
         for run in r["runs"]:
             assert run["err1"] < 1e-4 and run["err2"] < 1e-4, run
             assert not run["ipc"], run
+
+
+@pytest.mark.parametrize("how", ["phase", "transfer"])
+def test_bench_stall_after_headline_loopback(gpu, how):
+    """a diagnostic after the headline stalls on every rank (phase: the link-matrix phase never
+    returns; transfer: every link-matrix transfer never completes): the final line still comes
+    out complete (partial false) with exit status 0 on every rank, within the post-timing
+    budget, and says which diagnostic did not finish"""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+           "--cells", "48", "--mcts-iters", "4", "--bench-iters", "3", "--deadline-s", "300",
+           "--link-probe-iters", "2", "--post-budget-s", "25", "--link-matrix-wait-s", "3"]
+    env = dict(os.environ)
+    if how == "phase":
+        env["TZ_BENCH_STALL"] = "link_matrix"
+    else:
+        env["TZ_LINK_MATRIX_STALL"] = "1"
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=170, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    j = json.loads(lines[0])
+    assert j["partial"] is False and j["phase"] == "done" and j["verified_bad_cells"] == 0
+    assert j["value"] > 0 and "link_probe" in j["post_timing"]["done"]
+    if how == "phase":
+        assert j["post_timing"]["running"] == "link_matrix" and "link_matrix" not in j
+    else:
+        lm = j["link_matrix"]
+        assert lm["stuck"] is True and "did not complete" in lm["why"], lm
+        assert "link_matrix" in j["post_timing"]["done"]

@@ -609,7 +609,7 @@ def test_bench_save_best_then_run(tz, gpu, tmp_path):
     path = tmp_path / "bench_best.json"
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--cells", "64",
                         "--mcts-iters", "6", "--steps", "5", "--warmup", "2", "--rerank", "1",
-                        "--save-best", str(path)], cwd=root, capture_output=True, text=True,
+                        "--subrecords", "off", "--save-best", str(path)], cwd=root, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     doc = json.loads(path.read_text())

@@ -1,5 +1,7 @@
 """Matrix Market input for the SpMV workload (the reference vendors cwpearson/mm but never calls
 it; here any square matrix file can replace the random band matrix)."""
+import json
+
 import pytest
 
 
@@ -72,3 +74,44 @@ def test_spmv_workload_from_file_partitions_every_entry(tz, tmp_path):
     bad = _write(tmp_path / "r.mtx", "%%MatrixMarket matrix coordinate real general\n2 3 1\n1 3 1\n")
     with pytest.raises(Exception, match="square"):
         tz._tz.DistSpmv(SpmvConfig(matrix=bad).args(0, 1, -1))
+
+
+@pytest.mark.parametrize("ranks", [1, 4, 8])
+def test_band_matrix_parity_with_the_reference_generator(tz, ranks):
+    """the reference driver's matrix (spmv_run_strategy.cuh:67-68: m = 150,000, bw = m / ranks,
+    nnz = 10 m) has exactly nnz distinct entries, all with |c - r| <= bw (csr_mat.hpp:334-370:
+    refilled after duplicates are removed; columns drawn in [r - bw, r + bw])"""
+    import numpy as np
+
+    m = 150_000
+    bw = m // ranks
+    rp, ci, v = tz._tz.random_band_matrix(m, bw, 10 * m, 1)
+    rp, ci = np.asarray(rp, dtype=np.int64), np.asarray(ci, dtype=np.int64)
+    assert len(ci) == 10 * m and rp[-1] == 10 * m and len(v) == 10 * m
+    rows = np.repeat(np.arange(m), np.diff(rp))
+    assert np.abs(ci - rows).max() <= bw
+    assert (ci >= 0).all() and (ci < m).all()
+    # distinct (row, column) pairs, columns sorted within each row
+    key = rows * m + ci
+    assert (np.diff(key) > 0).all()
+
+
+def test_spmv_workload_records_its_actual_nnz(tz):
+    """every rank builds the same matrix; the args say how many entries it has, and the ranks'
+    local + remote blocks partition exactly those"""
+    from tenzing_amd.models import SpmvConfig
+
+    total = 0
+    for r in range(4):
+        s = tz._tz.DistSpmv(SpmvConfig(m=20_000).args(r, 4, -1))
+        assert s.args.nnz_actual == 200_000
+        assert json.loads(s.args.json())["nnz_actual"] == 200_000
+        total += s.local_nnz() + s.remote_nnz()
+    assert total == 200_000
+
+
+def test_band_matrix_rejects_more_entries_than_the_band_holds(tz):
+    with pytest.raises(Exception, match="exceeds"):
+        tz._tz.random_band_matrix(10, 1, 29, 1)  # 3 per row, minus the 2 corners: 28
+    rp, ci, _ = tz._tz.random_band_matrix(10, 1, 28, 1)
+    assert len(ci) == 28
