@@ -246,6 +246,14 @@ PYBIND11_MODULE(_tz, m) {
       .def_property_readonly("kind", &OpBase::kind)
       .def_property_readonly("op_class", [](const OpBase &o) { return std::string(op_class_name(o.op_class())); })
       .def("json", [](const OpBase &o) { return o.json().dump(); })
+      .def("traffic", [](const OpBase &o) {
+             const GpuOp *g = dynamic_cast<const GpuOp *>(&o);
+             if (auto b = dynamic_cast<const BoundGpuOp *>(&o)) g = b->unbound().get();
+             py::list l;
+             if (g)
+               for (const Traffic &t : g->traffic()) l.append(py::make_tuple(t.resource, t.engine, t.bytes));
+             return l;
+           }, "(resource, engine, bytes) a GPU op moves, for the link-aware simulator ([] otherwise)")
       .def("desc", &OpBase::desc)
       .def("eq", &OpBase::eq)
       .def_property_readonly("cost_us", &OpBase::cost_us)
@@ -254,7 +262,8 @@ PYBIND11_MODULE(_tz, m) {
       .def("__repr__", [](const OpBase &o) { return "<" + o.kind() + " " + o.desc() + ">"; });
   py::class_<BoundOp, OpBase, std::shared_ptr<BoundOp>>(m, "BoundOp");
   py::class_<CpuOp, BoundOp, std::shared_ptr<CpuOp>>(m, "CpuOp");
-  py::class_<GpuOp, OpBase, std::shared_ptr<GpuOp>>(m, "GpuOp");
+  py::class_<GpuOp, OpBase, std::shared_ptr<GpuOp>>(m, "GpuOp")
+      .def("latency_us", &GpuOp::latency_us);
   py::class_<Start, CpuOp, std::shared_ptr<Start>>(m, "Start").def(py::init<>());
   py::class_<Finish, CpuOp, std::shared_ptr<Finish>>(m, "Finish").def(py::init<>());
   py::class_<NoOp, CpuOp, std::shared_ptr<NoOp>>(m, "NoOp")
@@ -263,8 +272,16 @@ PYBIND11_MODULE(_tz, m) {
   py::class_<PyCpuOp, CpuOp, std::shared_ptr<PyCpuOp>>(m, "PyCpuOp")
       .def(py::init<std::string, py::function, double>(), py::arg("name"), py::arg("fn"), py::arg("cost_us") = 0.0);
   py::class_<SimGpuOp, GpuOp, std::shared_ptr<SimGpuOp>>(m, "SimGpuOp")
-      .def(py::init<std::string, double, std::string>(), py::arg("name"), py::arg("us"),
-           py::arg("domain") = "");
+      .def(py::init([](std::string name, double us, std::string domain, py::list traffic) {
+             std::vector<Traffic> tr;
+             for (auto h : traffic) {
+               auto t = h.cast<py::tuple>();
+               tr.push_back({t[0].cast<std::string>(), t[1].cast<std::string>(), t[2].cast<double>()});
+             }
+             return std::make_shared<SimGpuOp>(std::move(name), us, std::move(domain), std::move(tr));
+           }), py::arg("name"), py::arg("us"), py::arg("domain") = "", py::arg("traffic") = py::list(),
+           "a GPU op that only models time: `us`, or with `traffic` [(resource, engine, bytes)] "
+           "that fixed latency plus its transfers under the link-aware model");
   py::class_<PyGpuOp, GpuOp, std::shared_ptr<PyGpuOp>>(m, "PyGpuOp")
       .def(py::init<std::string, py::function, double, bool, std::string>(), py::arg("name"),
            py::arg("fn"), py::arg("cost_us") = 0.0, py::arg("capturable") = true,
@@ -478,9 +495,15 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("sync_us", &SimParams::sync_us)
       .def_readwrite("noise", &SimParams::noise)
       .def_readwrite("seed", &SimParams::seed)
-      .def_readwrite("contention", &SimParams::contention);
+      .def_readwrite("contention", &SimParams::contention)
+      .def_readwrite("link_model", &SimParams::link_model)
+      .def_readwrite("engine_GBps", &SimParams::engine_GBps)
+      .def_readwrite("resource_GBps", &SimParams::resource_GBps);
   py::class_<SimBenchmarker, Benchmarker>(m, "SimBenchmarker")
-      .def(py::init<int, SimParams>(), py::arg("n_streams"), py::arg("params") = SimParams());
+      .def(py::init<int, SimParams, Ctrl *>(), py::arg("n_streams"), py::arg("params") = SimParams(),
+           py::arg("ctrl") = nullptr, py::keep_alive<1, 4>(),
+           "discrete-event model; with `ctrl`, every rank simulates its own copy of each schedule "
+           "and the result is the max over ranks");
   py::class_<SimExecutor>(m, "SimExecutor")
       .def(py::init<int, SimParams>(), py::arg("n_streams"), py::arg("params") = SimParams())
       .def("run_once", &SimExecutor::run_once)
@@ -994,6 +1017,23 @@ PYBIND11_MODULE(_tz, m) {
       .def("shift_all", [](const HaloExchange &h, uintptr_t s) { h.shift_all(P(s)); })
       .def("direct", [](const HaloExchange &h, int i, uintptr_t s) { h.direct(i, P(s)); })
       .def("direct_group", [](const HaloExchange &h, std::vector<int> d, uintptr_t s) { h.direct_group(d, P(s)); })
+      .def("direct_moves", [](const HaloExchange &h, std::vector<int> dirs) {
+             py::list l;
+             for (const kern::MoveDesc &m : h.direct_moves(dirs)) {
+               py::dict d;
+               d["src_off"] = m.src_off;
+               d["dst_off"] = m.dst_off;
+               d["len"] = m.len;
+               d["n"] = py::make_tuple(m.n1, m.n2, m.n3);
+               d["s"] = py::make_tuple(m.s1, m.s2, m.s3);
+               d["pair"] = m.pair;
+               l.append(d);
+             }
+             return l;
+           }, "the moves direct_group launches for these directions (no GPU needed)")
+      .def("move_roof", &HaloExchange::move_roof, py::arg("iters") = 20, py::call_guard<py::gil_scoped_release>(),
+           "the fused direct move against its shape-matched roof (same 128-B lines, whole-line "
+           "accesses): us per launch of each, lines read / written, payload (re-inits the grid)")
       .def("uses_rccl", &HaloExchange::uses_rccl)
       .def("rccl_graph_ok", &HaloExchange::rccl_graph_ok, "RCCL ops may be captured into hipGraphs")
       .def("uses_direct", &HaloExchange::uses_direct)

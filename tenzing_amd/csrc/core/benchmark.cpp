@@ -229,14 +229,56 @@ double SimExecutor::dur(double us) {
   return std::max(0.0, us * nd(rng_));
 }
 
+double SimParams::rate_GBps(const std::string &engine) const {
+  const auto it = engine_GBps.find(engine);
+  TZ_CHECK(it != engine_GBps.end() && it->second > 0, "sim: no rate for engine '" << engine << "'");
+  return it->second;
+}
+
+double SimParams::capacity_GBps(const std::string &resource) const {
+  auto it = resource_GBps.find(resource);
+  if (it == resource_GBps.end()) it = resource_GBps.find(resource.substr(0, resource.find(':')));
+  TZ_CHECK(it != resource_GBps.end() && it->second > 0, "sim: no capacity for resource '" << resource << "'");
+  return it->second;
+}
+
+double SimExecutor::link_duration(const GpuOp &op, double start) {
+  const std::vector<Traffic> tr = op.traffic();
+  // bytes per (resource, engine): an op that sends several boxes to one peer is one transfer
+  std::map<std::pair<std::string, std::string>, double> per;
+  for (const Traffic &t : tr)
+    if (t.bytes > 0) per[{t.resource, t.engine}] += t.bytes;
+  double slowest = 0;
+  for (const auto &kv : per) {
+    const std::vector<double> &ends = active_[kv.first.first];
+    int k = 0;
+    for (double e : ends) k += e > start;
+    const double rate = std::min(p_.rate_GBps(kv.first.second),
+                                 p_.capacity_GBps(kv.first.first) / double(k + 1));
+    slowest = std::max(slowest, kv.second / (rate * 1e3)); // GB/s = 1e3 bytes per us
+  }
+  const double d = dur(op.latency_us() + slowest);
+  for (const auto &kv : per) {
+    std::vector<double> &ends = active_[kv.first.first];
+    ends.erase(std::remove_if(ends.begin(), ends.end(), [&](double e) { return e <= start; }), ends.end());
+    ends.push_back(start + d);
+  }
+  return d;
+}
+
 void SimExecutor::launch(const GpuOp &op, int stream) {
   TZ_CHECK(stream >= 0 && stream < n_, "sim stream out of range");
   host_ += p_.launch_us;
   const double start = std::max(host_, streamFree_[stream]);
-  int busy = 0;
-  for (int s = 0; s < n_; ++s)
-    if (s != stream && streamFree_[s] > start) ++busy;
-  const double d = dur(op.cost_us()) * (1.0 + p_.contention * busy);
+  double d;
+  if (p_.link_model && !op.traffic().empty()) {
+    d = link_duration(op, start);
+  } else {
+    int busy = 0;
+    for (int s = 0; s < n_; ++s)
+      if (s != stream && streamFree_[s] > start) ++busy;
+    d = dur(op.cost_us()) * (1.0 + p_.contention * busy);
+  }
   streamFree_[stream] = start + d;
   trace_.push_back({op.name(), stream, start, start + d});
 }
@@ -279,6 +321,7 @@ double SimExecutor::run_once(const Sequence &seq) {
   std::fill(streamFree_.begin(), streamFree_.end(), 0.0);
   events_.assign(events_.size(), 0.0);
   trace_.clear();
+  active_.clear();
   for (const auto &e : seq.entries) e.op->run(*this);
   // the sequence ends host-synchronized with all its GPU work (Finish has GPU preds synced)
   double end = host_;
@@ -293,6 +336,7 @@ BenchResult SimBenchmarker::benchmark(const Sequence &seq, const BenchOpts &opts
   std::vector<double> times;
   const int64_t n = std::max<int64_t>(1, std::min<int64_t>(opts.n_iters, 200));
   for (int64_t i = 0; i < n; ++i) times.push_back(ex.run_once(seq) * 1e-6);
+  if (ctrl_ && ctrl_->size() > 1) ctrl_->allreduce_max(times.data(), times.size()); // max over ranks
   BenchResult r = BenchResult::from_times(times);
   r.samples_per_measurement = 1;
   return r;

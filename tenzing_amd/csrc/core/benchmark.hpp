@@ -156,6 +156,20 @@ struct SimParams {
   /// concurrent kernels share the device: when k GPU ops overlap, each runs at rate
   /// 1/(1 + contention*(k-1)); 0 = perfect overlap
   double contention = 0.0;
+  /// Link-aware model: a GPU op that reports traffic() takes latency_us() plus, over its
+  /// resources, the longest bytes / rate, where rate = min(engine rate, resource capacity /
+  /// (transfers active on that resource when it starts + 1)). Ops without traffic keep cost_us().
+  bool link_model = false;
+  /// GB/s one transfer of an engine reaches alone (kernel: a local HBM stream; put / wide:
+  /// kernel stores over one xGMI link at the default / wide workgroup count; sdma / memcpy: copy
+  /// engines; rccl: an RCCL send; host: stores into host memory over PCIe)
+  std::map<std::string, double> engine_GBps = {{"kernel", 5000.0}, {"put", 60.0},  {"wide", 90.0},
+                                               {"sdma", 50.0},     {"memcpy", 50.0}, {"rccl", 50.0},
+                                               {"host", 40.0}};
+  /// capacity of a resource class (the text before ':') or of one resource ("xgmi:3")
+  std::map<std::string, double> resource_GBps = {{"hbm", 5000.0}, {"xgmi", 120.0}, {"pcie", 50.0}};
+  double rate_GBps(const std::string &engine) const;
+  double capacity_GBps(const std::string &resource) const;
 };
 
 class SimExecutor : public Executor {
@@ -182,24 +196,32 @@ public:
 
 private:
   double dur(double us);
+  /// duration of a GPU op starting at `start` under the link-aware model (registers its
+  /// transfers as active on their resources until start + duration)
+  double link_duration(const GpuOp &op, double start);
   int n_;
   SimParams p_;
   std::mt19937_64 rng_;
   double host_ = 0;
   std::vector<double> streamFree_;
+  std::map<std::string, std::vector<double>> active_; // resource -> end times of its transfers
   std::vector<double> events_;
   std::vector<Span> trace_;
 };
 
 class SimBenchmarker : public Benchmarker {
 public:
-  SimBenchmarker(int nStreams, SimParams p) : n_(nStreams), p_(p), rng_(p.seed + 17) {}
+  /// `ctrl` (optional): every rank simulates its own graph's copy of the sequence and the
+  /// result is the max over ranks, as the empirical benchmarker's is (SPMD searches on CPUs)
+  SimBenchmarker(int nStreams, SimParams p, Ctrl *ctrl = nullptr)
+      : n_(nStreams), p_(p), rng_(p.seed + 17), ctrl_(ctrl) {}
   BenchResult benchmark(const Sequence &seq, const BenchOpts &opts) override;
 
 private:
   int n_;
   SimParams p_;
   std::mt19937_64 rng_;
+  Ctrl *ctrl_ = nullptr;
 };
 
 /// Replays recorded timings from a results CSV (`i|p01|p10|p50|p90|p99|stddev|op-json|...`),

@@ -133,6 +133,16 @@ private:
   double us_;
 };
 
+/// Bytes an op moves through one shared resource, for the simulator's link-aware cost model
+/// (SimParams::link_model): `resource` is what concurrent ops share ("hbm", "xgmi:<peer rank>",
+/// "pcie"), `engine` what moves the bytes ("kernel", "put", "wide", "sdma", "memcpy", "rccl",
+/// "host"), which caps the rate one transfer gets.
+struct Traffic {
+  std::string resource;
+  std::string engine;
+  double bytes = 0;
+};
+
 /// GPU work that has to be bound to a stream. Implementations enqueue on `stream`
 /// (a hipStream_t, passed as void* so this header stays HIP-free).
 class GpuOp : public OpBase {
@@ -141,24 +151,33 @@ public:
   virtual void launch(void *stream, Executor &ex) const = 0;
   /// true if the op can be recorded into a hipGraph by stream capture
   virtual bool capturable() const { return true; }
+  /// the bytes this op moves through shared resources (empty: the simulator uses cost_us())
+  virtual std::vector<Traffic> traffic() const { return {}; }
+  /// fixed time beside the traffic (launch, signalling), for the link-aware model
+  virtual double latency_us() const { return 4.0; }
 };
 using GpuOpPtr = std::shared_ptr<const GpuOp>;
 
 /// GPU op that only models time (simulation / tests). On a real executor it launches nothing.
 class SimGpuOp : public GpuOp {
 public:
-  SimGpuOp(std::string name, double us, std::string domain = "")
-      : name_(std::move(name)), us_(us), domain_(std::move(domain)) {}
+  /// `traffic` (optional): what it moves under the link-aware model, which then takes
+  /// `us` as its fixed latency instead of its whole cost
+  SimGpuOp(std::string name, double us, std::string domain = "", std::vector<Traffic> traffic = {})
+      : name_(std::move(name)), us_(us), domain_(std::move(domain)), traffic_(std::move(traffic)) {}
   std::string name() const override { return name_; }
   std::string kind() const override { return "SimGpuOp"; }
   double cost_us() const override { return us_; }
   std::string order_domain() const override { return domain_; }
   void launch(void *, Executor &) const override {}
+  std::vector<Traffic> traffic() const override { return traffic_; }
+  double latency_us() const override { return us_; }
 
 private:
   std::string name_;
   double us_;
   std::string domain_;
+  std::vector<Traffic> traffic_;
 };
 
 class BoundGpuOp : public BoundOp {

@@ -255,6 +255,44 @@ __device__ __forceinline__ void move_body(const DevDesc &d, uint32_t tid, uint32
   }
 }
 
+// row pair (MoveDesc::pair, d.vec = -len): item (row, k), k < 2 len: k < len moves element k of
+// run A (row end -> row start), k >= len element k - len of run B (row start -> row end).
+// Consecutive lanes cover consecutive k of a row, as the plain move covers a row's x: per row
+// the same 2 line loads and 2 line stores as two separate boxes, but the lines a row's lanes
+// load are the lines its lanes store into (x = 0 at the row start), within one wave.
+template <int U, bool NTS>
+__device__ __forceinline__ void pair_body(const DevDesc &d, uint32_t tid, uint32_t nthreads) {
+  const int64_t len = -d.vec;
+  const double *__restrict__ src = d.src;
+  double *__restrict__ grid = d.buf;
+  uint32_t it = tid;
+  for (; it + (U - 1) * nthreads < d.items; it += U * nthreads) {
+    double v[U];
+    int64_t to[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = grid_index<1>(d, it + u * nthreads); // row base + k
+      const uint32_t row = d.dl.div(it + u * nthreads);
+      const int64_t k = int64_t(it + u * nthreads - row * d.lvec);
+      const int64_t base = g - k;
+      const int64_t from = k < len ? base + k : base + k + d.delta;          // A: end, B: start
+      to[u] = k < len ? base + d.delta + k : base + k;                        // A: start, B: end
+      v[u] = src[from];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NTS>(grid + to[u], v[u]);
+  }
+  for (; it < d.items; it += nthreads) {
+    const int64_t g = grid_index<1>(d, it);
+    const uint32_t row = d.dl.div(it);
+    const int64_t k = int64_t(it - row * d.lvec);
+    const int64_t base = g - k;
+    const int64_t from = k < len ? base + k : base + k + d.delta;
+    const int64_t to = k < len ? base + d.delta + k : base + k;
+    st<NTS>(grid + to, src[from]);
+  }
+}
+
 template <int U, bool NT, bool NTS>
 __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap r) {
   const uint32_t lb = logical_block(r);
@@ -272,7 +310,60 @@ __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap
   const uint32_t tid = j * kThreads + threadIdx.x;
   const uint32_t nth = nb * kThreads;
   if (d.vec == 2) move_body<2, U, NT, NTS>(d, tid, nth);
+  else if (d.vec < 0) pair_body<U, NTS>(d, tid, nth);
   else move_body<1, U, NT, NTS>(d, tid, nth);
+}
+
+// shape-matched roof (line_roof): whole lines, 16-B accesses; d.vec carries the mode. U items
+// per lane in flight (all loads issued before any is used); NTS: non-temporal stores (as the
+// move's ghost stores)
+template <int U, bool NTS>
+__global__ __launch_bounds__(kThreads) void line_roof_k(DevBatch b, double zero, double *sink) {
+  int box = 0;
+  while (box + 1 < b.n && blockIdx.x >= b.block_start[box + 1]) ++box;
+  const DevDesc &d = b.d[box];
+  const uint32_t nb = b.block_start[box + 1] - b.block_start[box];
+  const uint32_t tid = (blockIdx.x - b.block_start[box]) * kThreads + threadIdx.x;
+  const uint32_t nth = nb * kThreads;
+  const dbl2_t z = {zero, zero};
+  dbl2_t acc = z;
+  uint32_t it = tid;
+  for (; it + (U - 1) * nth < d.items; it += U * nth) {
+    dbl2_t *p[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) p[k] = reinterpret_cast<dbl2_t *>(d.buf + grid_index<2>(d, it + k * nth));
+    if (d.vec == 1) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) st<NTS>(p[k], z);
+    } else if (d.vec == 3) { // line-to-line copy: p indexes the source, + delta the target
+      dbl2_t v[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) v[k] = *reinterpret_cast<const dbl2_t *>(d.src + (reinterpret_cast<double *>(p[k]) - d.buf));
+#pragma unroll
+      for (int k = 0; k < U; ++k) st<NTS>(reinterpret_cast<dbl2_t *>(reinterpret_cast<double *>(p[k]) + d.delta), v[k]);
+    } else {
+      dbl2_t v[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) v[k] = *p[k];
+      if (d.vec == 0) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) acc += v[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < U; ++k) st<NTS>(p[k], v[k] + z); // read, written back by the same lane
+      }
+    }
+  }
+  for (; it < d.items; it += nth) {
+    dbl2_t *p = reinterpret_cast<dbl2_t *>(d.buf + grid_index<2>(d, it));
+    if (d.vec == 0) acc += *p;
+    else if (d.vec == 1) st<NTS>(p, z);
+    else if (d.vec == 3)
+      st<NTS>(reinterpret_cast<dbl2_t *>(reinterpret_cast<double *>(p) + d.delta),
+              *reinterpret_cast<const dbl2_t *>(d.src + (reinterpret_cast<double *>(p) - d.buf)));
+    else st<NTS>(p, *p + z);
+  }
+  if (acc.x + acc.y == 1.0e300) sink[0] = acc.x; // keeps the loads; never taken on a probe grid
 }
 
 struct DevSignal {
@@ -648,6 +739,8 @@ void box_move_many_signal(const MoveDesc *moves, int n, const MoveSignal &sig, v
   if (!sig.done) throw std::runtime_error("box_move_many_signal: null block counters");
   uint32_t total = 0;
   std::vector<int> keep;
+  for (int i = 0; i < n; ++i)
+    if (moves[i].pair) throw std::runtime_error("box_move_many_signal: row pairs are for self moves only");
   const DevBatch b = make_move_batch(moves, n, total, keep, put_cap(sig));
   if (b.n != n) throw std::runtime_error("box_move_many_signal: empty box (nothing to signal)");
   DevSignal ds{};
@@ -756,6 +849,21 @@ DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vec
     if (d.items == 0) continue;
     d.src = m.src;
     d.delta = m.dst_off - m.src_off;
+    if (m.pair) {
+      if (m.src != m.dst || m.len < 1 || m.len > kMaxPairLen)
+        throw std::runtime_error("box_move_many: a row pair needs src == dst and 1..8 elements per run");
+      // items (row, k < 2 len); d.vec < 0 marks the pair and carries the run length
+      d.vec = -m.len;
+      d.lvec = uint32_t(2 * m.len);
+      d.items = uint32_t(uint64_t(d.lvec) * m.n1 * m.n2 * m.n3);
+      d.dl = FastDiv(d.lvec);
+      b.d[b.n] = d;
+      b.block_start[b.n] = total;
+      total += blocks_for(d, cap, unroll);
+      keep.push_back(i);
+      ++b.n;
+      continue;
+    }
     // 16-B accesses need both rows 16-B aligned: make_dev checked the source side (and the
     // destination base); the destination offset must be even as well
     if (d.vec == 2 && (m.dst_off % 2 != 0 || reinterpret_cast<uintptr_t>(m.src) % 16 != 0)) {
@@ -774,6 +882,120 @@ DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vec
   return b;
 }
 } // namespace
+
+std::vector<LineBox> line_boxes(const MoveDesc *moves, int n, bool copies) {
+  std::vector<LineBox> reads, writes, moved;
+  auto add = [](std::vector<LineBox> &v, const MoveDesc &m, double *base, int64_t off) {
+    if (m.s1 % 16 || m.s2 % 16 || m.s3 % 16)
+      throw std::runtime_error("line_boxes: row strides must be whole 128-B lines");
+    LineBox b;
+    b.base = base;
+    b.off = off / 16 * 16;
+    b.lines = int32_t((off + m.len - 1) / 16 - off / 16 + 1);
+    b.s1 = m.s1;
+    b.s2 = m.s2;
+    b.s3 = m.s3;
+    b.n1 = m.n1;
+    b.n2 = m.n2;
+    b.n3 = m.n3;
+    v.push_back(b);
+  };
+  for (int i = 0; i < n; ++i) {
+    const MoveDesc &m = moves[i];
+    double *src = const_cast<double *>(m.src);
+    if (m.pair) {
+      const int64_t delta = m.dst_off - m.src_off;
+      add(reads, m, src, m.src_off);
+      add(reads, m, src, m.src_off + m.len + delta);
+      add(writes, m, m.dst, m.dst_off);
+      add(writes, m, m.dst, m.src_off + m.len);
+    } else {
+      add(reads, m, src, m.src_off);
+      add(writes, m, m.dst, m.dst_off);
+      const LineBox &r = reads.back(), &w = writes.back();
+      if (copies && r.lines == w.lines && m.src_off % 16 == m.dst_off % 16) {
+        LineBox c = r;
+        c.mode = 3;
+        c.dst_base = w.base;
+        c.dst_off = w.off;
+        moved.push_back(c);
+        reads.pop_back();
+        writes.pop_back();
+      }
+    }
+  }
+  auto same = [](const LineBox &a, const LineBox &b) {
+    return a.base == b.base && a.off == b.off && a.lines == b.lines && a.s1 == b.s1 && a.s2 == b.s2 &&
+           a.s3 == b.s3 && a.n1 == b.n1 && a.n2 == b.n2 && a.n3 == b.n3;
+  };
+  std::vector<LineBox> out;
+  std::vector<bool> merged(writes.size(), false);
+  for (LineBox r : reads) {
+    r.mode = 0;
+    for (size_t k = 0; k < writes.size(); ++k)
+      if (!merged[k] && same(r, writes[k])) {
+        r.mode = 2;
+        merged[k] = true;
+        break;
+      }
+    out.push_back(r);
+  }
+  for (size_t k = 0; k < writes.size(); ++k)
+    if (!merged[k]) {
+      LineBox w = writes[k];
+      w.mode = 1;
+      out.push_back(w);
+    }
+  out.insert(out.begin(), moved.begin(), moved.end());
+  return out;
+}
+
+void line_roof(const LineBox *boxes, int n, void *stream, int variant) {
+  if (variant < 0 || variant >= kLineRoofVariants) throw std::runtime_error("line_roof: bad variant");
+  static double *sink = nullptr;
+  if (!sink && hipMalloc(&sink, 64) != hipSuccess) throw std::runtime_error("line_roof: hipMalloc");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int k0 = 0; k0 < n; k0 += kMaxBoxes) {
+    DevBatch b{};
+    uint32_t total = 0;
+    for (int i = k0; i < std::min(n, k0 + kMaxBoxes); ++i) {
+      BoxDesc box;
+      box.buf = boxes[i].base;
+      box.grid_off = boxes[i].off;
+      box.len = boxes[i].lines * 16;
+      box.n1 = boxes[i].n1;
+      box.n2 = boxes[i].n2;
+      box.n3 = boxes[i].n3;
+      box.s1 = boxes[i].s1;
+      box.s2 = boxes[i].s2;
+      box.s3 = boxes[i].s3;
+      DevDesc d = make_dev(box);
+      if (d.items == 0) continue;
+      if (d.vec != 2) throw std::runtime_error("line_roof: boxes must be whole 128-B lines");
+      d.buf = boxes[i].base;
+      d.vec = boxes[i].mode;
+      if (boxes[i].mode == 3) { // source: base; target: dst_base + dst_off, same geometry
+        if (!boxes[i].dst_base) throw std::runtime_error("line_roof: copy box without a target");
+        d.src = boxes[i].base;
+        d.buf = boxes[i].base;
+        d.delta = (boxes[i].dst_base - boxes[i].base) + (boxes[i].dst_off - boxes[i].off);
+      }
+      b.d[b.n] = d;
+      b.block_start[b.n] = total;
+      total += blocks_for(d, 0, std::max(1, box_tuning().move_items));
+      ++b.n;
+    }
+    if (b.n == 0) continue;
+    b.block_start[b.n] = total;
+    switch (variant) { // (items in flight per lane, non-temporal stores)
+    case 0: hipLaunchKernelGGL((line_roof_k<1, true>), dim3(total), dim3(kThreads), 0, s, b, 0.0, sink); break;
+    case 1: hipLaunchKernelGGL((line_roof_k<4, true>), dim3(total), dim3(kThreads), 0, s, b, 0.0, sink); break;
+    case 2: hipLaunchKernelGGL((line_roof_k<1, false>), dim3(total), dim3(kThreads), 0, s, b, 0.0, sink); break;
+    default: hipLaunchKernelGGL((line_roof_k<4, false>), dim3(total), dim3(kThreads), 0, s, b, 0.0, sink); break;
+    }
+    TZ_HIP_LAUNCH_CHECK();
+  }
+}
 
 } // namespace kern
 } // namespace tz

@@ -5,6 +5,7 @@
 #pragma once
 
 #include <cstdint>
+#include <vector>
 
 namespace tz {
 namespace kern {
@@ -73,9 +74,44 @@ struct MoveDesc {
   int64_t src_off = 0, dst_off = 0;
   int64_t s1 = 0, s2 = 0, s3 = 0;
   int32_t len = 0, n1 = 0, n2 = 0, n3 = 0;
+  /// row pair (self-wrap of the x axis in one array, src == dst): every row also moves its
+  /// run [src - (dst_off - src_off) - ... ] back the other way. With delta = dst_off - src_off,
+  /// row element e = src_off + row: [e, e + len) -> [e + delta, ...) AND
+  /// [e + len + delta, e + 2 len + delta) -> [e + len, e + 2 len) -- the +x and -x boxes of one
+  /// (dy, dz) moved by one lane per row, so that a row's ghost and source runs that share a
+  /// cache line (x = 0 at the row start) are read and written while the line is in L2.
+  /// At most kMaxPairLen elements per run.
+  bool pair = false;
 };
+constexpr int kMaxPairLen = 8;
 /// up to kMaxBoxes moves in ONE launch
 void box_move_many(const MoveDesc *d, int n, void *stream);
+
+/// Shape-matched roof probe of a move: whole 128-B lines of a pitched array, rows of `lines`
+/// lines at `off` (elements, a multiple of 16) with strides s1..s3 (multiples of 16), read
+/// (mode 0), written (mode 1) or read and written back by the same lane (mode 2), with full
+/// 16-B accesses and the same flat indexing as the move. One launch for all boxes: the time of
+/// touching exactly the lines a move touches, at the best access shape.
+struct LineBox {
+  double *base = nullptr;
+  int64_t off = 0, s1 = 0, s2 = 0, s3 = 0;
+  int32_t lines = 0, n1 = 0, n2 = 0, n3 = 0;
+  /// 0 read, 1 write, 2 read + write back, 3 line-to-line copy to dst_base + dst_off (the
+  /// move's own shape: each lane loads 16 B of a source line and stores them to its target line)
+  int mode = 0;
+  double *dst_base = nullptr;
+  int64_t dst_off = 0;
+};
+/// variants: 0 one item in flight per lane + non-temporal stores, 1 four in flight + nt,
+/// 2 one + plain stores, 3 four + plain
+constexpr int kLineRoofVariants = 4;
+void line_roof(const LineBox *boxes, int n, void *stream, int variant = 0);
+/// the line boxes a batch of moves reads and writes (a move's rows at one intra-line alignment:
+/// every row covers the same number of lines). `copies`: a move whose source and destination
+/// rows cover the same number of lines becomes one mode-3 box (line-to-line copy, the move's
+/// shape); otherwise reads and writes are separate boxes. Lines read and written by the same
+/// rows become mode-2 boxes.
+std::vector<LineBox> line_boxes(const MoveDesc *moves, int n, bool copies = true);
 
 /// Completion signal of a move whose destination is another rank's memory (IPC peer put):
 /// when the last block of box i has stored its part, it makes every store of the box visible

@@ -3,6 +3,9 @@
 // IPC / SDMA transport: halo_ipc.cpp; op graph: halo_graph.cpp; stencil: halo_stencil.cpp.
 #include "halo_internal.hpp"
 
+#include <functional>
+#include <map>
+
 #include "core/health.hpp"
 #include "core/solve.hpp"
 
@@ -857,7 +860,7 @@ void HaloExchange::shift_group(const std::vector<int> &dirs, void *stream, int s
   }
 }
 
-void HaloExchange::direct_group(const std::vector<int> &dirs_in, void *stream) const {
+std::vector<kern::MoveDesc> HaloExchange::direct_moves(const std::vector<int> &dirs_in) const {
   // faces first, then edges, then corners: blocks are dispatched box by box in batch order,
   // and leaving the many small edge/corner boxes for the last waves measured best (fused
   // 26-direction move 44.13 us vs 44.23 in the natural order and 45.18 with the small boxes
@@ -870,7 +873,6 @@ void HaloExchange::direct_group(const std::vector<int> &dirs_in, void *stream) c
   std::vector<kern::MoveDesc> ms;
   for (int i : dirs) {
     TZ_CHECK(i >= 0 && i < ndirs() && direct_[i], "direction " << i << " is not a direct (self) transfer");
-    TZ_CHECK(ready(), "halo not set up");
     // my slab facing d lands in nbr(d)'s ghost on side -d (self-neighbours: my own grid)
     const kern::BoxDesc s = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
     const kern::BoxDesc d = make_box(a_, dirs_[opp_[i]], true, xoff_, sy_, sz_, sq_);
@@ -889,8 +891,163 @@ void HaloExchange::direct_group(const std::vector<int> &dirs_in, void *stream) c
     if (a_.ghost_align > 0) widen_to_sectors(dirs_[opp_[i]].dx, m);
     ms.push_back(m);
   }
+  if (a_.order == "xyzq" && move_pairs()) ms = pair_x_moves(ms);
+  return ms;
+}
+
+void HaloExchange::direct_group(const std::vector<int> &dirs, void *stream) const {
+  TZ_CHECK(ready(), "halo not set up");
+  const std::vector<kern::MoveDesc> ms = direct_moves(dirs);
   for (size_t k = 0; k < ms.size(); k += kern::kMaxBoxes)
     kern::box_move_many(ms.data() + k, int(std::min<size_t>(kern::kMaxBoxes, ms.size() - k)), stream);
+}
+
+std::map<std::string, double> HaloExchange::move_roof(int iters) {
+  // The fused direct move of every self direction against the shape-matched roof: a kernel
+  // that touches exactly the lines the move touches (line_boxes: per box, the 128-B lines of
+  // its source rows read, of its destination rows written; rows a lane both reads and writes
+  // read and written back together), with whole-line 16-B accesses and trivial indexing. Both
+  // timed back to back on one stream, `iters` launches each after 3 untimed ones; the grid is
+  // initialized again afterwards (the roof writes zeros into the lines it writes).
+  TZ_CHECK(ready(), "halo not set up");
+  TZ_CHECK(iters >= 1, "iters must be positive");
+  std::vector<int> dirs;
+  for (int i = 0; i < ndirs(); ++i)
+    if (direct_[i]) dirs.push_back(i);
+  TZ_CHECK(!dirs.empty(), "move_roof: no direct (self) direction");
+  const std::vector<kern::MoveDesc> ms = direct_moves(dirs);
+  // the same lines as line-to-line copies where a move's source and target rows cover equal
+  // lines (the move's own shape), and as separate read-only and write-only boxes
+  const std::vector<kern::LineBox> lb = kern::line_boxes(ms.data(), int(ms.size()), true);
+  const std::vector<kern::LineBox> lbSplit = kern::line_boxes(ms.data(), int(ms.size()), false);
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  TZ_HIP(hipEventCreate(&e0));
+  TZ_HIP(hipEventCreate(&e1));
+  auto time = [&](const std::function<void()> &launch) {
+    for (int k = 0; k < 3; ++k) launch();
+    TZ_HIP(hipEventRecord(e0, s));
+    for (int k = 0; k < iters; ++k) launch();
+    TZ_HIP(hipEventRecord(e1, s));
+    TZ_HIP(hipEventSynchronize(e1));
+    float ms_ = 0;
+    TZ_HIP(hipEventElapsedTime(&ms_, e0, e1));
+    return double(ms_) * 1e3 / iters;
+  };
+  std::map<std::string, double> r;
+  try {
+    r["move_us"] = time([&] { direct_group(dirs, s); });
+    // each roof: the fastest of its access variants (items in flight, store policy)
+    auto roof = [&](const std::vector<kern::LineBox> &boxes, const std::string &key) {
+      double best = 0;
+      for (int v = 0; v < kern::kLineRoofVariants; ++v) {
+        const double t = time([&] { kern::line_roof(boxes.data(), int(boxes.size()), s, v); });
+        r[key + "_v" + std::to_string(v)] = t;
+        if (v == 0 || t < best) best = t;
+      }
+      r[key] = best;
+    };
+    roof(lb, "roof_us");
+    roof(lbSplit, "roof_split_us");
+    // the same number of lines read and written as one contiguous line-to-line copy (the plain
+    // HBM roof of this traffic, no shape at all)
+    int64_t lines = 0;
+    for (const kern::LineBox &b : lb)
+      if (b.mode != 1) lines += int64_t(b.lines) * b.n1 * b.n2 * b.n3;
+    if (lines > 0 && 2 * lines * 16 + (int64_t(1) << 20) <= int64_t(gridElems_) && lines < (int64_t(1) << 27)) {
+      kern::LineBox c;
+      c.base = c.dst_base = grid();
+      c.off = 0;
+      c.dst_off = (lines * 16 + (int64_t(1) << 17)) / 16 * 16;
+      c.lines = int32_t(lines);
+      c.n1 = c.n2 = c.n3 = 1;
+      c.mode = 3;
+      roof({c}, "copy_roof_us");
+    }
+    r["move_us_again"] = time([&] { direct_group(dirs, s); });
+  } catch (...) {
+    (void)hipStreamSynchronize(s);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(s);
+    throw;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(s);
+  double rd = 0, wr = 0, payload = 0, rows = 0;
+  for (const kern::LineBox &b : lb) {
+    const double bytes = 128.0 * b.lines * double(b.n1) * b.n2 * b.n3;
+    if (b.mode != 1) rd += bytes;
+    if (b.mode != 0) wr += bytes;
+  }
+  for (int i : dirs) payload += 8.0 * double(box_elems(i));
+  for (const kern::MoveDesc &m : ms) rows += double(m.n1) * m.n2 * m.n3;
+  r["read_lines_MB"] = rd / 1e6;
+  r["write_lines_MB"] = wr / 1e6;
+  r["payload_MB"] = payload / 1e6;
+  r["line_boxes"] = double(lb.size());
+  r["moves"] = double(ms.size());
+  r["pairs"] = double(std::count_if(ms.begin(), ms.end(), [](const kern::MoveDesc &m) { return m.pair; }));
+  r["lines_TBps_at_roof"] = (rd + wr) / (r["roof_us"] * 1e-6) / 1e12;
+  if (r.count("copy_roof_us")) r["lines_TBps_at_copy_roof"] = (rd + wr) / (r["copy_roof_us"] * 1e-6) / 1e12;
+  r["lines_TBps_at_move"] = (rd + wr) / (std::min(r["move_us"], r["move_us_again"]) * 1e-6) / 1e12;
+  init_grid(nullptr, gen_);
+  return r;
+}
+
+bool HaloExchange::move_pairs() {
+  static const bool on = [] {
+    const char *v = std::getenv("TZ_MOVE_PAIRS");
+    return !v || std::atoi(v) != 0;
+  }();
+  return on;
+}
+
+std::vector<kern::MoveDesc> HaloExchange::pair_x_moves(const std::vector<kern::MoveDesc> &ms) const {
+  // XYZQ, x self-wrap: the +x and -x moves of one (dy, dz) cover the same rows, one run at each
+  // end of the row. Moved by one lane per row, a row's ghost run and the source run beside it
+  // (one 128-B line when x = 0 sits at the row start, as in the reference's layout) are read
+  // and written while the line is in L2, instead of by two boxes far apart in time.
+  // partner[a] = b: move a (delta < 0) pairs with move b; the pair takes the earlier slot
+  std::vector<int> partner(ms.size(), -1);
+  std::vector<bool> taken(ms.size(), false);
+  for (size_t a = 0; a < ms.size(); ++a) {
+    const kern::MoveDesc &m = ms[a];
+    const int64_t delta = m.dst_off - m.src_off;
+    if (taken[a] || m.src != m.dst || m.len < 1 || m.len > kern::kMaxPairLen || delta >= 0) continue;
+    for (size_t b = 0; b < ms.size(); ++b) {
+      if (b == a || taken[b]) continue;
+      const kern::MoveDesc &q = ms[b];
+      if (q.src == m.src && q.dst == m.dst && q.len == m.len && q.n1 == m.n1 && q.n2 == m.n2 &&
+          q.n3 == m.n3 && q.s1 == m.s1 && q.s2 == m.s2 && q.s3 == m.s3 &&
+          q.src_off == m.src_off + m.len + delta && q.dst_off == m.src_off + m.len) {
+        partner[a] = int(b);
+        taken[a] = taken[b] = true;
+        break;
+      }
+    }
+  }
+  std::vector<kern::MoveDesc> out;
+  std::vector<bool> done(ms.size(), false);
+  for (size_t k = 0; k < ms.size(); ++k) {
+    if (done[k]) continue;
+    int a = -1;
+    if (partner[k] >= 0) a = int(k);
+    for (size_t j = 0; j < ms.size() && a < 0; ++j)
+      if (partner[j] == int(k)) a = int(j);
+    if (a < 0) {
+      out.push_back(ms[k]);
+      done[k] = true;
+      continue;
+    }
+    kern::MoveDesc p = ms[size_t(a)];
+    p.pair = true;
+    out.push_back(p);
+    done[size_t(a)] = done[size_t(partner[size_t(a)])] = true;
+  }
+  return out;
 }
 
 void HaloExchange::widen_to_sectors(int ghostDx, kern::MoveDesc &m) const {

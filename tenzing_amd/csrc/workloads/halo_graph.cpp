@@ -10,6 +10,57 @@ namespace {
 // byte-cost model for the simulator: ~5 TB/s effective HBM stream + launch latency
 double copy_cost_us(double bytes) { return 3.0 + bytes / 5.0e6; }
 
+// link-aware model (SimParams::link_model): the bytes of `dirs` (times `scale`) to each peer,
+// one transfer per peer by `engine`; `hbm`: plus the local reads of them
+std::vector<Traffic> to_peers(const HaloExchange &h, const std::vector<int> &dirs, const std::string &engine,
+                              double scale = 1.0, bool hbm = true) {
+  std::map<int, double> per;
+  double total = 0;
+  for (int i : dirs) {
+    const double b = scale * 8.0 * double(h.box_elems(i));
+    per[h.neighbor(i)] += b;
+    total += b;
+  }
+  std::vector<Traffic> t;
+  for (const auto &kv : per) t.push_back({"xgmi:" + std::to_string(kv.first), engine, kv.second});
+  if (hbm && total > 0) t.push_back({"hbm", "kernel", total});
+  return t;
+}
+std::vector<Traffic> local_hbm(double bytes) { return {{"hbm", "kernel", bytes}}; }
+double dirs_bytes(const HaloExchange &h, const std::vector<int> &dirs) {
+  double b = 0;
+  for (int i : dirs) b += 8.0 * double(h.box_elems(i));
+  return b;
+}
+
+// relay routing (2x2x2): the corner peer (all three axes differ) and the edge peers (two differ)
+int corner_peer(const HaloExchange &h) {
+  for (int i = 0; i < h.ndirs(); ++i) {
+    const auto d = h.dir(i);
+    if (d.dx && d.dy && d.dz) return h.neighbor(i);
+  }
+  return -1;
+}
+std::vector<int> edge_peers(const HaloExchange &h) {
+  std::vector<int> v;
+  for (int i = 0; i < h.ndirs(); ++i) {
+    const auto d = h.dir(i);
+    if ((d.dx != 0) + (d.dy != 0) + (d.dz != 0) == 2 &&
+        std::find(v.begin(), v.end(), h.neighbor(i)) == v.end())
+      v.push_back(h.neighbor(i));
+  }
+  return v;
+}
+// the direct part of a relayed / host-split exchange: (1 - frac) of every face, all the rest
+std::vector<Traffic> split_direct(const HaloExchange &h, const std::vector<int> &dirs,
+                                  const std::vector<int> &faces, double frac) {
+  std::vector<int> f, rest;
+  for (int i : dirs) (std::find(faces.begin(), faces.end(), i) != faces.end() ? f : rest).push_back(i);
+  std::vector<Traffic> t = to_peers(h, f, "put", 1.0 - frac);
+  for (const Traffic &x : to_peers(h, rest, "put")) t.push_back(x);
+  return t;
+}
+
 class HaloPack : public GpuOp {
 public:
   HaloPack(std::shared_ptr<const HaloExchange> h, int i) : h_(std::move(h)), i_(i) {}
@@ -17,6 +68,7 @@ public:
   std::string kind() const override { return "HaloPack"; }
   double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
   double cost_us() const override { return copy_cost_us(bytes()); }
+  std::vector<Traffic> traffic() const override { return local_hbm(bytes()); }
   void launch(void *s, Executor &) const override { h_->pack(i_, s); }
 
 private:
@@ -31,6 +83,7 @@ public:
   std::string kind() const override { return "HaloUnpack"; }
   double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
   double cost_us() const override { return copy_cost_us(bytes()); }
+  std::vector<Traffic> traffic() const override { return local_hbm(bytes()); }
   void launch(void *s, Executor &) const override { h_->unpack(i_, s); }
 
 private:
@@ -51,6 +104,13 @@ public:
   std::string order_domain() const override { return h_->uses_rccl() ? "rccl" : ""; }
   // RCCL inside hipGraphs only once the preflight verified it (else the runtime runs eagerly)
   bool capturable() const override { return !h_->uses_rccl() || h_->rccl_graph_ok(); }
+  std::vector<Traffic> traffic() const override {
+    if (!h_->uses_rccl()) return local_hbm(2.0 * bytes());
+    std::vector<Traffic> t = to_peers(*h_, {i_}, "rccl", 1.0, false);
+    t.push_back({"hbm", "kernel", 2.0 * bytes()}); // send buffer read, receive buffer written
+    return t;
+  }
+  double latency_us() const override { return h_->uses_rccl() ? 8.0 : 3.0; }
   void launch(void *s, Executor &ex) const override { h_->shift(i_, s, ex.stream_index(s)); }
 
 private:
@@ -66,6 +126,8 @@ public:
   std::string kind() const override { return "HaloDirect"; }
   double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
   double cost_us() const override { return copy_cost_us(bytes()); }
+  std::vector<Traffic> traffic() const override { return local_hbm(bytes()); }
+  double latency_us() const override { return 3.0; }
   void launch(void *s, Executor &) const override { h_->direct(i_, s); }
 
 private:
@@ -83,6 +145,7 @@ public:
   double bytes() const override { return 2.0 * 8.0 * double(h_->box_elems(i_)); }
   // peer stores over one xGMI link (~60 GB/s effective)
   double cost_us() const override { return 4.0 + bytes() / 2.0 / 6.0e4; }
+  std::vector<Traffic> traffic() const override { return to_peers(*h_, {i_}, cap_ ? "wide" : "put"); }
   void launch(void *s, Executor &) const override { h_->put_group({i_}, s, cap_); }
 
 private:
@@ -106,6 +169,7 @@ public:
     return 16.0 * cells * a.nq;
   }
   double cost_us() const override { return 3.0 + bytes() / 4.0e6; }
+  std::vector<Traffic> traffic() const override { return local_hbm(bytes()); }
   void launch(void *s, Executor &) const override { h_->stencil(region_, s); }
 
 private:
@@ -162,6 +226,28 @@ public:
   }
   std::string order_domain() const override { return st_ == Shift && h_->uses_rccl() ? "rccl" : ""; }
   bool capturable() const override { return !(st_ == Shift && h_->uses_rccl()) || h_->rccl_graph_ok(); }
+  std::vector<Traffic> traffic() const override {
+    switch (st_) {
+    case Shift:
+      if (!h_->uses_rccl()) return local_hbm(2.0 * bytes());
+      {
+        std::vector<Traffic> t = to_peers(*h_, dirs_, "rccl", 1.0, false);
+        t.push_back({"hbm", "kernel", 2.0 * bytes()});
+        return t;
+      }
+    case Put: return to_peers(*h_, dirs_, "put");
+    case WidePut: return to_peers(*h_, dirs_, "wide");
+    case CopyPut:
+    case MemcpyPut: {
+      // pack locally (read + write), then the copy engines move the buffer to each peer
+      std::vector<Traffic> t = to_peers(*h_, dirs_, st_ == CopyPut ? "sdma" : "memcpy", 1.0, false);
+      t.push_back({"hbm", "kernel", bytes()});
+      return t;
+    }
+    default: return local_hbm(bytes());
+    }
+  }
+  double latency_us() const override { return st_ == Shift && h_->uses_rccl() ? 10.0 : 4.0; }
   void launch(void *s, Executor &ex) const override {
     if (st_ == Pack) h_->pack_group(dirs_, s);
     else if (st_ == Shift) h_->shift_group(dirs_, s, ex.stream_index(s));
@@ -215,6 +301,28 @@ public:
     const double links = st_ == PutCorner ? 1.0 : 3.0;
     return 4.0 + bytes() / links / 6.0e4;
   }
+  std::vector<Traffic> traffic() const override {
+    const double shared = frac_ * dirs_bytes(*h_, faces_);
+    switch (st_) {
+    case PutDirect: return split_direct(*h_, dirs_, faces_, frac_);
+    case PutCorner: {
+      const int c = corner_peer(*h_);
+      return {{"xgmi:" + std::to_string(c), "put", shared}, {"hbm", "kernel", shared}};
+    }
+    case Forward:
+    case ForwardCopy: {
+      // as the corner of other ranks: their shares on to their face neighbours, my edge peers
+      const std::vector<int> e = edge_peers(*h_);
+      std::vector<Traffic> t;
+      for (int q : e)
+        t.push_back({"xgmi:" + std::to_string(q), st_ == Forward ? "put" : "sdma", shared / double(e.size())});
+      t.push_back({"hbm", "kernel", shared});
+      return t;
+    }
+    case Unpack: return local_hbm(bytes());
+    default: return {};
+    }
+  }
   void launch(void *s, Executor &) const override {
     switch (st_) {
     case PutDirect: h_->relay_put_direct(dirs_, frac_, s); break;
@@ -264,6 +372,15 @@ public:
     if (st_ == Wait) return 3.0;
     if (st_ == Unpack) return copy_cost_us(bytes()) + frac_ * 2.0 * bytes() / 4.0e4;
     return 4.0 + bytes() / (st_ == PutHost ? 4.0e4 : 3.0 * 6.0e4);
+  }
+  std::vector<Traffic> traffic() const override {
+    const double shared = frac_ * dirs_bytes(*h_, faces_);
+    switch (st_) {
+    case PutDirect: return split_direct(*h_, dirs_, faces_, frac_);
+    case PutHost: return {{"pcie", "host", shared}, {"hbm", "kernel", shared}};
+    case Unpack: return {{"hbm", "kernel", bytes()}, {"pcie", "sdma", shared}};
+    default: return {};
+    }
   }
   void launch(void *s, Executor &) const override {
     switch (st_) {

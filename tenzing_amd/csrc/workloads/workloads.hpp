@@ -441,6 +441,12 @@ public:
   /// direct transport: move the interior slab facing each direction of `dirs` straight into
   /// the neighbour's ghost region on the opposite side (one launch)
   void direct_group(const std::vector<int> &dirs, void *stream) const;
+  /// the moves of direct_group (order, widening, row pairs), not launched
+  std::vector<kern::MoveDesc> direct_moves(const std::vector<int> &dirs) const;
+  /// the fused direct move of every self direction against its shape-matched roof (a kernel
+  /// touching exactly the same 128-B lines with whole-line accesses): microseconds per launch
+  /// of both, the lines read / written (MB) and the payload; re-initializes the grid
+  std::map<std::string, double> move_roof(int iters);
   void direct(int i, void *stream) const { direct_group({i}, stream); }
 
 private:
@@ -562,6 +568,10 @@ private:
   unsigned long long *peer_slot(int rank, int set, int i) const;
   std::vector<unsigned long long *> credit_ptrs(const std::vector<int> &dirs) const;
   const RcclComm &comm_for(int streamIdx, int dir) const;
+  /// XYZQ direct moves: the +x / -x moves of one (dy, dz) as one row-pair move (env
+  /// TZ_MOVE_PAIRS=0: off)
+  std::vector<kern::MoveDesc> pair_x_moves(const std::vector<kern::MoveDesc> &ms) const;
+  static bool move_pairs();
   void widen_to_sectors(int ghostDx, kern::MoveDesc &m) const;
   static constexpr int kDefaultComms = 4;
   bool ipcGrid_ = true;

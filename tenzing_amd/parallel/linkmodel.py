@@ -1,0 +1,114 @@
+"""Link-aware cost model of the multi-GPU halo exchange, for hardware-free searches.
+
+The discrete-event simulator (``SimBenchmarker`` with ``SimParams.link_model``) times a GPU op
+that reports its traffic (``GpuOp.traffic()``: bytes per shared resource and engine) as its
+fixed latency plus, over its resources, the longest ``bytes / rate``, where ``rate`` is the
+engine's own rate capped by the resource's capacity shared with the transfers already active
+on it. The halo ops report per-peer xGMI bytes (kernel puts, wide puts, copy engines, RCCL,
+relay hops through the corner peer), PCIe bytes (host split) and local HBM bytes.
+
+``link_sim_params`` fills the rates from what a multi-GPU bench run measured (its
+``link_probe`` and ``link_matrix`` fields), so that a search over recorded link rates runs on a
+CPU. ``headline_graph`` builds the bench's N-rank tree for one rank without a GPU, and
+``transport_seeds`` the bench's one-schedule-per-transport seeds.
+
+Reference: tenzing-mcts replays recorded timings without hardware (CsvBenchmarker,
+src/benchmarker.cpp:169-223); the MCTS loop is tenzing-mcts/include/tenzing/mcts/mcts.hpp:154-326.
+"""
+from __future__ import annotations
+
+from .. import _tz
+
+# xGMI: 7 links of ~153 GB/s peak per direction per MI355X; what one transfer reaches depends on
+# the engine (CU stores at the default / wide workgroup count, SDMA, RCCL)
+DEFAULT_ENGINE_GBPS = {"kernel": 5000.0, "put": 60.0, "wide": 90.0, "sdma": 50.0, "memcpy": 50.0,
+                       "rccl": 50.0, "host": 40.0}
+DEFAULT_RESOURCE_GBPS = {"hbm": 5000.0, "xgmi": 120.0, "pcie": 50.0}
+
+
+def link_sim_params(probe: dict | None = None, matrix: dict | None = None, noise: float = 0.0,
+                    seed: int = 0, **engine_overrides) -> "_tz.SimParams":
+    """SimParams with the link-aware model on. ``probe``: a bench record's ``link_probe`` (one
+    transfer's GB/s per transport over one link, and both faces of an axis at once, which
+    bounds the link's capacity); ``matrix``: its ``link_matrix`` (every ordered pair, all ranks
+    sending at once: per-link capacities ``xgmi:<peer>`` of rank 0's links). Missing fields keep
+    the defaults; ``engine_overrides`` (e.g. ``put=70``) win over both."""
+    p = _tz.SimParams()
+    p.link_model = True
+    p.noise = noise
+    p.seed = seed
+    eng = dict(DEFAULT_ENGINE_GBPS)
+    res = dict(DEFAULT_RESOURCE_GBPS)
+    if probe:
+        rates = probe.get("GBps") or {}
+        for key, name in (("put", "put"), ("put_wide", "wide"), ("sdma", "sdma"),
+                          ("memcpy", "memcpy"), ("rccl", "rccl")):
+            if rates.get(key):
+                eng[name] = float(rates[key])
+        pair = [v for v in (probe.get("pair_GBps") or {}).values() if v]
+        if pair:  # both faces of one axis at once over the same link: at least this much
+            res["xgmi"] = max(res["xgmi"], float(max(pair)))
+    if matrix and matrix.get("put_GBps") and not matrix.get("why"):
+        row = matrix["put_GBps"][0]
+        for q, v in enumerate(row):
+            if v and v > 0:
+                res[f"xgmi:{q}"] = max(float(v), eng["put"])
+    eng.update({k: float(v) for k, v in engine_overrides.items()})
+    p.engine_GBps = eng
+    p.resource_GBps = res
+    return p
+
+
+def headline_graph(rank: int, size: int, n: int = 512, neighbors: int = 26, order: str = "qxyz",
+                   wide_puts: str = "on", relay: str = "auto", hostsplit: str = "auto"):
+    """(halo, graph) of one rank of the bench's N-rank tree, built without a GPU: every remote
+    transport offered (RCCL, kernel / wide / copy-engine puts, their mix, relays, host split)
+    as the top-level ChoiceOp, per-direction or fused groups below it. Set TZ_IPC_GRID=0 first
+    for the receive-buffer transports (copy engines, relay, host split)."""
+    from ..models import HaloConfig
+
+    cfg = HaloConfig(n=n, neighbors=neighbors, order=order, fuse="choice", transport="auto",
+                     wide_puts=wide_puts, relay=relay, hostsplit=hostsplit)
+    h = _tz.HaloExchange(cfg.args(rank, size, -1))
+    g = _tz.Graph()
+    h.add_to_graph(g)
+    return h, g
+
+
+def transport_seeds(graph, platform, streams: int):
+    """The bench's seeds (bench.py, --seed-transports): one greedy schedule per remote transport
+    of the ``he_remote`` choice, every group fused, direct (self) moves on stream 1."""
+    from ..search import choice_alternatives, greedy_schedule
+
+    seeds, alts = [], []
+    for alt in choice_alternatives(graph, "he_remote"):
+        try:
+            seeds.append(greedy_schedule(
+                graph, platform, {"he_remote": alt, "*": ["allfused", "fused"]},
+                stream_for=lambda n: 1 if n.startswith("he_direct") and streams > 1 else 0))
+            alts.append(alt)
+        except RuntimeError:
+            continue
+    return seeds, alts
+
+
+def tree_stats(graph, platform, rollouts: int = 50, seed: int = 0) -> dict:
+    """Size of the decision tree: decisions per complete schedule and the mean / max number of
+    alternatives at each step, over random rollouts."""
+    import random
+
+    rng = random.Random(seed)
+    depths, widths = [], []
+    for _ in range(rollouts):
+        st = _tz.State(graph, platform)
+        d = 0
+        while not st.complete():
+            ds = st.get_decisions()
+            widths.append(len(ds))
+            st = st.apply(ds[rng.randrange(len(ds))])
+            d += 1
+        depths.append(d)
+    log10 = sum(__import__("math").log10(w) for w in widths) / max(1, len(depths))
+    return {"rollouts": rollouts, "depth_mean": sum(depths) / len(depths), "depth_max": max(depths),
+            "branching_mean": sum(widths) / len(widths), "branching_max": max(widths),
+            "log10_paths_per_rollout": round(log10, 1)}

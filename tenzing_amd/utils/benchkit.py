@@ -71,11 +71,13 @@ def branch_probe(tz, rt, branches: int = 3, us: float = 50.0, iters: int = 10):
             "all_us": round(many, 1), "ratio": round(many / one, 3)}
 
 
-def choose_pad(make_rt, probe, pads, threshold: float = 1.5):
+def choose_pad(make_rt, probe, pads, threshold: float = 1.5, margin: float = 0.9):
     """Runtime whose graph branches run concurrently: ``make_rt(pad)`` builds a runtime with that
     stream padding (None: the default), ``probe(rt)`` returns its branch probe (a dict with
     ``ratio``, or None). The first padding whose ratio is at most ``threshold`` is kept;
-    otherwise the one with the lowest ratio (built again if it is not the last one probed).
+    otherwise the one with the lowest ratio if that is below ``margin`` times the first
+    padding's (a clear gain, not probe noise), else the first (built again if it is not the last
+    one probed).
 
     Returns (runtime, record); the record lists every probe in order and the padding chosen."""
     tried = []
@@ -96,6 +98,9 @@ def choose_pad(make_rt, probe, pads, threshold: float = 1.5):
     if best is None:  # the probe could not run at all: keep the last runtime, say so
         return rt, {"pad_streams": tried[-1]["pad_streams"] if tried else None,
                     "serialized": None, "tried": tried, "threshold": threshold}
+    first = tried[0]["probe"]["ratio"] if tried[0]["probe"] else None
+    if first is not None and best[0] > margin * first:  # no padding is clearly better
+        best = (first, pads[0], tried[0]["pad_streams"])
     if best[1] != pads[-1]:
         rt = None
         rt = make_rt(best[1])
@@ -132,11 +137,13 @@ def timed_replay(tz, rt, ctrl, seq, mode, steps: int, warmup: int):
 def search_record(tz, ctrl, rt, graph, streams: int, verify, steps: int, warmup: int,
                   mcts_iters: int = 40, bench_iters: int = 6, target_secs: float = 0.002,
                   search_unroll: int = 10, graph_unroll: int = 20, seed: int = 0,
-                  time_budget_s: float = 30.0, strategy: str = "FastMin", rerank: int = 4):
+                  time_budget_s: float = 30.0, strategy: str = "FastMin", rerank: int = 4,
+                  seeds=()):
     """Search ``graph`` briefly (MCTS, hipGraph candidates, racing and settling as the headline),
     re-rank the ``rerank`` best distinct candidates interleaved, verify the winner with
     ``verify(seq) -> bad count`` (the next finalist if it fails), then time it eagerly and as a
-    hipGraph exactly as the headline is timed. Returns the sub-record dict."""
+    hipGraph exactly as the headline is timed. ``seeds``: schedules measured before the search
+    (they count as results). Returns the sub-record dict."""
     t_start = time.time()
     plat = tz.Platform(streams)
     rt.set_mode(tz.ExecMode.Graph)
@@ -149,9 +156,11 @@ def search_record(tz, ctrl, rt, graph, streams: int, verify, steps: int, warmup:
     o.seed = seed
     o.bench = tz.BenchOpts(n_iters=bench_iters, max_retries=3, target_secs=target_secs,
                            race_ratio=1.25, settle_ratio=0.03)
+    if seeds and ctrl.rank == 0:
+        o.seed_schedules = list(seeds)
     res = tz.mcts_explore(graph, plat, bench, ctrl, o)
     rec = {"mcts_candidates": len(res.sims), "mcts_skipped": res.failed,
-           "search_wall_s": round(res.wall_s, 3)}
+           "search_wall_s": round(res.wall_s, 3), "seeded": len(seeds)}
     if not res.sims:
         rec["error"] = "the search measured no candidate"
         return rec

@@ -45,9 +45,18 @@ def test_choose_pad_retries_until_a_padding_runs_branches_at_once():
 def test_choose_pad_falls_back_to_the_least_serialized():
     FakeRt.made = []
     rt, rec = choose_pad(FakeRt, fake_probe({6: 2.0, 8: 1.7, 12: 1.9, 4: 2.1}), [None, 8, 12, 4])
-    # none within the threshold: the lowest ratio (8) is rebuilt and recorded as serialized
+    # none within the threshold: the lowest ratio (8, clearly below the default's) is rebuilt
+    # and recorded as serialized
     assert rt.pad_streams == 8 and rec["pad_streams"] == 8 and rec["serialized"] is True
     assert FakeRt.made == [6, 8, 12, 4, 8]
+
+
+def test_choose_pad_keeps_the_default_when_no_padding_is_clearly_better():
+    """every padding serializes alike (probe noise apart): the default stays"""
+    FakeRt.made = []
+    rt, rec = choose_pad(FakeRt, fake_probe({6: 1.67, 8: 1.634, 12: 1.629, 4: 1.637}), [None, 8, 12, 4])
+    assert rt.pad_streams == 6 and rec["serialized"] is True
+    assert FakeRt.made == [6, 8, 12, 4, 6]
 
 
 def test_choose_pad_when_the_probe_cannot_run():

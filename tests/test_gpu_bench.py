@@ -33,7 +33,9 @@ def test_bench_one_rank_subrecords(gpu):
     bp = j["graph_branch_probe"]
     assert bp["tried"] and bp["tried"][0]["probe"]["ratio"] > 0, bp
     assert j["pad_streams"] == bp["pad_streams"]
-    assert j["post_timing"]["done"] == ["reference_layout", "baseline_configs"]
+    assert j["post_timing"]["done"] == ["move_roof", "reference_layout", "baseline_configs"]
+    for roof in (j["move_roof"], j["reference_layout"]["move_roof"]):
+        assert roof["move_us"] > 0 and roof["roof_us"] > 0 and roof["read_lines_MB"] > 0, roof
     ref = j["reference_layout"]
     assert "error" not in ref, ref
     assert ref["verified_bad"] == 0 and ref["verified_bad_after_timing"] == 0
@@ -41,6 +43,8 @@ def test_bench_one_rank_subrecords(gpu):
     lay = ref["config"]["layout"]
     # the reference's storage: x = 0 at the row start, rows padded to 128 B (64 + 6 -> 80)
     assert lay["order"] == "xyzq" and lay["x_offset_cells"] == 0 and lay["row_pitch_elems"] == 80
+    # the x faces of one row moved together (their ghost and source runs share a line)
+    assert ref["move_roof"]["pairs"] == 1
     for name in ("spmv_c2", "fused_c5"):
         rec = j["baseline_configs"][name]
         assert "error" not in rec, rec

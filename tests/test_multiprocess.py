@@ -309,3 +309,67 @@ def test_racing_is_collective(tmp_path):
 def test_bad_seed_schedule_fails_on_every_rank(tmp_path):
     rs = _run("body_bad_seed", 2, tmp_path)
     assert all("race" in r["err"] for r in rs), rs
+
+
+def body_headline_sim(overrides=None):
+    """the bench's 8-rank headline tree (2x2x2, 26 neighbours, 4 streams, every remote transport
+    offered) searched by 8 CPU ranks under the link-aware cost model: every rank simulates its
+    own graph's copy of each candidate, the result is the max over ranks"""
+    os.environ["TZ_IPC_GRID"] = "0"  # receive buffers: copy engines, relays, host split offered
+    import time
+
+    import tenzing_amd as tz
+    from tenzing_amd.parallel import init_ctrl
+    from tenzing_amd.parallel.linkmodel import (headline_graph, link_sim_params, transport_seeds,
+                                                tree_stats)
+
+    c = init_ctrl(timeout_s=120)
+    h, g = headline_graph(c.rank, c.size)
+    plat = tz.Platform(4)
+    seeds, alts = transport_seeds(g, plat, 4)
+    out = {"rank": c.rank, "alternatives": alts}
+    for name, iters, strategy in (("fastmin120", 120, "FastMin"), ("coverage120", 120, "Coverage"),
+                                  ("fastmin2000", 2000, "FastMin")):
+        o = tz.MctsOpts()
+        o.n_iters = iters
+        o.strategy = strategy
+        o.seed = 0
+        o.bench = tz.BenchOpts(n_iters=6, max_retries=1, target_secs=0.002)
+        if c.rank == 0:
+            o.seed_schedules = seeds
+        t0 = time.time()
+        r = tz.mcts_explore(g, plat, tz.SimBenchmarker(4, link_sim_params(**(overrides or {})), c), c, o)
+        if c.rank == 0:
+            b = r.sims[r.best()]
+            names = [x.name for x in b.seq.ops()]
+            out[name] = {"best_us": b.res.pct10 * 1e6, "tree_nodes": r.tree_size,
+                         "candidates": len(r.sims), "wall_s": time.time() - t0,
+                         "best_remote": sorted({n.split("_")[1] for n in names
+                                                if n.startswith("he_") and not n.startswith("he_direct")}),
+                         "seeded_best_us": min(s.res.pct10 for s in r.sims if s.seeded) * 1e6}
+    if c.rank == 0:
+        out["tree"] = tree_stats(g, plat, 40)
+    return out
+
+
+def body_headline_sim_fast_engines():
+    # copy engines and RCCL fast, kernel puts slow: another transport wins
+    return body_headline_sim(dict(sdma=110, memcpy=110, rccl=100, put=35, wide=45))
+
+
+@pytest.mark.parametrize("model", ["default", "fast_engines"])
+def test_solver_converges_at_the_8_rank_headline_tree(tmp_path, model):
+    """with the bench's seeds and 120 iterations, FastMin and Coverage land
+    within 5 % of the best schedule a 2,000-iteration search finds on the same model, and the
+    search improves on the best seeded (one per transport, greedy streams) schedule"""
+    rs = _run("body_headline_sim" + ("" if model == "default" else "_fast_engines"), 8, tmp_path)
+    r0 = rs[0]
+    ref = r0["fastmin2000"]["best_us"]
+    report = {k: r0[k] for k in ("fastmin120", "coverage120", "fastmin2000", "tree")}
+    print(json.dumps(report))
+    assert len(r0["alternatives"]) >= 10, r0["alternatives"]
+    for k in ("fastmin120", "coverage120"):
+        assert r0[k]["best_us"] <= 1.05 * ref, report
+        assert r0[k]["best_us"] <= r0[k]["seeded_best_us"], report
+    assert r0["fastmin2000"]["tree_nodes"] > r0["fastmin120"]["tree_nodes"]
+    assert r0["tree"]["branching_mean"] > 2 and r0["tree"]["depth_mean"] > 20, report

@@ -335,3 +335,77 @@ def test_seed_schedules_join_the_tree(tz, which, streams):
     # every distinct seed found its path (equal seeds share one result and one path)
     distinct = len({s.canonical_key() for s in seeds})
     assert r.counter_counts()["SEED_IN_TREE"] >= distinct
+
+
+def test_link_model_shares_a_resource_and_overlaps_separate_ones(tz):
+    """the link-aware simulator: two transfers over one link on two streams share its capacity,
+    two over different links overlap fully, and an engine caps what one transfer gets"""
+    from tenzing_amd.parallel.linkmodel import link_sim_params
+
+    p = link_sim_params(put=100)
+    p.resource_GBps = {"hbm": 5000.0, "xgmi": 100.0, "pcie": 50.0}
+    mb = 10e6  # 10 MB at 100 GB/s: 100 us
+
+    def sim(peers):
+        g = tz.Graph()
+        for i, q in enumerate(peers):
+            op = tz.SimGpuOp(f"t{i}", 0.0, traffic=[(f"xgmi:{q}", "put", mb)])
+            g.start_then(op)
+            g.then_finish(op)
+        from tenzing_amd.search import greedy_schedule
+
+        seq = greedy_schedule(g, tz.Platform(2, symmetric_streams=False),
+                              stream_for=lambda n: int(n[1:]))
+        ex = tz.SimExecutor(2, p)
+        ex.run_once(seq)
+        return {n: t1 - t0 for n, s, t0, t1 in ex.trace()}
+
+    one = sim([1])
+    assert abs(one["t0"] - 100.0) < 1.0
+    apart = sim([1, 2])  # different links: both at the full rate
+    assert all(abs(d - 100.0) < 1.0 for d in apart.values()), apart
+    shared = sim([1, 1])  # the same link: the second starts while the first is active
+    assert max(shared.values()) > 150.0, shared
+    p.engine_GBps = dict(p.engine_GBps, put=50.0)  # the engine, not the link, limits
+    assert abs(sim([1])["t0"] - 200.0) < 1.0
+
+
+def test_link_sim_params_from_a_bench_record(tz):
+    from tenzing_amd.parallel.linkmodel import link_sim_params
+
+    probe = {"GBps": {"put": 70.0, "put_wide": 95.0, "sdma": 48.0, "memcpy": None},
+             "pair_GBps": {"put": 130.0, "mixed": 140.0}}
+    matrix = {"why": "", "put_GBps": [[-1, 80.0, 75.0], [80.0, -1, 79.0], [74.0, 78.0, -1]]}
+    p = link_sim_params(probe, matrix, rccl=60)
+    assert p.link_model
+    e, r = p.engine_GBps, p.resource_GBps
+    assert e["put"] == 70.0 and e["wide"] == 95.0 and e["sdma"] == 48.0 and e["rccl"] == 60
+    assert e["memcpy"] == 50.0  # not measured: the default stays
+    assert r["xgmi"] == 140.0 and r["xgmi:1"] == 80.0 and r["xgmi:2"] == 75.0
+
+
+def test_halo_ops_report_per_peer_traffic(tz, monkeypatch):
+    """every rank's halo ops say which peer links their bytes cross (the link model's input)"""
+    monkeypatch.setenv("TZ_IPC_GRID", "0")
+    from tenzing_amd.parallel.linkmodel import headline_graph
+
+    h, g = headline_graph(0, 8, n=64)
+    seen = {}
+
+    def visit(op):
+        if op.name in seen:
+            return
+        seen[op.name] = op.traffic() if hasattr(op, "traffic") else None
+        for c in (op.choices() if hasattr(op, "choices") else []):
+            visit(c)
+        if hasattr(op, "graph"):
+            for v in op.graph().vertices():
+                visit(op.graph().op(v))
+    for v in g.vertices():
+        visit(g.op(v))
+    put = seen["he_put_all"]
+    peers = {res for res, eng, b in put if res.startswith("xgmi:")}
+    assert len(peers) == 7 and all(eng == "put" for res, eng, b in put if res.startswith("xgmi:"))
+    total = sum(b for res, eng, b in put if res.startswith("xgmi:"))
+    assert abs(total - h.exchange_bytes()) < 1.0
+    assert {e for r, e, b in seen["he_copyput_all"] if r.startswith("xgmi")} == {"sdma"}
