@@ -176,14 +176,14 @@ def main() -> int:
     # per candidate: 6 measurements of >= 2 ms each; the 4 best are re-measured interleaved
     # (--rerank) before the final timing. 20 x 4 ms, 10 x 3 ms, 8 x 2 ms and 5 x 1.5 ms all find
     # the same best schedule; 6 x 2 ms halves the search wall-clock of 10 x 3 ms
-    # (profiles/r1_search_len/)
+    # (profiles/archive/r1_search_len/)
     ap.add_argument("--bench-iters", type=int, default=6)
     ap.add_argument("--target-secs", type=float, default=0.002)
     ap.add_argument("--race-ratio", type=float, default=1.25,
                     help="stop measuring a candidate once race-min measurements are all slower "
                          "than this times the best so far (0 = measure every candidate fully)")
     # settling: a candidate whose first 4 measurements agree within 3 % is measured enough
-    # (search 0.62-0.68 -> 0.53-0.57 s, same best schedule and timed value, profiles/r2_settle/)
+    # (search 0.62-0.68 -> 0.53-0.57 s, same best schedule and timed value, profiles/archive/r2_settle/)
     ap.add_argument("--settle-ratio", type=float, default=0.03,
                     help="stop measuring a candidate once its first 4 measurements agree within "
                          "this ratio (0 = off)")
@@ -191,7 +191,7 @@ def main() -> int:
     ap.add_argument("--search-mode", default="graph", choices=["eager", "graph"],
                     help="benchmark candidates eagerly or compiled to hipGraphs (default: graph, "
                          "the way the final number is measured; eager rankings can mislead, "
-                         "profiles/r1_bench_loopback/)")
+                         "profiles/archive/r1_bench_loopback/)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--seed-transports", type=int, default=1,
                     help="several ranks: measure one fused schedule per remote transport before "

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--unrolls", default="",
                     help="comma list: sweep items per lane (grid sizing) at the default nt "
                          "settings instead of the round-1 grid (1-2: more workgroups, one item "
-                         "in flight; the direct move gained 1.2 %% that way, profiles/r2_move_shape/)")
+                         "in flight; the direct move gained 1.2 %% that way, profiles/archive/r2_move_shape/)")
     a = ap.parse_args()
     torch.zeros(1, device="cuda")
     h, _ = build_halo(HaloConfig(n=a.n, neighbors=26, order=a.order, transport="copy"),

@@ -1073,6 +1073,7 @@ PYBIND11_MODULE(_tz, m) {
       .def(py::init<>())
       .def_readwrite("matrix", &SpmvArgs::matrix)
       .def_readwrite("m", &SpmvArgs::m)
+      .def_readwrite("distribute", &SpmvArgs::distribute)
       .def_readwrite("bw", &SpmvArgs::bw)
       .def_readwrite("nnz", &SpmvArgs::nnz)
       .def_readonly("nnz_actual", &SpmvArgs::nnz_actual)
@@ -1088,7 +1089,10 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("prefix", &SpmvArgs::prefix)
       .def("json", [](const SpmvArgs &a) { return a.json().dump(); });
   py::class_<DistSpmv, std::shared_ptr<DistSpmv>>(m, "DistSpmv")
-      .def(py::init([](const SpmvArgs &a) { return std::make_shared<DistSpmv>(a); }))
+      .def(py::init([](const SpmvArgs &a, Ctrl *c) {
+             py::gil_scoped_release r; // collective with "root" distribution
+             return std::make_shared<DistSpmv>(a, c);
+           }), py::arg("args"), py::arg("ctrl") = nullptr)
       .def_property_readonly("args", &DistSpmv::args)
       .def("local_rows", &DistSpmv::local_rows)
       .def("local_nnz", &DistSpmv::local_nnz)

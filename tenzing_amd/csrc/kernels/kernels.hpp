@@ -28,13 +28,13 @@ constexpr int kMaxBoxes = 32;
 struct BoxTuning {
   // pack / unpack: items per lane the grid is sized for; 4 or 8 keep that many loads in flight,
   // 1-3 keep one in flight. 3 packs and unpacks 2 % faster than 4 in pipeline context
-  // (scripts/ktune.py --unrolls, profiles/r2_move_shape/ktune_unrolls*.jsonl); 8 is slower
+  // (scripts/ktune.py --unrolls, profiles/archive/r2_move_shape/ktune_unrolls*.jsonl); 8 is slower
   int unroll = 3;
   bool nt_pack = true;    // non-temporal grid loads in pack: -27 % pack time in pipeline context
   // non-temporal ghost stores in unpack: the ghosts are not read again within the exchange.
   // Round 1 measured +5 % on the one-rank pack -> copy -> unpack chain; the receive-buffer
   // unpack of the multi-rank exchange gains 7-8 % (2 loopback ranks, 0.228-0.239 -> 0.210-0.218
-  // ms, scripts/nt_multi_ab.sh, profiles/r2_nt/)
+  // ms, scripts/nt_multi_ab.sh, profiles/archive/r2_nt/)
   bool nt_unpack = true;
   int max_blocks = 4096;  // cap per box (grid-stride beyond)
   // cap per box of the signalling put kernels, whose stores cross xGMI (env
@@ -53,7 +53,7 @@ struct BoxTuning {
   // items per lane the grid is sized for (>= in flight; the lane loops over them). One in
   // flight, two per lane (twice the workgroups of 4 x 4) moves the 26 directions at 512^3 x 3
   // in 43.5 us against 44.1 us, the best of 10 shapes (scripts/move_ab.py --blocks,
-  // profiles/r2_move_shape/)
+  // profiles/archive/r2_move_shape/)
   int move_unroll = 1;
   int move_items = 2;
   int xcd_remap = 0; // box_move block order: 0 round-robin, 1 one contiguous range per XCD,
@@ -222,7 +222,7 @@ struct StencilBox {
 struct StencilTuning {
   int ty = 16; // 64 x 16 tiles (scripts/stencil_bench.py)
   // 16-plane chunks: 4x the workgroups of 64-plane chunks for two extra planes read per chunk;
-  // 1580 vs 1620 us at 512^3 x 3 (profiles/r2_move_shape/stencil_zc.jsonl)
+  // 1580 vs 1620 us at 512^3 x 3 (profiles/archive/r2_move_shape/stencil_zc.jsonl)
   int zc = 16;
   int pf = 1;  // planes in flight beyond z + 1 (1 or 2)
   bool db = true; // double-buffered LDS tile (one barrier per plane instead of two)

@@ -281,7 +281,8 @@ int main(int argc, char **argv) {
       s.form = opt("spmv-form", "choice");
       s.transport = opt("spmv-transport", "auto");
       s.library = opt("spmv-library", "adaptive");
-      spmv = std::make_shared<DistSpmv>(s);
+      s.distribute = opt("spmv-distribute", "auto");
+      spmv = std::make_shared<DistSpmv>(s, ctrl.get());
       if (!sim) spmv->setup(ctrl.get());
       spmv->add_to_graph(*g);
     }

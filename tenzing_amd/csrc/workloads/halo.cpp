@@ -864,7 +864,7 @@ std::vector<kern::MoveDesc> HaloExchange::direct_moves(const std::vector<int> &d
   // faces first, then edges, then corners: blocks are dispatched box by box in batch order,
   // and leaving the many small edge/corner boxes for the last waves measured best (fused
   // 26-direction move 44.13 us vs 44.23 in the natural order and 45.18 with the small boxes
-  // first; scripts/box_order_ab.py, profiles/r2_box_order/)
+  // first; scripts/box_order_ab.py, profiles/archive/r2_box_order/)
   std::vector<int> dirs = dirs_in;
   std::stable_sort(dirs.begin(), dirs.end(), [&](int a, int b) {
     auto k = [&](int i) { return (dirs_[i].dx != 0) + (dirs_[i].dy != 0) + (dirs_[i].dz != 0); };

@@ -36,6 +36,7 @@ Json SpmvArgs::json() const {
   j["library"] = library;
   j["transport"] = transport;
   j["matrix"] = matrix;
+  j["distribute"] = distribute;
   return j;
 }
 
@@ -306,8 +307,39 @@ private:
 
 } // namespace
 
-DistSpmv::DistSpmv(SpmvArgs a) : a_(std::move(a)) {
-  TZ_CHECK(a_.size >= 1 && a_.rank >= 0 && a_.rank < a_.size, "bad rank/size");
+namespace {
+// (de)serialization of plain arrays for the setup messages
+template <typename T> void put_vec(std::string &s, const std::vector<T> &v) {
+  const uint64_t n = v.size();
+  s.append(reinterpret_cast<const char *>(&n), sizeof(n));
+  if (n) s.append(reinterpret_cast<const char *>(v.data()), n * sizeof(T));
+}
+template <typename T> std::vector<T> get_vec(const std::string &s, size_t &at) {
+  uint64_t n = 0;
+  TZ_CHECK(at + sizeof(n) <= s.size(), "spmv setup message truncated");
+  std::memcpy(&n, s.data() + at, sizeof(n));
+  at += sizeof(n);
+  TZ_CHECK(at + n * sizeof(T) <= s.size(), "spmv setup message truncated");
+  std::vector<T> v(n);
+  if (n) std::memcpy(v.data(), s.data() + at, n * sizeof(T));
+  at += n * sizeof(T);
+  return v;
+}
+// rows [r0, r1) of A as a CSR of their own (row pointers from 0, global columns)
+CsrHost row_block(const CsrHost &A, int64_t r0, int64_t r1) {
+  CsrHost B;
+  B.rows = r1 - r0;
+  B.cols = A.cols;
+  B.rowPtr.assign(size_t(B.rows + 1), 0);
+  const int32_t base = A.rowPtr[size_t(r0)];
+  for (int64_t r = r0; r <= r1; ++r) B.rowPtr[size_t(r - r0)] = A.rowPtr[size_t(r)] - base;
+  B.colInd.assign(A.colInd.begin() + base, A.colInd.begin() + A.rowPtr[size_t(r1)]);
+  B.val.assign(A.val.begin() + base, A.val.begin() + A.rowPtr[size_t(r1)]);
+  return B;
+}
+} // namespace
+
+CsrHost DistSpmv::build_matrix() {
   CsrHost A;
   if (!a_.matrix.empty()) {
     A = read_matrix_market(a_.matrix);
@@ -322,15 +354,98 @@ DistSpmv::DistSpmv(SpmvArgs a) : a_(std::move(a)) {
     A = random_band_matrix(a_.m, a_.bw, a_.nnz, a_.seed);
   }
   a_.nnz_actual = A.nnz();
+  return A;
+}
+
+DistSpmv::DistSpmv(SpmvArgs a, Ctrl *ctrl) : a_(std::move(a)) {
+  TZ_CHECK(a_.size >= 1 && a_.rank >= 0 && a_.rank < a_.size, "bad rank/size");
+  TZ_CHECK(a_.distribute == "local" || a_.distribute == "root" || a_.distribute == "auto",
+           "SpMV distribute must be local, root or auto (got " << a_.distribute << ")");
+  if (a_.distribute == "auto") a_.distribute = ctrl && a_.size > 1 ? "root" : "local";
+  const bool root = a_.distribute == "root" && a_.size > 1;
+  TZ_CHECK(!root || (ctrl && ctrl->size() == a_.size && ctrl->rank() == a_.rank),
+           "SpMV root distribution needs the control plane of its " << a_.size << " ranks");
+  CsrHost mine; // my rows, global columns
+  // needFrom[q]: the global columns of mine that rank q's rows use (what I send q, in q's order)
+  std::vector<std::vector<int64_t>> needFrom(size_t(a_.size));
+  if (!root) {
+    // every rank derives the same matrix and every plan itself (no setup communication)
+    const CsrHost A = build_matrix();
+    TZ_CHECK(a_.m >= a_.size, "fewer matrix rows (" << a_.m << ") than ranks (" << a_.size << ")");
+    std::tie(r0_, r1_) = row_partition(a_.m, a_.rank, a_.size);
+    mine = row_block(A, r0_, r1_);
+    for (int q = 0; q < a_.size; ++q) {
+      if (q == a_.rank) continue;
+      auto [q0, q1] = row_partition(a_.m, q, a_.size);
+      std::vector<int64_t> &need = needFrom[size_t(q)];
+      for (int64_t r = q0; r < q1; ++r)
+        for (int32_t j = A.rowPtr[r]; j < A.rowPtr[r + 1]; ++j)
+          if (A.colInd[j] >= r0_ && A.colInd[j] < r1_) need.push_back(A.colInd[j]);
+      std::sort(need.begin(), need.end());
+      need.erase(std::unique(need.begin(), need.end()), need.end());
+    }
+  } else {
+    // the reference's setup (include/tenzing/spmv/row_part_spmv.cuh:24-90, :322-403): rank 0
+    // builds (or reads) the matrix and sends every rank its row block; then every rank tells
+    // each owner which of its columns it needs, and each owner builds its send plan from that
+    std::vector<std::string> out(size_t(a_.size));
+    if (a_.rank == 0) {
+      const CsrHost A = build_matrix();
+      TZ_CHECK(a_.m >= a_.size, "fewer matrix rows (" << a_.m << ") than ranks (" << a_.size << ")");
+      for (int q = 0; q < a_.size; ++q) {
+        auto [q0, q1] = row_partition(a_.m, q, a_.size);
+        const CsrHost B = row_block(A, q0, q1);
+        std::string &m = out[size_t(q)];
+        const int64_t hdr[5] = {a_.m, a_.nnz, a_.bw, a_.nnz_actual, 0};
+        m.append(reinterpret_cast<const char *>(hdr), sizeof(hdr));
+        put_vec(m, B.rowPtr);
+        put_vec(m, B.colInd);
+        put_vec(m, B.val);
+      }
+    }
+    const std::vector<std::string> in = ctrl->alltoallv(out);
+    const std::string &msg = in[0];
+    int64_t hdr[5];
+    TZ_CHECK(msg.size() >= sizeof(hdr), "spmv setup: no row block from rank 0");
+    std::memcpy(hdr, msg.data(), sizeof(hdr));
+    a_.m = hdr[0];
+    a_.nnz = hdr[1];
+    a_.bw = hdr[2];
+    a_.nnz_actual = hdr[3];
+    size_t at = sizeof(hdr);
+    std::tie(r0_, r1_) = row_partition(a_.m, a_.rank, a_.size);
+    mine.rows = r1_ - r0_;
+    mine.cols = a_.m;
+    mine.rowPtr = get_vec<int32_t>(msg, at);
+    mine.colInd = get_vec<int32_t>(msg, at);
+    mine.val = get_vec<float>(msg, at);
+    TZ_CHECK(int64_t(mine.rowPtr.size()) == mine.rows + 1, "spmv setup: row block of the wrong size");
+    // column requests: to each owner, the sorted columns of its I need
+    std::vector<std::vector<int64_t>> want(size_t(a_.size));
+    for (int32_t c : mine.colInd)
+      if (c < r0_ || c >= r1_) want[size_t(owner_of(c, a_.m, a_.size))].push_back(c);
+    std::vector<std::string> req(size_t(a_.size));
+    for (int q = 0; q < a_.size; ++q) {
+      std::vector<int64_t> &w = want[size_t(q)];
+      std::sort(w.begin(), w.end());
+      w.erase(std::unique(w.begin(), w.end()), w.end());
+      put_vec(req[size_t(q)], w);
+    }
+    const std::vector<std::string> got = ctrl->alltoallv(req);
+    for (int q = 0; q < a_.size; ++q) {
+      if (q == a_.rank) continue;
+      size_t k = 0;
+      needFrom[size_t(q)] = get_vec<int64_t>(got[size_t(q)], k);
+      for (int64_t c : needFrom[size_t(q)])
+        TZ_CHECK(c >= r0_ && c < r1_, "spmv setup: rank " << q << " asked for column " << c << ", not mine");
+    }
+  }
   const int64_t n = a_.m;
-  TZ_CHECK(n >= a_.size, "fewer matrix rows (" << n << ") than ranks (" << a_.size << ")");
-  std::tie(r0_, r1_) = row_partition(n, a_.rank, a_.size);
 
   // split my rows into local (own x) and remote (others' x) blocks
   std::vector<int64_t> rc;
-  for (int64_t r = r0_; r < r1_; ++r)
-    for (int32_t j = A.rowPtr[r]; j < A.rowPtr[r + 1]; ++j)
-      if (A.colInd[j] < r0_ || A.colInd[j] >= r1_) rc.push_back(A.colInd[j]);
+  for (int32_t c : mine.colInd)
+    if (c < r0_ || c >= r1_) rc.push_back(c);
   std::sort(rc.begin(), rc.end());
   rc.erase(std::unique(rc.begin(), rc.end()), rc.end());
   remoteCols_ = rc;
@@ -342,23 +457,23 @@ DistSpmv::DistSpmv(SpmvArgs a) : a_(std::move(a)) {
   local_.rowPtr.assign(size_t(nl + 1), 0);
   remote_.rowPtr.assign(size_t(nl + 1), 0);
   yRef_.assign(size_t(nl), 0.0);
-  for (int64_t r = r0_; r < r1_; ++r) {
+  for (int64_t i = 0; i < nl; ++i) {
     double acc = 0;
-    for (int32_t j = A.rowPtr[r]; j < A.rowPtr[r + 1]; ++j) {
-      const int64_t c = A.colInd[j];
-      acc += double(A.val[j]) * double(x_value(c));
+    for (int32_t j = mine.rowPtr[size_t(i)]; j < mine.rowPtr[size_t(i + 1)]; ++j) {
+      const int64_t c = mine.colInd[size_t(j)];
+      acc += double(mine.val[size_t(j)]) * double(x_value(c));
       if (c >= r0_ && c < r1_) {
         local_.colInd.push_back(int32_t(c - r0_));
-        local_.val.push_back(A.val[j]);
+        local_.val.push_back(mine.val[size_t(j)]);
       } else {
         const int64_t p = std::lower_bound(rc.begin(), rc.end(), c) - rc.begin();
         remote_.colInd.push_back(int32_t(p));
-        remote_.val.push_back(A.val[j]);
+        remote_.val.push_back(mine.val[size_t(j)]);
       }
     }
-    yRef_[size_t(r - r0_)] = acc;
-    local_.rowPtr[size_t(r - r0_ + 1)] = int32_t(local_.colInd.size());
-    remote_.rowPtr[size_t(r - r0_ + 1)] = int32_t(remote_.colInd.size());
+    yRef_[size_t(i)] = acc;
+    local_.rowPtr[size_t(i + 1)] = int32_t(local_.colInd.size());
+    remote_.rowPtr[size_t(i + 1)] = int32_t(remote_.colInd.size());
   }
 
   // receive plan: remote cols are sorted, hence grouped by owner
@@ -372,16 +487,8 @@ DistSpmv::DistSpmv(SpmvArgs a) : a_(std::move(a)) {
   sendOff_.assign(size_t(a_.size), 0);
   for (int q = 0; q < a_.size; ++q) {
     sendOff_[q] = int32_t(sendIdx_.size());
-    if (q == a_.rank) continue;
-    auto [q0, q1] = row_partition(n, q, a_.size);
-    std::vector<int64_t> need;
-    for (int64_t r = q0; r < q1; ++r)
-      for (int32_t j = A.rowPtr[r]; j < A.rowPtr[r + 1]; ++j)
-        if (A.colInd[j] >= r0_ && A.colInd[j] < r1_) need.push_back(A.colInd[j]);
-    std::sort(need.begin(), need.end());
-    need.erase(std::unique(need.begin(), need.end()), need.end());
-    for (int64_t c : need) sendIdx_.push_back(int32_t(c - r0_));
-    sendCount_[q] = int32_t(need.size());
+    for (int64_t c : needFrom[size_t(q)]) sendIdx_.push_back(int32_t(c - r0_));
+    sendCount_[q] = int32_t(needFrom[size_t(q)].size());
   }
   xLocal_.resize(size_t(nl));
   for (int64_t i = 0; i < nl; ++i) xLocal_[size_t(i)] = x_value(r0_ + i);

@@ -524,7 +524,7 @@ private:
   // TZ_COPY_ENGINES). One engine moves ~60 GB/s, and independent copies on 2 / 4 streams reach
   // 120 / 235 GB/s. Forking the chunks from the op's stream and joining them back through events
   // costs more than it gains (19 MB: 58 GB/s on one stream, 33 on two, 15 on four;
-  // scripts/sdma_probe.hip, profiles/r2_sdma/), so the default keeps one stream per op and
+  // scripts/sdma_probe.hip, profiles/archive/r2_sdma/), so the default keeps one stream per op and
   // leaves engine parallelism to the search (per-direction copy ops on different streams).
   int copyEngines_ = 1;
   struct EngineSet {
@@ -635,12 +635,18 @@ struct SpmvArgs {
   // when both can be set up, else whichever can)
   std::string transport = "auto";
   std::string prefix = "";  // op-name prefix (to combine several workloads in one graph)
+  // "root": rank 0 builds / reads the matrix and sends every rank its rows, then each rank asks
+  // the owners for the x entries it needs (the reference's setup); "local": every rank builds
+  // the whole matrix and derives every plan itself (no setup messages); "auto": root when the
+  // control plane is given and there are several ranks
+  std::string distribute = "auto";
   Json json() const;
 };
 
 class DistSpmv : public std::enable_shared_from_this<DistSpmv> {
 public:
-  explicit DistSpmv(SpmvArgs a);
+  /// `ctrl`: the control plane of the ranks (needed for SpmvArgs::distribute "root")
+  explicit DistSpmv(SpmvArgs a, Ctrl *ctrl = nullptr);
   ~DistSpmv();
   const SpmvArgs &args() const { return a_; }
   int64_t local_rows() const { return r1_ - r0_; }
@@ -710,6 +716,8 @@ private:
   void ipc_preflight(Ctrl *ctrl);
   /// one verified RCCL exchange under a bounded wait; "" on success, else why not
   std::string rccl_preflight_local();
+  /// the random band matrix or the Matrix Market file (a_.m / nnz / bw / nnz_actual updated)
+  CsrHost build_matrix();
   /// the RCCL exchange compiled into hipGraphs as the runtime compiles candidates, in the
   /// process's capture mode (or, if no workload has settled it yet, whole-schedule capture
   /// first, then child capture): collective; sets rcclGraphOk_ / rcclCaptureNote_

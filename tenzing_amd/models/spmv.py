@@ -24,6 +24,10 @@ class SpmvConfig:
     transport: str = "auto"     # x halo between ranks: rccl | ipc | auto (ChoiceOp over both)
     prefix: str = ""
     matrix: str = ""            # Matrix Market file of a square matrix instead of the band matrix
+    # root: rank 0 builds / reads the matrix and sends each rank its rows, the ranks then ask
+    # the owners for the x entries they need (the reference's setup); local: every rank builds
+    # it all itself; auto: root with a control plane of several ranks
+    distribute: str = "auto"
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.SpmvArgs":
         a = _tz.SpmvArgs()
@@ -33,6 +37,7 @@ class SpmvConfig:
         a.library = self.library
         a.transport = self.transport
         a.matrix = self.matrix
+        a.distribute = self.distribute
         a.rank, a.size, a.device = rank, size, device
         return a
 
@@ -40,7 +45,7 @@ class SpmvConfig:
 def build_spmv(cfg: SpmvConfig, ctrl=None, device: int = -1, setup: bool = True, graph=None):
     rank = ctrl.rank if ctrl is not None else 0
     size = ctrl.size if ctrl is not None else 1
-    s = _tz.DistSpmv(cfg.args(rank, size, device))
+    s = _tz.DistSpmv(cfg.args(rank, size, device), ctrl if size > 1 else None)
     if setup:
         s.setup(ctrl)
     g = graph if graph is not None else _tz.Graph()
