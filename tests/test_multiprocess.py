@@ -373,3 +373,32 @@ def test_solver_converges_at_the_8_rank_headline_tree(tmp_path, model):
         assert r0[k]["best_us"] <= r0[k]["seeded_best_us"], report
     assert r0["fastmin2000"]["tree_nodes"] > r0["fastmin120"]["tree_nodes"]
     assert r0["tree"]["branching_mean"] > 2 and r0["tree"]["depth_mean"] > 20, report
+
+
+def body_spmv_root_distribution():
+    """the reference's SpMV setup: rank 0 builds the band matrix and sends each rank its rows,
+    the ranks ask the owners for the x entries they need; the plans match every rank deriving
+    everything itself"""
+    import tenzing_amd as tz
+    from tenzing_amd.models import SpmvConfig
+    from tenzing_amd.parallel import init_ctrl
+
+    c = init_ctrl(timeout_s=60)
+    out = {"rank": c.rank}
+    for how in ("root", "local"):
+        s = tz._tz.DistSpmv(SpmvConfig(m=30_000, distribute=how).args(c.rank, c.size, -1), c)
+        out[how] = dict(distribute=s.args.distribute, nnz=s.args.nnz_actual, rows=s.local_rows(),
+                        local=s.local_nnz(), remote=s.remote_nnz(), cols=s.remote_cols(),
+                        send=s.send_elems(), peers=s.num_peers())
+    return out
+
+
+def test_spmv_root_distribution_matches_local_derivation(tmp_path):
+    rs = _run("body_spmv_root_distribution", 3, tmp_path)
+    for r in rs:
+        assert r["root"]["distribute"] == "root" and r["local"]["distribute"] == "local"
+        assert {k: v for k, v in r["root"].items() if k != "distribute"} == \
+               {k: v for k, v in r["local"].items() if k != "distribute"}, r
+        # band of half-width m / 3: the middle rank's rows reach both neighbours, the ends one
+        assert r["root"]["nnz"] == 300_000 and r["root"]["peers"] == (2 if r["rank"] == 1 else 1)
+    assert sum(r["root"]["local"] + r["root"]["remote"] for r in rs) == 300_000
