@@ -224,9 +224,10 @@ def main() -> int:
                          "this + --watchdog-k x n x its expected iteration time, then its device "
                          "waits and RCCL communicators are aborted and the candidate is skipped")
     ap.add_argument("--watchdog-k", type=float, default=50.0)
-    ap.add_argument("--ghost-align", type=int, default=16,
+    ap.add_argument("--ghost-align", type=int, default=-2,
                     help="x ghost runs aligned to 16 (line) / 8 (sector) elements, 0 = interior "
-                         "rows sector-aligned, -1 = x=0 at the pitched row start (reference)")
+                         "rows sector-aligned, -1 = x=0 at the pitched row start (reference), "
+                         "-2 = auto (16 for qxyz, -1 for xyzq)")
     ap.add_argument("--subrecords", default="auto", choices=["auto", "on", "off"],
                     help="after the headline: the reference's XYZQ layout and BASELINE configs 2 "
                          "(SpMV) and 5 (SpMV + halo), each searched briefly, verified and timed "

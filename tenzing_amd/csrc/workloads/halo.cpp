@@ -65,8 +65,13 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.order == "xyzq" || a_.order == "qxyz", "order must be xyzq or qxyz");
   TZ_CHECK(a_.rank >= 0 && a_.rank < a_.size, "bad rank");
   TZ_CHECK(a_.pitch_pad >= 0 && a_.pitch_pad % 16 == 0, "pitch_pad must be a multiple of 16");
-  TZ_CHECK(a_.ghost_align == -1 || a_.ghost_align == 0 || a_.ghost_align == 8 || a_.ghost_align == 16,
-           "ghost_align must be -1 (x = 0 at the row start), 0, 8 or 16");
+  TZ_CHECK(a_.ghost_align >= -2 && (a_.ghost_align <= 0 || a_.ghost_align == 8 || a_.ghost_align == 16),
+           "ghost_align must be -2 (auto), -1 (x = 0 at the row start), 0, 8 or 16");
+  // auto: QXYZ with line-aligned ghost runs (a row's ghost and source runs, 9 doubles each,
+  // cannot share a line: each on a line of its own is the minimum traffic); XYZQ with x = 0 at
+  // the row start, where a row's 3-double ghost and source runs share lines that the row-pair
+  // move reads and writes together (profiles/r5_roof/: 90 us vs 93 line-aligned)
+  if (a_.ghost_align == -2) a_.ghost_align = a_.order == "qxyz" ? 16 : -1;
   TZ_CHECK(a_.wide_puts == "auto" || a_.wide_puts == "on" || a_.wide_puts == "off",
            "wide_puts must be auto, on or off");
   TZ_CHECK(a_.wide_put_blocks >= 1 && a_.wide_put_blocks <= 4096,

@@ -206,7 +206,9 @@ struct HaloArgs {
   // start) on 8-element (64-B sector) / 16-element (128-B line) boundaries, and direct moves
   // widen their x ghost writes over the neighbouring row padding to whole sectors / lines (no
   // partially written sectors or lines on the x faces). 0: line-optimal padding, exact runs.
-  int ghost_align = 16;
+  // -1: no padding, x = 0 at the row start (the reference's layout). -2 (default): 16 for
+  // QXYZ, -1 for XYZQ.
+  int ghost_align = -2;
   // also run a 7-point stencil over the interior after the exchange (into a second grid): the
   // search may update the ghost-free interior while ghosts are in flight and the one-cell
   // boundary shell afterwards, or the whole domain after the exchange (a ChoiceOp)

@@ -29,7 +29,9 @@ class HaloConfig:
     comms: int = 0        # RCCL communicators (0 = one per direction)
     pitch_pad: int = 0    # extra row-pitch elements (multiple of 16)
     rank_grid: tuple = ()  # (px, py, pz); () = reference rule (prime factors, smallest dim first)
-    ghost_align: int = 16  # x ghost runs aligned to 8 (sector) / 16 (line) elements, 0 = off
+    # x ghost runs aligned to 8 (sector) / 16 (line) elements, 0 = off, -1 = x = 0 at the row
+    # start (the reference's layout), -2 = auto (16 for qxyz, -1 for xyzq)
+    ghost_align: int = -2
     stencil: bool = False  # add a 7-point stencil (interior beside / shell after the exchange)
     # two-hop routing of a share of every face through the corner peer (2x2x2 rank grid, ipc
     # receive buffers): "auto" offers it to the search, "off", "force" (only transport)
