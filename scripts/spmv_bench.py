@@ -21,8 +21,9 @@ def main():
     ap.add_argument("--m", type=int, default=150_000)
     ap.add_argument("--per-row", type=int, default=10)
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--bw", type=int, default=0, help="band half-width (0: m, as at one rank)")
     a = ap.parse_args()
-    rp, ci, val = tz._tz.random_band_matrix(a.m, a.m, a.per_row * a.m, 1)
+    rp, ci, val = tz._tz.random_band_matrix(a.m, a.bw or a.m, a.per_row * a.m, 1)
     dev = "cuda"
     rp_t = torch.tensor(rp, dtype=torch.int32, device=dev)
     ci_t = torch.tensor(ci, dtype=torch.int32, device=dev)
@@ -33,6 +34,7 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     K = tz._tz.kernels
     variants = [(f"lanes{w}", w) for w in (4, 8, 16, 32)] + [("stream", -1)]
+    variants += [(f"ilp{w}", 1000 + w) for w in (1, 2, 4)]
     variants += [(f"rocsparse_{alg}", alg) for alg in ("adaptive", "lrb", "rowsplit")]
     yref = None
     for name, v in variants:

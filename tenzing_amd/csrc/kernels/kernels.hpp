@@ -167,7 +167,10 @@ void copy_many(const CopyDesc *d, int n, void *stream);
 
 /// y[r] = sum_j A[r,j] x[j] for CSR A (f32 values, i32 indices). `lanesPerRow` in {1,2,4,8,16,32,64}
 /// (0 = 8), or -1 for the CSR-stream kernel (block-contiguous nnz streaming + LDS segmented
-/// reduction). When `accumulate`, y[r] += ... instead.
+/// reduction). When `accumulate`, y[r] += ... instead. lanesPerRow = kSpmvIlp + W (W = 1, 2, 4):
+/// the ILP kernel (every lane issues 16 / W column loads, then the value loads and x gathers,
+/// before using any).
+constexpr int kSpmvIlp = 1000;
 void csr_spmv(int nRows, const int32_t *rowPtr, const int32_t *colInd, const float *val,
               const float *x, float *y, int lanesPerRow, bool accumulate, void *stream);
 /// dst[i] = src[idx[i]]

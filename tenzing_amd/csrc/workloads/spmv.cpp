@@ -1000,6 +1000,8 @@ OpPtr DistSpmv::local_op(bool accum, const std::string &p) {
   std::vector<OpPtr> ch;
   for (int w : {4, 8, 16})
     ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_w" + std::to_string(w), w, accum));
+  for (int w : {1, 2, 4})
+    ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_i" + std::to_string(w), kern::kSpmvIlp + w, accum));
   ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_stream", -1, accum));
   if (!a_.library.empty())
     ch.push_back(std::make_shared<SpmvLocal>(self, p + "yl_rocsparse_" + a_.library, kLibrary, accum));

@@ -112,9 +112,12 @@ def test_box_copy_many_equals_single(tz, gpu):
 
 
 @pytest.mark.parametrize("lanes,per_row", [(0, 10), (1, 10), (4, 10), (8, 10), (16, 10),
-                                           (64, 10), (-1, 10), (-1, 90), (16, 90)])
+                                           (64, 10), (-1, 10), (-1, 90), (16, 90),
+                                           (1001, 10), (1002, 10), (1004, 10), (1001, 40),
+                                           (1004, 90)])
 def test_csr_spmv_matches_torch(tz, gpu, lanes, per_row):
-    # per_row 90: a 64-row CSR-stream block holds > 4096 nnz, exercising its multi-pass path
+    # per_row 90: a 64-row CSR-stream block holds > 4096 nnz, exercising its multi-pass path;
+    # 1000 + W: the ILP kernel (16 entries per lane group and pass: 40 / 90 take several passes)
     n = 5000
     rp, ci, val = tz._tz.random_band_matrix(n, 300, per_row * n, 7)
     rp_t = torch.tensor(rp, dtype=torch.int32, device="cuda")
