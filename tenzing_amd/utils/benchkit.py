@@ -31,12 +31,14 @@ def _busy_graph(tz, branches: int, us: float):
     return g
 
 
-def branch_probe(tz, rt, branches: int = 3, us: float = 50.0, iters: int = 10):
+def branch_probe(tz, rt, branches: int = 3, us: float = 200.0, iters: int = 10):
     """Microseconds per hipGraph launch of ``branches`` independent ``us``-long single-workgroup
     kernels, one per stream of ``rt`` (compiled the way the runtime compiles every schedule), and
     of one such kernel alone. ``ratio`` = all / one: about 1 when the branches run at once,
-    about ``branches`` when they serialize. The runtime's mode and unroll are restored; None if
-    the runtime cannot build the graph."""
+    about ``branches`` when they serialize. HIP's graph executor starts each further branch
+    12-25 us after the previous one on MI355X (``stagger_us``; profiles/r5_branch/), so the
+    kernels are long (200 us) for the ratio to tell overlap from serialization. The runtime's
+    mode and unroll are restored; None if the runtime cannot build the graph."""
     from ..search import greedy_schedule
 
     if rt.num_streams() < branches:
@@ -68,7 +70,8 @@ def branch_probe(tz, rt, branches: int = 3, us: float = 50.0, iters: int = 10):
     if not one or not many:
         return None
     return {"branches": branches, "kernel_us": us, "one_us": round(one, 1),
-            "all_us": round(many, 1), "ratio": round(many / one, 3)}
+            "all_us": round(many, 1), "ratio": round(many / one, 3),
+            "stagger_us": round((many - one) / max(1, branches - 1), 1)}
 
 
 def choose_pad(make_rt, probe, pads, threshold: float = 1.5, margin: float = 0.9):
@@ -209,3 +212,33 @@ def search_record(tz, ctrl, rt, graph, streams: int, verify, steps: int, warmup:
     after = verify(None)
     rec["verified_bad_after_timing"] = int(after)
     return rec
+
+
+def _main(argv=None) -> int:
+    """``python -m tenzing_amd.utils.benchkit probe [--streams 4] [--pad -1] [--us 50]``: one JSON
+    line per branch count (2, 3, 4) with the graph-branch probe of a fresh runtime (for A/B of
+    the HIP runtime's environment knobs, one process per setting)."""
+    import argparse
+    import json
+    import os
+
+    ap = argparse.ArgumentParser(prog="python -m tenzing_amd.utils.benchkit")
+    ap.add_argument("cmd", choices=["probe"])
+    ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--pad", type=int, default=-1)
+    ap.add_argument("--us", type=float, default=200.0)
+    a = ap.parse_args(argv)
+    import tenzing_amd as tz
+
+    rt = tz.HipRuntime(device=0, n_streams=a.streams, pad_streams=a.pad)
+    env = {k: v for k, v in os.environ.items() if k.startswith(("DEBUG_HIP", "GPU_MAX_HW", "HIP_", "TZ_PAD"))}
+    for k in (2, 3, 4):
+        if k > a.streams:
+            continue
+        print(json.dumps({"env": env, "pad_streams": rt.pad_streams,
+                          "probe": branch_probe(tz, rt, branches=k, us=a.us)}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(_main())
