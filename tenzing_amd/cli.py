@@ -42,7 +42,7 @@ def _build_workload(a, ctrl, device, setup):
                     hostsplit_chunks=a.hostsplit_chunks, rank_grid=grid,
                     wide_puts=a.wide_puts, wide_put_blocks=a.wide_put_blocks)
     sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport,
-                    matrix=a.spmv_matrix, library=a.spmv_library)
+                    matrix=a.spmv_matrix, library=a.spmv_library, distribute=a.spmv_distribute)
     if a.workload == "halo":
         h, g = build_halo(hc, ctrl, device, setup)
         return g, {"halo": h}
@@ -184,6 +184,7 @@ _WORKLOAD_KEYS = ("workload", "noop_width", "streams", "halo_n", "nq", "ghost", 
                   "hostsplit_fracs", "hostsplit_chunks", "wide_puts", "wide_put_blocks",
                   "stencil", "rank_grid",
                   "spmv_m", "spmv_matrix", "spmv_form", "spmv_transport", "spmv_library",
+                  "spmv_distribute",
                   "cu_partition", "stream_priorities")
 
 
@@ -452,6 +453,9 @@ def _parser() -> argparse.ArgumentParser:
                    help="Matrix Market file (square) instead of the random band matrix")
     s.add_argument("--spmv-form", default="choice", choices=["choice", "split", "accum"])
     s.add_argument("--spmv-transport", default="auto", choices=["auto", "rccl", "ipc"])
+    s.add_argument("--spmv-distribute", default="auto", choices=["auto", "root", "local"],
+                   help="several ranks: rank 0 builds / reads the matrix and sends each rank its "
+                        "rows (root, the reference's setup) or every rank builds it (local)")
     s.set_defaults(fn=cmd_search)
     r = sub.add_parser("rules")
     r.add_argument("results")

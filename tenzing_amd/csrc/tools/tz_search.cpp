@@ -59,7 +59,7 @@ void usage() {
          "  [--halo-n N] [--nq N] [--ghost N] [--neighbors 6|26] [--order xyzq|qxyz]\n"
          "  [--fuse none|pack|all|groups|choice] [--graph-unroll K]\n"
          "  [--transport auto|rccl|ipc|copy|direct] [--rank-grid PXxPYxPZ] [--spmv-m N] [--spmv-matrix F.mtx]\n"
-         "  [--spmv-form choice|split|accum] [--spmv-transport auto|rccl|ipc]\n"
+         "  [--spmv-form choice|split|accum] [--spmv-transport auto|rccl|ipc] [--spmv-distribute auto|root|local]\n"
          "  [--spmv-library adaptive|lrb|rowsplit|''] [--cu-partition] [--stencil] [--max-seqs N]\n"
          "  [--relay auto|off|force] [--relay-fracs F1,F2]\n"
          "  [--hostsplit auto|off|force] [--hostsplit-fracs F1,F2,...] [--hostsplit-chunks N]\n"
