@@ -196,6 +196,9 @@ def main() -> int:
     ap.add_argument("--seed-transports", type=int, default=1,
                     help="several ranks: measure one fused schedule per remote transport before "
                          "the search (each transport is then measured at least once; 0 = off)")
+    ap.add_argument("--sim-seeds", type=int, default=2,
+                    help="several ranks: also seed the search with the K best schedules of a "
+                         "short hardware-free search under the link-aware cost model (0 = off)")
     ap.add_argument("--graph-unroll", type=int, default=20,
                     help="iterations per hipGraph launch when timing the graph-compiled schedule")
     ap.add_argument("--search-graph-unroll", type=int, default=10,
@@ -392,6 +395,20 @@ def main() -> int:
                 seed_alts.append(alt)
             except Exception as e:  # noqa: BLE001 (same graph on every rank: all skip alike)
                 print(f"bench.py: rank {rank}: no seed schedule for {alt}: {e}", file=sys.stderr)
+        sim_seeded = []
+        if rank == 0 and args.sim_seeds > 0:
+            # the link-aware model's own best structures (stream splits, transport mixes) as
+            # extra seeds: 400 hardware-free iterations on this rank's graph, a fraction of a
+            # second; a wrong model costs only these few measurements
+            from tenzing_amd.parallel.linkmodel import sim_seeds
+            try:
+                for sq, us in sim_seeds(graph, platform, args.sim_seeds, 400, exclude=seeds,
+                                        seed=args.seed):
+                    seeds.append(sq)
+                    sim_seeded.append({"key": sq.canonical_key(), "model_us": round(us, 1),
+                                       "transport": remote_via([o.name for o in sq.ops()])})
+            except Exception as e:  # noqa: BLE001 (seeds are optional)
+                print(f"bench.py: model seeds skipped: {e}", file=sys.stderr)
         if rank == 0:
             opts.seed_schedules = seeds
 
@@ -439,11 +456,18 @@ def main() -> int:
             if len(top) >= max(1, args.rerank):
                 break
         seeded = {}
+        model = {d["key"]: d for d in (sim_seeded if world > 1 and args.seed_transports else [])}
         for s_ in res.sims:
             if s_.seeded:
+                key = s_.seq.canonical_key()
+                if key in model:  # a model seed: its measured time beside the model's
+                    model[key]["measured_ms"] = s_.res.pct10 * 1e3
+                    continue
                 v = remote_via([o.name for o in s_.seq.ops()]) or "none"
                 seeded[v] = s_.res.pct10 * 1e3
+        model_seeded = [{k: v for k, v in d.items() if k != "key"} for d in model.values()]
         payload = json.dumps({"seqs": [res.sims[i].seq.json() for i in top],
+                              "model_seeded": model_seeded,
                               "pct10": [res.sims[i].res.pct10 for i in top],
                               "n_sims": len(res.sims), "tree": res.tree_size,
                               "failed": res.failed, "seeded": seeded})
@@ -586,6 +610,7 @@ def main() -> int:
         "search_mode": "hipgraph" if mode == tz.ExecMode.Graph else "eager",
         "search_best_pct10_ms": best_pct10 * 1e3,
         "seeded_pct10_ms": payload["seeded"] or None,
+        "model_seeded": payload.get("model_seeded") or None,
         "rerank": rerank,
         "eager_ms_per_step": t_eager / args.steps * 1e3,
         "graph_ms_per_step": (t_graph / args.steps * 1e3) if graph_ok else None,

@@ -112,3 +112,34 @@ def tree_stats(graph, platform, rollouts: int = 50, seed: int = 0) -> dict:
     return {"rollouts": rollouts, "depth_mean": sum(depths) / len(depths), "depth_max": max(depths),
             "branching_mean": sum(widths) / len(widths), "branching_max": max(widths),
             "log10_paths_per_rollout": round(log10, 1)}
+
+
+def sim_seeds(graph, platform, k: int = 2, iters: int = 400, params=None, exclude=(), seed: int = 0):
+    """The ``k`` best distinct schedules of a hardware-free MCTS (FastMin, ``iters`` iterations)
+    under the link-aware model: seeds for a measured search, so that it starts from structures
+    the model ranks well (stream splits, transport mixes) besides the greedy per-transport ones.
+    ``exclude``: sequences already seeded (skipped by canonical key). Returns
+    [(sequence, model_us)], best first. One process, no GPU, no collectives."""
+    if k <= 0:
+        return []
+    p = params if params is not None else link_sim_params()
+    o = _tz.MctsOpts()
+    o.n_iters = iters
+    o.strategy = "FastMin"
+    o.seed = seed
+    o.bench = _tz.BenchOpts(n_iters=2, max_retries=1, target_secs=0.001)
+    if exclude:
+        o.seed_schedules = list(exclude)
+    res = _tz.mcts_explore(graph, platform, _tz.SimBenchmarker(platform.n_streams, p), _tz.SelfCtrl(), o)
+    skip = {s.canonical_key() for s in exclude}
+    out, keys = [], set(skip)
+    for i in sorted(range(len(res.sims)), key=lambda i: res.sims[i].res.pct10):
+        sq = res.sims[i].seq
+        key = sq.canonical_key()
+        if key in keys:
+            continue
+        keys.add(key)
+        out.append((sq, res.sims[i].res.pct10 * 1e6))
+        if len(out) >= k:
+            break
+    return out

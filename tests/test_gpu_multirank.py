@@ -267,6 +267,10 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     assert ta["peer_access"].endswith("(loopback)")
     assert "libamdhip64" in j["runtime"]["hip_runtime"]["path"]
     assert "librccl" in j["runtime"]["rccl_library"]["path"]
+    # the link-aware model's best structures seeded too, each measured (loopback rates say
+    # nothing about xGMI: only the plumbing is checked here)
+    ms = j["model_seeded"]
+    assert ms and len(ms) <= 2 and all(d["model_us"] > 0 and d["measured_ms"] > 0 for d in ms), ms
     if mode == "buffers":
         # one seed per remote transport, each measured before the search
         assert set(j["seeded_pct10_ms"]) == {"ipc", "sdma", "memcpy", "mixed", "hostsplit10",
