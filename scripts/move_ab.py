@@ -25,8 +25,14 @@ def main():
     ap.add_argument("--blocks", action="store_true",
                     help="also 1-2 items in flight per lane (2-4x the workgroups; the HBM probe, "
                          "scripts/hbm_roof.hip, copies fastest with ~128 workgroups per CU)")
+    ap.add_argument("--groups", action="store_true",
+                    help="instead: the default move of each direction group alone (x / y / z "
+                         "faces, edges, corners) and all together, with its line traffic rate")
+    ap.add_argument("--order", default="qxyz")
     a = ap.parse_args()
     torch.zeros(1, device="cuda")
+    if a.groups:
+        return groups(a)
     h, _ = build_halo(HaloConfig(n=a.n, neighbors=26, order="qxyz", transport="direct"),
                       tz.SelfCtrl(), device=0)
     k = tz._tz.kernels
@@ -89,6 +95,52 @@ def main():
         print(json.dumps({"variant": name, "median_us": round(v[len(v) // 2], 2),
                           "min_us": round(v[0], 2), "all": [round(x, 2) for x in v]}))
     print(json.dumps({"bad_cells_after_default": int(bad)}))
+
+
+def _lines(moves):
+    """128-B lines read + written by these moves (every row at one intra-line alignment)"""
+    tot = 0
+    for m in moves:
+        rows = m["n"][0] * m["n"][1] * m["n"][2]
+        runs = [(m["src_off"], m["len"]), (m["dst_off"], m["len"])]
+        if m["pair"]:
+            d = m["dst_off"] - m["src_off"]
+            runs += [(m["src_off"] + m["len"] + d, m["len"]), (m["src_off"] + m["len"], m["len"])]
+        for off, ln in runs:
+            tot += rows * ((off + ln - 1) // 16 - off // 16 + 1)
+    return tot * 128
+
+
+def groups(a):
+    h, _ = build_halo(HaloConfig(n=a.n, neighbors=26, order=a.order, transport="direct"),
+                      tz.SelfCtrl(), device=0)
+    st = torch.cuda.current_stream()
+    kind = {}
+    for i in range(h.ndirs()):
+        d = h.dir(i)
+        nz = sum(1 for c in d if c)
+        key = ("x", "y", "z")[[c != 0 for c in d].index(True)] + "_faces" if nz == 1 else \
+            ("edges" if nz == 2 else "corners")
+        kind.setdefault(key, []).append(i)
+    kind["all"] = list(range(h.ndirs()))
+    for name, dirs in kind.items():
+        v = []
+        for _ in range(a.rounds):
+            for _ in range(3):
+                h.direct_group(dirs, st.cuda_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.reps):
+                h.direct_group(dirs, st.cuda_stream)
+            e1.record(st)
+            e1.synchronize()
+            v.append(e0.elapsed_time(e1) * 1e3 / a.reps)
+        v.sort()
+        lines = _lines(h.direct_moves(dirs))
+        us = v[len(v) // 2]
+        print(json.dumps({"group": name, "dirs": len(dirs), "median_us": round(us, 2),
+                          "line_MB": round(lines / 1e6, 2), "TBps": round(lines / us / 1e6, 2)}),
+              flush=True)
 
 
 if __name__ == "__main__":

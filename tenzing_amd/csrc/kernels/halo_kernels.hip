@@ -58,6 +58,14 @@ BoxTuning &box_tuning() {
   return t;
 }
 
+bool peel_moves() {
+  static const bool on = [] {
+    const char *v = std::getenv("TZ_MOVE_PEEL");
+    return !v || std::atoi(v) != 0;
+  }();
+  return on;
+}
+
 void set_xcd_remap(int mode) {
   if (mode < 0 || mode > 2)
     throw std::invalid_argument("xcd_remap must be 0 (round-robin), 1 (per-XCD range) or 2 (per-box)");
@@ -255,6 +263,30 @@ __device__ __forceinline__ void move_body(const DevDesc &d, uint32_t tid, uint32
   }
 }
 
+// peeled rows (d.vec == 3, or 5 with a tail): a row [x0, x0 + len) with x0 odd (the interior of
+// an XYZQ grid with x = 0 at the row start begins at x = 3): element x0 alone, 16-B pairs from
+// x0 + 1 (16-B aligned), and the last element alone when len - 1 is odd. Item xv of a row:
+// xv < pairs a pair, then the head, then the tail; d.lvec = pairs + 1 + tail.
+template <bool NT, bool NTS>
+__device__ __forceinline__ void peel_body(const DevDesc &d, uint32_t tid, uint32_t nthreads) {
+  const uint32_t tail = d.vec == 5 ? 1u : 0u;
+  const uint32_t pairs = d.lvec - 1u - tail;
+  const double *__restrict__ src = d.src;
+  double *__restrict__ dst = d.buf + d.delta;
+  for (uint32_t it = tid; it < d.items; it += nthreads) {
+    const uint32_t row = d.dl.div(it);
+    const uint32_t xv = it - row * d.lvec;
+    const int64_t base = grid_index<1>(d, it) - int64_t(xv); // the row's x0
+    if (xv < pairs) {
+      const int64_t g = base + 1 + 2 * int64_t(xv);
+      st<NTS>(reinterpret_cast<dbl2_t *>(dst + g), ld<NT>(reinterpret_cast<const dbl2_t *>(src + g)));
+    } else {
+      const int64_t g = xv == pairs ? base : base + 2 * int64_t(pairs) + 1;
+      st<NTS>(dst + g, ld<NT>(src + g));
+    }
+  }
+}
+
 // row pair (MoveDesc::pair, d.vec = -len): item (row, k), k < 2 len: k < len moves element k of
 // run A (row end -> row start), k >= len element k - len of run B (row start -> row end).
 // Consecutive lanes cover consecutive k of a row, as the plain move covers a row's x: per row
@@ -311,6 +343,7 @@ __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap
   const uint32_t nth = nb * kThreads;
   if (d.vec == 2) move_body<2, U, NT, NTS>(d, tid, nth);
   else if (d.vec < 0) pair_body<U, NTS>(d, tid, nth);
+  else if (d.vec >= 3) peel_body<NT, NTS>(d, tid, nth);
   else move_body<1, U, NT, NTS>(d, tid, nth);
 }
 
@@ -392,6 +425,7 @@ __global__ __launch_bounds__(kThreads) void box_move_signal_k(DevBatch b, DevSig
   const uint32_t tid = (blockIdx.x - b.block_start[box]) * kThreads + threadIdx.x;
   const uint32_t nth = nb * kThreads;
   if (d.vec == 2) move_body<2, U, NT>(d, tid, nth);
+  else if (d.vec >= 3) peel_body<NT, false>(d, tid, nth);
   else move_body<1, U, NT>(d, tid, nth);
   signal_box_done(sig, box, nb);
 }
@@ -871,6 +905,17 @@ DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vec
       d.lvec = uint32_t(m.len);
       d.items = uint32_t(uint64_t(m.len) * m.n1 * m.n2 * m.n3);
       d.dl = FastDiv(std::max<uint32_t>(d.lvec, 1));
+    }
+    // rows that start one element past a 16-B boundary on both sides (strides even): peel the
+    // first element (and an odd last one), move the rest 16 B at a time
+    if (d.vec == 1 && peel_moves() && m.len >= 3 && m.src_off % 2 != 0 && m.dst_off % 2 != 0 &&
+        m.s1 % 2 == 0 && m.s2 % 2 == 0 && m.s3 % 2 == 0 &&
+        reinterpret_cast<uintptr_t>(m.src) % 16 == 0 && reinterpret_cast<uintptr_t>(m.dst) % 16 == 0) {
+      const uint32_t tail = uint32_t((m.len - 1) % 2), pairs = uint32_t((m.len - 1) / 2);
+      d.vec = tail ? 5 : 3;
+      d.lvec = pairs + 1 + tail;
+      d.items = uint32_t(uint64_t(d.lvec) * m.n1 * m.n2 * m.n3);
+      d.dl = FastDiv(d.lvec);
     }
     b.d[b.n] = d;
     b.block_start[b.n] = total;

@@ -62,6 +62,9 @@ struct BoxTuning {
 BoxTuning &box_tuning();
 /// set BoxTuning::xcd_remap; throws std::invalid_argument unless mode is 0, 1 or 2
 void set_xcd_remap(int mode);
+/// moves of rows that start one element past a 16-B boundary peel that element and move the
+/// rest with 16-B accesses (env TZ_MOVE_PEEL=0: 8-B accesses throughout)
+bool peel_moves();
 
 /// A box-to-box move between two arrays of the SAME pitched layout: element (x,i1,i2,i3) of
 /// the box at `src + src_off` goes to the same element of the box at `dst + dst_off`
