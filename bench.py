@@ -658,6 +658,23 @@ def main() -> int:
     # probe) cannot turn a finished measurement into a partial one.
     post = {"budget_s": args.post_budget_s, "done": [], "running": None}
     out["post_timing"] = post
+    # the best schedule, saved before anything optional runs
+    if rank == 0 and args.save_best:
+        doc = {"tenzing_amd": tz.__version__, "ranks": world,
+               "mode": "graph" if use_graph else "eager", "pct10_ms": ms,
+               "args": {"workload": "halo", "streams": args.streams, "halo_n": args.n,
+                        "nq": cfg.nq, "ghost": cfg.ghost, "neighbors": args.neighbors,
+                        "order": args.order, "fuse": args.fuse, "transport": args.transport,
+                        "relay": args.relay,
+                        "relay_fracs": ",".join(str(f) for f in cfg.relay_fracs),
+                        "hostsplit": args.hostsplit,
+                        "hostsplit_fracs": ",".join(str(f) for f in cfg.hostsplit_fracs),
+                        "hostsplit_chunks": cfg.hostsplit_chunks,
+                        "wide_puts": args.wide_puts, "wide_put_blocks": args.wide_put_blocks,
+                        "stencil": bool(args.stencil), "rank_grid": args.rank_grid},
+               "schedule": json.loads(best.json(True))}
+        with open(args.save_best, "w") as f:
+            json.dump(doc, f, indent=1)
 
     def post_phase(name):
         post["running"] = name
@@ -673,7 +690,8 @@ def main() -> int:
 
     if deadline is not None:
         report()
-        deadline.tighten(max(5.0, min(args.post_budget_s, deadline.remaining - 10.0)), 0)
+        deadline.tighten(max(5.0, min(args.post_budget_s, deadline.remaining - 10.0)),
+                         0 if bad == 0 else 3)
 
     stuck = False
     # per-link bandwidth of each transport (context for the multi-GPU number: an exchange can
@@ -726,22 +744,6 @@ def main() -> int:
         if deadline is not None:
             deadline.cancel()
         print(json.dumps(out), flush=True)
-        if args.save_best:
-            doc = {"tenzing_amd": tz.__version__, "ranks": world,
-                   "mode": "graph" if use_graph else "eager", "pct10_ms": ms,
-                   "args": {"workload": "halo", "streams": args.streams, "halo_n": args.n,
-                            "nq": cfg.nq, "ghost": cfg.ghost, "neighbors": args.neighbors,
-                            "order": args.order, "fuse": args.fuse, "transport": args.transport,
-                            "relay": args.relay,
-                            "relay_fracs": ",".join(str(f) for f in cfg.relay_fracs),
-                            "hostsplit": args.hostsplit,
-                            "hostsplit_fracs": ",".join(str(f) for f in cfg.hostsplit_fracs),
-                            "hostsplit_chunks": cfg.hostsplit_chunks,
-                            "wide_puts": args.wide_puts, "wide_put_blocks": args.wide_put_blocks,
-                            "stencil": bool(args.stencil), "rank_grid": args.rank_grid},
-                   "schedule": json.loads(best.json(True))}
-            with open(args.save_best, "w") as f:
-                json.dump(doc, f, indent=1)
     elif deadline is not None:
         deadline.cancel()
     if stuck:
