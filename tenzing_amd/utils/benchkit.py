@@ -206,6 +206,7 @@ def search_record(tz, ctrl, rt, graph, streams: int, verify, steps: int, warmup:
                 "eager_ms_per_step": t_e / steps * 1e3,
                 "graph_ms_per_step": (t_g / steps * 1e3) if graph_ok else None,
                 "schedule_ops": len(best), "steps": steps, "warmup": warmup,
+                "schedule_gpu_ops": [o.name for o in best.ops() if o.op_class == "BoundGpu"],
                 "wall_s": round(time.time() - t_start, 2)})
     # correctness after the timed iterations too (the sub-record's workload decides what a
     # bad result is)
