@@ -497,6 +497,10 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("seed", &SimParams::seed)
       .def_readwrite("contention", &SimParams::contention)
       .def_readwrite("link_model", &SimParams::link_model)
+      .def_readwrite("graph", &SimParams::graph)
+      .def_readwrite("graph_gap_us", &SimParams::graph_gap_us)
+      .def_readwrite("graph_join_us", &SimParams::graph_join_us)
+      .def_readwrite("graph_wait_us", &SimParams::graph_wait_us)
       .def_readwrite("engine_GBps", &SimParams::engine_GBps)
       .def_readwrite("resource_GBps", &SimParams::resource_GBps);
   py::class_<SimBenchmarker, Benchmarker>(m, "SimBenchmarker")

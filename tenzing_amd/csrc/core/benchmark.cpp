@@ -221,7 +221,14 @@ void HostExecutor::run(int64_t n) {
 // ---------------------------------------------------------------- Sim
 
 SimExecutor::SimExecutor(int nStreams, SimParams p)
-    : n_(nStreams), p_(p), rng_(p.seed), streamFree_(nStreams, 0.0) {}
+    : n_(nStreams), p_(p), rng_(p.seed), streamFree_(nStreams, 0.0), lastEnd_(nStreams, 0.0),
+      pending_(nStreams), used_(nStreams, 0) {}
+
+void SimExecutor::graph_dep(int stream, double t) {
+  // work the stream's own order already covers costs nothing; an event from the sequence's
+  // start (t = 0) neither
+  if (t > lastEnd_[stream] && t > 0) pending_[stream].push_back(t);
+}
 
 double SimExecutor::dur(double us) {
   if (p_.noise <= 0) return us;
@@ -268,8 +275,20 @@ double SimExecutor::link_duration(const GpuOp &op, double start) {
 
 void SimExecutor::launch(const GpuOp &op, int stream) {
   TZ_CHECK(stream >= 0 && stream < n_, "sim stream out of range");
-  host_ += p_.launch_us;
-  const double start = std::max(host_, streamFree_[stream]);
+  double start;
+  if (p_.graph) {
+    graph_dep(stream, host_); // after a host sync or host op: a dependency like any other
+    start = streamFree_[stream];
+    std::vector<double> &pw = pending_[stream];
+    if (!pw.empty()) {
+      const double last = *std::max_element(pw.begin(), pw.end());
+      start = std::max(start, last + p_.graph_join_us + p_.graph_wait_us * double(pw.size() - 1));
+      pw.clear();
+    }
+  } else {
+    host_ += p_.launch_us;
+    start = std::max(host_, streamFree_[stream]);
+  }
   double d;
   if (p_.link_model && !op.traffic().empty()) {
     d = link_duration(op, start);
@@ -279,38 +298,66 @@ void SimExecutor::launch(const GpuOp &op, int stream) {
       if (s != stream && streamFree_[s] > start) ++busy;
     d = dur(op.cost_us()) * (1.0 + p_.contention * busy);
   }
-  streamFree_[stream] = start + d;
+  lastEnd_[stream] = start + d;
+  used_[stream] = 1;
+  streamFree_[stream] = start + d + (p_.graph ? p_.graph_gap_us : 0.0);
   trace_.push_back({op.name(), stream, start, start + d});
 }
 
 void SimExecutor::event_record(int event, int stream) {
-  host_ += p_.api_us;
   if (event >= int(events_.size())) events_.resize(event + 1, 0.0);
+  if (p_.graph) {
+    double t = lastEnd_[stream];
+    for (double w : pending_[stream]) t = std::max(t, w);
+    events_[event] = t;
+    return;
+  }
+  host_ += p_.api_us;
   events_[event] = std::max(streamFree_[stream], host_);
 }
 
 void SimExecutor::stream_wait_event(int stream, int event) {
+  if (p_.graph) {
+    if (event < int(events_.size())) graph_dep(stream, events_[event]);
+    return;
+  }
   host_ += p_.api_us;
   if (event < int(events_.size()))
     streamFree_[stream] = std::max(streamFree_[stream], events_[event]);
 }
 
 void SimExecutor::event_sync(int event) {
+  if (p_.graph) {
+    if (event < int(events_.size())) host_ = std::max(host_, events_[event]);
+    return;
+  }
   if (event < int(events_.size()) && events_[event] > host_) host_ = events_[event] + p_.sync_us;
   else host_ += p_.api_us;
 }
 
 void SimExecutor::stream_sync(int stream) {
+  if (p_.graph) {
+    host_ = std::max(host_, lastEnd_[stream]);
+    return;
+  }
   if (streamFree_[stream] > host_) host_ = streamFree_[stream] + p_.sync_us;
   else host_ += p_.api_us;
 }
 
 void SimExecutor::stream_wait(int waiter, int waitee) {
+  if (p_.graph) {
+    graph_dep(waiter, lastEnd_[waitee]);
+    return;
+  }
   host_ += 2 * p_.api_us;
   streamFree_[waiter] = std::max(streamFree_[waiter], streamFree_[waitee]);
 }
 
 void SimExecutor::device_sync() {
+  if (p_.graph) {
+    for (double t : lastEnd_) host_ = std::max(host_, t);
+    return;
+  }
   double m = host_;
   for (double t : streamFree_) m = std::max(m, t);
   host_ = m + p_.sync_us;
@@ -319,10 +366,25 @@ void SimExecutor::device_sync() {
 double SimExecutor::run_once(const Sequence &seq) {
   host_ = 0;
   std::fill(streamFree_.begin(), streamFree_.end(), 0.0);
+  std::fill(lastEnd_.begin(), lastEnd_.end(), 0.0);
+  std::fill(used_.begin(), used_.end(), 0);
+  for (auto &pw : pending_) pw.clear();
   events_.assign(events_.size(), 0.0);
   trace_.clear();
   active_.clear();
   for (const auto &e : seq.entries) e.op->run(*this);
+  if (p_.graph) {
+    // replayed back to back: the next iteration starts after the join of every stream used
+    double end = host_;
+    int used = 0;
+    for (int s = 0; s < n_; ++s) {
+      end = std::max(end, lastEnd_[s]);
+      used += used_[s];
+    }
+    if (used > 1) end += p_.graph_join_us + p_.graph_wait_us * double(used - 2);
+    else if (used == 1) end += p_.graph_gap_us;
+    return end;
+  }
   // the sequence ends host-synchronized with all its GPU work (Finish has GPU preds synced)
   double end = host_;
   for (double t : streamFree_) end = std::max(end, t);

@@ -168,6 +168,16 @@ struct SimParams {
                                                {"host", 40.0}};
   /// capacity of a resource class (the text before ':') or of one resource ("xgmi:3")
   std::map<std::string, double> resource_GBps = {{"hbm", 5000.0}, {"xgmi", 120.0}, {"pcie", 50.0}};
+  /// hipGraph replay, the mode the bench searches and times in: no host issue cost (launch_us
+  /// and api_us unused); consecutive ops on one stream are graph_gap_us apart; an op that waits
+  /// on work of other streams starts graph_join_us after the latest of it, plus graph_wait_us
+  /// per further dependency; an iteration ends with the join of every stream it used (one gap
+  /// if it used one). Calibrated on MI355X from device timestamps of unrolled fork/join graphs
+  /// (scripts/stagger_probe.hip, profiles/r5_branch/README.md): 1.0 / 5.5 / 1.2 us.
+  bool graph = false;
+  double graph_gap_us = 1.0;
+  double graph_join_us = 5.5;
+  double graph_wait_us = 1.2;
   double rate_GBps(const std::string &engine) const;
   double capacity_GBps(const std::string &resource) const;
 };
@@ -199,6 +209,8 @@ private:
   /// duration of a GPU op starting at `start` under the link-aware model (registers its
   /// transfers as active on their resources until start + duration)
   double link_duration(const GpuOp &op, double start);
+  /// graph mode: wait (on the device) for work that ends at `t` before the next op of `stream`
+  void graph_dep(int stream, double t);
   int n_;
   SimParams p_;
   std::mt19937_64 rng_;
@@ -207,6 +219,11 @@ private:
   std::map<std::string, std::vector<double>> active_; // resource -> end times of its transfers
   std::vector<double> events_;
   std::vector<Span> trace_;
+  // graph mode: end of each stream's last op, its pending cross-stream dependencies, and
+  // whether the iteration used it
+  std::vector<double> lastEnd_;
+  std::vector<std::vector<double>> pending_;
+  std::vector<char> used_;
 };
 
 class SimBenchmarker : public Benchmarker {

@@ -27,14 +27,18 @@ DEFAULT_RESOURCE_GBPS = {"hbm": 5000.0, "xgmi": 120.0, "pcie": 50.0}
 
 
 def link_sim_params(probe: dict | None = None, matrix: dict | None = None, noise: float = 0.0,
-                    seed: int = 0, **engine_overrides) -> "_tz.SimParams":
+                    seed: int = 0, graph: bool = True, **engine_overrides) -> "_tz.SimParams":
     """SimParams with the link-aware model on. ``probe``: a bench record's ``link_probe`` (one
     transfer's GB/s per transport over one link, and both faces of an axis at once, which
     bounds the link's capacity); ``matrix``: its ``link_matrix`` (every ordered pair, all ranks
     sending at once: per-link capacities ``xgmi:<peer>`` of rank 0's links). Missing fields keep
-    the defaults; ``engine_overrides`` (e.g. ``put=70``) win over both."""
+    the defaults; ``engine_overrides`` (e.g. ``put=70``) win over both. ``graph``: time the
+    sequence as a back-to-back hipGraph replay (``SimParams.graph``: device-side kernel gaps and
+    fork/join costs measured on MI355X), the way the bench searches and times; False: as eager
+    launches from the host."""
     p = _tz.SimParams()
     p.link_model = True
+    p.graph = graph
     p.noise = noise
     p.seed = seed
     eng = dict(DEFAULT_ENGINE_GBPS)

@@ -31,47 +31,60 @@ def _busy_graph(tz, branches: int, us: float):
     return g
 
 
-def branch_probe(tz, rt, branches: int = 3, us: float = 200.0, iters: int = 10):
-    """Microseconds per hipGraph launch of ``branches`` independent ``us``-long single-workgroup
-    kernels, one per stream of ``rt`` (compiled the way the runtime compiles every schedule), and
-    of one such kernel alone. ``ratio`` = all / one: about 1 when the branches run at once,
-    about ``branches`` when they serialize. HIP's graph executor starts each further branch
-    12-25 us after the previous one on MI355X (``stagger_us``; profiles/r5_branch/), so the
-    kernels are long (200 us) for the ratio to tell overlap from serialization. The runtime's
-    mode and unroll are restored; None if the runtime cannot build the graph."""
+def branch_probe(tz, rt, branches: int = 3, us: float = 200.0, iters: int = 10, unroll: int = 10):
+    """Microseconds per run of ``branches`` independent ``us``-long single-workgroup kernels, one
+    per stream of ``rt`` (compiled the way the runtime compiles every schedule), and of one such
+    kernel alone. ``ratio`` = all / one: about 1 when the branches run at once, about
+    ``branches`` when they serialize.
+
+    Two forms: one schedule copy per hipGraphLaunch (``ratio``), and ``unroll`` copies captured
+    into one graph (``unrolled``), which is how the search and the timing replay a schedule.
+    Device timestamps (``scripts/stagger_probe.hip``, profiles/r5_branch/) show why both are
+    kept: with one copy per launch, HIP starts each further branch 4-10 us after the previous one
+    and the next launch 18-27 us after the join; inside an unrolled graph the branches start
+    within ~1 us of each other and a join costs 5-8 us. So the kernels are long (200 us) for the
+    one-copy ratio to tell overlap from serialization. The runtime's mode and unroll are
+    restored; None if the runtime cannot build the graph."""
     from ..search import greedy_schedule
 
     if rt.num_streams() < branches:
         return None
-    mode, unroll = rt.mode, rt.graph_unroll
+    mode, old_unroll = rt.mode, rt.graph_unroll
     rt.set_mode(tz.ExecMode.Graph)
-    rt.set_graph_unroll(1)
 
-    def per_launch(k):
+    def per_run(k, u):
+        rt.set_graph_unroll(u)
         g = _busy_graph(tz, k, us)
         seq = greedy_schedule(g, tz.Platform(rt.num_streams(), symmetric_streams=False),
                               stream_for=lambda n: int(n[len(BRANCH_PREFIX):]))
         rt.prepare(seq)
         if rt.effective_mode != tz.ExecMode.Graph:
             return None
-        rt.run(3)
+        n = iters * u
+        rt.run(u)
         rt.device_sync()
         t0 = time.perf_counter()
-        rt.run(iters)
+        rt.run(n)
         rt.device_sync()
-        return (time.perf_counter() - t0) / iters * 1e6
+        return (time.perf_counter() - t0) / n * 1e6
 
     try:
-        one = per_launch(1)
-        many = per_launch(branches)
+        one = per_run(1, 1)
+        many = per_run(branches, 1)
+        one_u = per_run(1, unroll) if unroll > 1 else None
+        many_u = per_run(branches, unroll) if unroll > 1 else None
     finally:
         rt.set_mode(mode)
-        rt.set_graph_unroll(unroll)
+        rt.set_graph_unroll(old_unroll)
     if not one or not many:
         return None
-    return {"branches": branches, "kernel_us": us, "one_us": round(one, 1),
-            "all_us": round(many, 1), "ratio": round(many / one, 3),
-            "stagger_us": round((many - one) / max(1, branches - 1), 1)}
+    out = {"branches": branches, "kernel_us": us, "one_us": round(one, 1),
+           "all_us": round(many, 1), "ratio": round(many / one, 3),
+           "extra_us_per_branch": round((many - one) / max(1, branches - 1), 1)}
+    if one_u and many_u:
+        out["unrolled"] = {"unroll": unroll, "one_us": round(one_u, 1), "all_us": round(many_u, 1),
+                           "ratio": round(many_u / one_u, 3)}
+    return out
 
 
 def choose_pad(make_rt, probe, pads, threshold: float = 1.5, margin: float = 0.9):

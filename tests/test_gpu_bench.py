@@ -32,6 +32,7 @@ def test_bench_one_rank_subrecords(gpu):
     # the padding the search ran with, and whether 3 graph branches ran at once with it
     bp = j["graph_branch_probe"]
     assert bp["tried"] and bp["tried"][0]["probe"]["ratio"] > 0, bp
+    assert bp["tried"][0]["probe"]["unrolled"]["ratio"] > 0, bp
     assert j["pad_streams"] == bp["pad_streams"]
     assert j["post_timing"]["done"] == ["move_roof", "reference_layout", "baseline_configs"]
     for roof in (j["move_roof"], j["reference_layout"]["move_roof"]):

@@ -409,3 +409,40 @@ def test_halo_ops_report_per_peer_traffic(tz, monkeypatch):
     total = sum(b for res, eng, b in put if res.startswith("xgmi:"))
     assert abs(total - h.exchange_bytes()) < 1.0
     assert {e for r, e, b in seen["he_copyput_all"] if r.startswith("xgmi")} == {"sdma"}
+
+
+def test_graph_replay_sim_matches_the_measured_fork_join_costs(tz):
+    """SimParams.graph: k independent kernels on k streams vs one after another on one stream,
+    replayed back to back, against the MI355X device timestamps of profiles/r5_branch/
+    (stamps_back_to_back.jsonl, 20 us kernels: span + gap to the next copy)"""
+    from tenzing_amd.search import greedy_schedule
+
+    measured = {("forkjoin", 1): 21.0, ("forkjoin", 2): 26.2, ("forkjoin", 3): 27.7,
+                ("forkjoin", 4): 28.6, ("serial", 2): 42.0, ("serial", 3): 63.0,
+                ("serial", 4): 84.0}
+    p = tz.SimParams()
+    p.graph = True
+
+    def sim(k, serial):
+        g = tz.Graph()
+        ops = [tz.SimGpuOp(f"k{i}", 20.0) for i in range(k)]
+        prev = None
+        for op in ops:
+            if serial and prev is not None:
+                g.then(prev, op)
+            else:
+                g.start_then(op)
+            prev = op
+        for op in ops:
+            g.then_finish(op)
+        seq = greedy_schedule(g, tz.Platform(4, symmetric_streams=False),
+                              stream_for=lambda n: 0 if serial else int(n[1:]))
+        return tz.SimExecutor(4, p).run_once(seq)
+
+    for (form, k), us in measured.items():
+        got = sim(k, form == "serial")
+        assert abs(got - us) <= 0.08 * us, (form, k, got, us)
+    # the eager model (the default) charges the host's issue and sync costs instead
+    replay = sim(2, False)
+    p.graph = False
+    assert sim(2, False) > replay
