@@ -37,11 +37,13 @@ def main():
     s, g = build_spmv(SpmvConfig(m=150_000), ctrl, 0)
     rt = tz.HipRuntime(device=0, n_streams=2)
     for form in ("accum", "split"):
-        time_seq(rt, greedy_schedule(g, tz.Platform(2), {"*": [form, "w16"]}), f"spmv_{form}_s0")
+        for k in ("w16", "i4"):
+            time_seq(rt, greedy_schedule(g, tz.Platform(2), {"*": [form, k]}), f"spmv_{form}_{k}_s0")
     del rt, s, g
     h, s, g = build_fused(HaloConfig(n=n, neighbors=26, order="qxyz", fuse="choice"), SpmvConfig(m=150_000), ctrl, 0)
     rt = tz.HipRuntime(device=0, n_streams=4)
-    pref = {"*": ["allfused", "accum", "w16"]}
+    kern = os.environ.get("SPMV_KERNEL", "i4")
+    pref = {"*": ["allfused", "accum", kern]}
     time_seq(rt, greedy_schedule(g, tz.Platform(4), pref), "fused_all_stream0")
     time_seq(rt, greedy_schedule(g, tz.Platform(4), pref,
                                  stream_for=lambda nm: 1 if nm.startswith("he_") else 0), "fused_halo_s1")

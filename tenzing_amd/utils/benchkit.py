@@ -95,7 +95,15 @@ def choose_pad(make_rt, probe, pads, threshold: float = 1.5, margin: float = 0.9
     padding's (a clear gain, not probe noise), else the first (built again if it is not the last
     one probed).
 
+    The ratio judged is the probe's ``unrolled`` one when it has it (the form the search and the
+    timing replay: several schedule copies per graph launch), else its one-copy ``ratio``.
+
     Returns (runtime, record); the record lists every probe in order and the padding chosen."""
+    def judged(r):
+        if not r:
+            return None
+        return (r.get("unrolled") or {}).get("ratio") or r.get("ratio")
+
     tried = []
     best = None  # (ratio, pad)
     rt = None
@@ -105,7 +113,7 @@ def choose_pad(make_rt, probe, pads, threshold: float = 1.5, margin: float = 0.9
         r = probe(rt)
         used = rt.pad_streams if hasattr(rt, "pad_streams") else pad
         tried.append({"pad_streams": used, "probe": r})
-        ratio = r["ratio"] if r else None
+        ratio = judged(r)
         if ratio is not None and ratio <= threshold:
             return rt, {"pad_streams": used, "serialized": False, "tried": tried,
                         "threshold": threshold}
@@ -114,7 +122,7 @@ def choose_pad(make_rt, probe, pads, threshold: float = 1.5, margin: float = 0.9
     if best is None:  # the probe could not run at all: keep the last runtime, say so
         return rt, {"pad_streams": tried[-1]["pad_streams"] if tried else None,
                     "serialized": None, "tried": tried, "threshold": threshold}
-    first = tried[0]["probe"]["ratio"] if tried[0]["probe"] else None
+    first = judged(tried[0]["probe"])
     if first is not None and best[0] > margin * first:  # no padding is clearly better
         best = (first, pads[0], tried[0]["pad_streams"])
     if best[1] != pads[-1]:

@@ -59,6 +59,17 @@ def test_choose_pad_keeps_the_default_when_no_padding_is_clearly_better():
     assert FakeRt.made == [6, 8, 12, 4, 6]
 
 
+def test_choose_pad_judges_the_unrolled_ratio_when_the_probe_has_it():
+    """one copy per launch looks serialized (launch-boundary stagger), the unrolled graph the
+    search replays runs the branches at once: the default padding stays"""
+    FakeRt.made = []
+
+    def probe(rt):
+        return {"ratio": 1.9, "unrolled": {"ratio": 1.05 if rt.pad_streams == 6 else 1.0}}
+    rt, rec = choose_pad(FakeRt, probe, [None, 8, 12, 4])
+    assert rt.pad_streams == 6 and rec["serialized"] is False and FakeRt.made == [6]
+
+
 def test_choose_pad_when_the_probe_cannot_run():
     FakeRt.made = []
     rt, rec = choose_pad(FakeRt, fake_probe({6: None, 8: None}), [None, 8])
