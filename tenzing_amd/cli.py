@@ -111,7 +111,9 @@ def cmd_search(a) -> int:
         rt = tz.HostExecutor(a.streams)
         bench = tz.EmpiricalBenchmarker(rt, ctrl)
     elif a.sim:
-        bench = tz.SimBenchmarker(a.streams)
+        p = tz.SimParams()
+        p.graph = a.mode == "graph"  # time candidates as a replayed hipGraph (measured costs)
+        bench = tz.SimBenchmarker(a.streams, p)
     else:
         mode = tz.ExecMode.Graph if a.mode == "graph" else tz.ExecMode.Eager
         prio = [int(x) for x in a.stream_priorities.split(",")] if a.stream_priorities else []
@@ -393,7 +395,8 @@ def _parser() -> argparse.ArgumentParser:
                    help="stop measuring a candidate once settle-min measurements agree within this ratio")
     s.add_argument("--device-timer", action="store_true",
                    help="time measurements with device events (GPU time) instead of host wall clock")
-    s.add_argument("--mode", default="eager", choices=["eager", "graph"])
+    s.add_argument("--mode", default="eager", choices=["eager", "graph"],
+                   help="with --sim: graph = the hipGraph replay cost model (SimParams.graph)")
     s.add_argument("--graph-unroll", type=int, default=1,
                    help="graph mode: iterations per hipGraph launch while benchmarking")
     s.add_argument("--cu-partition", action="store_true",

@@ -308,7 +308,9 @@ int main(int argc, char **argv) {
     std::unique_ptr<HipRuntime> rt;
     std::unique_ptr<Benchmarker> bench;
     if (sim) {
-      bench = std::make_unique<SimBenchmarker>(streams, SimParams());
+      SimParams sp;
+      sp.graph = a.get("mode", "eager") == "graph"; // a replayed hipGraph's measured costs
+      bench = std::make_unique<SimBenchmarker>(streams, sp);
     } else {
       HipRuntimeOpts ro;
       ro.n_streams = streams;
