@@ -42,7 +42,7 @@ public:
   std::string kind() const override { return "PyCpuOp"; }
   double cost_us() const override { return cost_; }
   void run(Executor &ex) const override {
-    if (!fn_) {
+    if (!fn_ || ex.simulated()) { // the cost model charges the cost; the callback is not run
       ex.host_busy(cost_);
       return;
     }

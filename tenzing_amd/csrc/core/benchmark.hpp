@@ -188,6 +188,7 @@ public:
   int num_streams() const override { return n_; }
   void launch(const GpuOp &op, int stream) override;
   void host_busy(double us) override { host_ += us; }
+  bool simulated() const override { return true; }
   void event_record(int event, int stream) override;
   void stream_wait_event(int stream, int event) override;
   void event_sync(int event) override;

@@ -352,6 +352,9 @@ public:
   virtual void stream_sync(int stream) = 0;
   virtual void stream_wait(int waiter, int waitee) = 0;
   virtual void device_sync() = 0;
+  /// a cost model, not a machine: ops with side effects outside the executor (host transfers
+  /// over the control plane, user callbacks) only charge their cost_us() to host_busy
+  virtual bool simulated() const { return false; }
   /// native handle (hipStream_t) of a logical stream, or nullptr when simulated
   virtual void *native_stream(int stream) { (void)stream; return nullptr; }
   /// logical index of a native stream handle (-1 if it is not one of this executor's)

@@ -415,7 +415,12 @@ public:
   // PCIe copies both ways plus loopback TCP through the hub: ~1 GB/s end to end
   double cost_us() const override { return 50.0 + bytes() / 1.0e3; }
   std::string order_domain() const override { return "host"; }
-  void run(Executor &) const override { h_->host_exchange(dirs_); }
+  void run(Executor &ex) const override {
+    // a hardware-free search (e.g. the bench's model seeds, on rank 0 alone) must not enter
+    // the collective exchange
+    if (ex.simulated()) return ex.host_busy(cost_us());
+    h_->host_exchange(dirs_);
+  }
 
 private:
   std::shared_ptr<const HaloExchange> h_;

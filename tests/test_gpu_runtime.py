@@ -228,7 +228,9 @@ def test_spmv_every_local_kernel_variant(tz, gpu, form):
         assert len(v) == 1, names
         by_variant.setdefault(v[0], seq)
     assert any("rocsparse" in k for k in by_variant), sorted(by_variant)
-    assert len(by_variant) == 5, sorted(by_variant)
+    # lane-group kernels, CSR-stream, the ILP kernels (1 / 2 / 4 lanes) and rocSPARSE
+    assert {"yl_i1", "yl_i2", "yl_i4", "yl_stream"} <= set(by_variant), sorted(by_variant)
+    assert len(by_variant) == 8, sorted(by_variant)
     rt = tz.HipRuntime(device=0, n_streams=2)
     for m in (tz.ExecMode.Eager, tz.ExecMode.Graph):
         rt.set_mode(m)

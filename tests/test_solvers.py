@@ -132,6 +132,15 @@ def test_pycpuop_callback(tz):
     ex.prepare(seq)
     ex.run(5)
     assert len(calls) == 5
+    # the cost model charges a host op's cost and never runs its side effects (a model search
+    # on one rank must not enter, e.g., the halo's collective host exchange)
+    op2 = tz.PyCpuOp("py2", lambda: calls.append(2), 30.0)
+    g2 = tz.Graph()
+    g2.start_then(op2)
+    g2.then_finish(op2)
+    seq2 = tz.get_all_sequences(g2, tz.Platform(1))[0]
+    assert tz.SimExecutor(1, tz.SimParams()).run_once(seq2) >= 30.0
+    assert calls == [1] * 5
 
 
 def test_tree_dump_and_counters(tz, tmp_path):
