@@ -74,6 +74,36 @@ def _build_workload(a, ctrl, device, setup):
     raise SystemExit(f"unknown workload {a.workload}")
 
 
+def _link_record(path: str) -> dict:
+    """the first object holding a ``link_probe`` in a bench record file: one JSON document, or
+    the JSON lines a bench run printed (the last complete line wins), searched recursively"""
+    import json
+
+    text = open(path).read()
+    try:
+        docs = [json.loads(text)]
+    except ValueError:
+        docs = [json.loads(x) for x in text.splitlines() if x.startswith("{")][::-1]
+
+    def find(o):
+        if isinstance(o, dict):
+            if "link_probe" in o:
+                return o
+            o = list(o.values())
+        if isinstance(o, list):
+            for v in o:
+                r = find(v)
+                if r is not None:
+                    return r
+        return None
+
+    for d in docs:
+        r = find(d)
+        if r is not None:
+            return r
+    raise SystemExit(f"--link-model: no record with a link_probe in {path}")
+
+
 def cmd_search(a) -> int:
     import tenzing_amd as tz
     from tenzing_amd.parallel import init_ctrl, select_device
@@ -111,9 +141,17 @@ def cmd_search(a) -> int:
         rt = tz.HostExecutor(a.streams)
         bench = tz.EmpiricalBenchmarker(rt, ctrl)
     elif a.sim:
-        p = tz.SimParams()
-        p.graph = a.mode == "graph"  # time candidates as a replayed hipGraph (measured costs)
-        bench = tz.SimBenchmarker(a.streams, p)
+        if a.link_model is not None:
+            # per-peer link / engine rates (a multi-GPU bench record's, or the defaults)
+            from tenzing_amd.parallel.linkmodel import link_sim_params
+            rec = _link_record(a.link_model) if a.link_model else {}
+            p = link_sim_params(rec.get("link_probe"), rec.get("link_matrix"),
+                                graph=a.mode == "graph")
+        else:
+            p = tz.SimParams()
+            p.graph = a.mode == "graph"  # time candidates as a replayed hipGraph (measured costs)
+        # every rank simulates its own graph; the time of a schedule is the max over ranks
+        bench = tz.SimBenchmarker(a.streams, p, ctrl)
     else:
         mode = tz.ExecMode.Graph if a.mode == "graph" else tz.ExecMode.Eager
         prio = [int(x) for x in a.stream_priorities.split(",")] if a.stream_priorities else []
@@ -167,6 +205,9 @@ def cmd_search(a) -> int:
                    "stop_reason": res.stop_reason, "counters": res.counters(),
                    "skipped": res.failed, "dead_domains": list(res.dead_domains),
                    "pruned_dead": res.pruned_dead, "elapsed_s": time.time() - t0}
+        if a.sim:
+            summary["sim"] = {"graph_replay": a.mode == "graph", "link_model": a.link_model is not None,
+                              "link_record": a.link_model or None}
         if b >= 0:
             summary["best_pct10_ms"] = res.sims[b].res.pct10 * 1e3
             summary["best_schedule"] = json.loads(res.sims[b].seq.json())
@@ -404,6 +445,10 @@ def _parser() -> argparse.ArgumentParser:
     s.add_argument("--stream-priorities", default="",
                    help="comma-separated HIP stream priorities, one per stream (e.g. -1,0)")
     s.add_argument("--sim", action="store_true", help="discrete-event cost model, no GPU")
+    s.add_argument("--link-model", nargs="?", const="", default=None, metavar="RECORD",
+                   help="with --sim: the link-aware model (per-peer xGMI / PCIe / HBM bytes over "
+                        "shared link capacities); RECORD: a multi-GPU bench record whose link_probe "
+                        "and link_matrix give the rates (default: built-in rates)")
     s.add_argument("--replay", default="", help="results CSV to replay instead of running")
     s.add_argument("--seed", type=int, default=0)
     s.add_argument("--no-expand-rollout", action="store_true")

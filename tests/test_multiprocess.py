@@ -282,6 +282,44 @@ def test_relay_search_8_ranks_sim(tmp_path):
     assert len(rows) == 12 and all('"he_rl' in row for row in rows)
 
 
+def test_cli_link_model_search_two_ranks(tmp_path):
+    """`search --sim --mode graph --link-model RECORD` on 2 CPU ranks: the hardware-free search
+    under a recorded bench run's link rates, every rank simulating its own graph (max over
+    ranks)"""
+    import subprocess
+
+    rec = tmp_path / "bench.jsonl"
+    rec.write_text('{"phase": "search", "partial": true}\n' + json.dumps(
+        {"metric": "m", "link_probe": {"GBps": {"put": 70.0, "put_wide": 95.0, "sdma": 48.0},
+                                       "pair_GBps": {"put": 130.0}},
+         "link_matrix": {"why": "", "put_GBps": [[-1, 80.0], [80.0, -1]]}}) + "\n")
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TZ_IPC_GRID="0")
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "tenzing_amd", "search", "--workload", "halo", "--sim",
+             "--mode", "graph", "--link-model", str(rec), "--halo-n", "32", "--fuse", "choice",
+             "--streams", "2", "--iters", "20", "--bench-iters", "2"],
+            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        outs = [p.communicate(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert [p.returncode for p in procs] == [0, 0], [o[1][-1500:] for o in outs]
+    j = json.loads([x for x in outs[0][0].splitlines() if x.startswith('{"workload"')][-1])
+    assert j["sim"] == {"graph_replay": True, "link_model": True, "link_record": str(rec)}
+    assert j["ranks"] == 2 and j["candidates"] == 20 and j["best_pct10_ms"] > 0
+    names = [o["name"] for o in j["best_schedule"]]
+    # the remote directions go through some transport's ops, the local ones stay direct moves
+    assert any(n.startswith("he_") and not n.startswith(("he_direct", "CER", "CSWE")) for n in names), names
+    assert any(n.startswith("he_direct") for n in names), names
+
+
 def body_racing_two_ranks():
     """racing decides on max-over-ranks times, so both ranks stop the same candidates"""
     import tenzing_amd as tz
