@@ -326,6 +326,28 @@ TEST(sim_prefers_overlap) {
   CHECK(worst > 200e-6); // serialized
 }
 
+TEST(sim_graph_replay_costs) {
+  // SimParams::graph on a diamond 10 -> (100 || 100) -> 10: on one stream four ops in a row pay
+  // a 1-us gap each; the best two-stream schedule pays one cross-stream wait on each side of
+  // the overlap (5.5 us after the op it waits on) and the end-of-iteration join of two streams
+  auto g = diamond(10, 100, 100, 10);
+  SimParams p;
+  p.graph = true;
+  for (auto &s : get_all_sequences(*g, Platform::make_n_streams(1), -1)) {
+    SimExecutor ex(1, p);
+    CHECK(std::abs(ex.run_once(s) - (220.0 + 4 * p.graph_gap_us)) < 1e-6);
+  }
+  double best = 1e9;
+  auto seqs = get_all_sequences(*g, Platform::make_n_streams(2), -1);
+  for (auto &s : seqs) {
+    SimExecutor ex(2, p);
+    best = std::min(best, ex.run_once(s));
+  }
+  // k1 [0,10] | k3 on the other stream from 10 + 5.5, k2 after k1 + gap | k4 on k3's stream at
+  // k2's end + 5.5 | + the join
+  CHECK(std::abs(best - (10 + p.graph_join_us + 100 + p.graph_gap_us + 10 + p.graph_join_us)) < 1e-6);
+}
+
 TEST(mcts_finds_good_schedule) {
   auto g = diamond(10, 100, 100, 10);
   SimParams p;
