@@ -30,33 +30,6 @@ import os  # noqa: E402
 import sys  # noqa: E402
 
 
-# which transport an op of a halo schedule belongs to (by op-name prefix)
-VIA_PREFIXES = (("direct", "he_direct_"), ("rccl", "he_shift_"), ("ipc", "he_put_"),
-                ("ipc_wide", "he_putw_"),
-                ("sdma", "he_copyput_"), ("memcpy", "he_mcput_"), ("relay", "he_rl"),
-                ("hostsplit", "he_hs"), ("host", "he_hostxfer"))
-
-
-def schedule_via(names):
-    """Transports a schedule uses, in VIA_PREFIXES order."""
-    return [t for t, key in VIA_PREFIXES if any(n.startswith(key) for n in names)]
-
-
-def remote_via(names):
-    """The transport of the remote directions ("mixed": kernel and copy-engine puts at once;
-    relay and host split carry their share in percent, e.g. "relay20", "hostsplit35")."""
-    via = [t for t in schedule_via(names) if t != "direct"]
-    if "ipc" in via and "sdma" in via:
-        return "mixed"
-    if not via:
-        return None
-    if via[0] in ("relay", "hostsplit"):
-        key = "he_rl" if via[0] == "relay" else "he_hs"
-        share = next(n[len(key):].split("_")[0] for n in names if n.startswith(key))
-        return via[0] + share
-    return via[0]
-
-
 def link_probe(tz, halo, ctrl, iters, rccl=False):
     """GB/s of ONE transfer over one xGMI link with each available transport (the +z face to
     the +z neighbour, every rank at once, one transfer at a time), of both z faces at once
@@ -254,6 +227,7 @@ def main() -> int:
         os.environ["NCCL_SOCKET_IFNAME"] = "lo"
 
     import tenzing_amd as tz
+    from tenzing_amd.utils.benchkit import remote_via, schedule_via
     from tenzing_amd.models import HaloConfig, build_halo
     from tenzing_amd.parallel import init
     from tenzing_amd.utils.env import runtime_libraries

@@ -75,33 +75,14 @@ def _build_workload(a, ctrl, device, setup):
 
 
 def _link_record(path: str) -> dict:
-    """the first object holding a ``link_probe`` in a bench record file: one JSON document, or
-    the JSON lines a bench run printed (the last complete line wins), searched recursively"""
-    import json
+    """the last bench record holding a ``link_probe`` in a file (JSON lines, one document, or
+    any JSON nesting records)"""
+    from tenzing_amd.parallel.linkmodel import load_records
 
-    text = open(path).read()
-    try:
-        docs = [json.loads(text)]
-    except ValueError:
-        docs = [json.loads(x) for x in text.splitlines() if x.startswith("{")][::-1]
-
-    def find(o):
-        if isinstance(o, dict):
-            if "link_probe" in o:
-                return o
-            o = list(o.values())
-        if isinstance(o, list):
-            for v in o:
-                r = find(v)
-                if r is not None:
-                    return r
-        return None
-
-    for d in docs:
-        r = find(d)
-        if r is not None:
-            return r
-    raise SystemExit(f"--link-model: no record with a link_probe in {path}")
+    recs = load_records(path)
+    if not recs:
+        raise SystemExit(f"--link-model: no record with a link_probe in {path}")
+    return recs[-1]
 
 
 def cmd_search(a) -> int:

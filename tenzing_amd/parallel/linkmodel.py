@@ -147,3 +147,121 @@ def sim_seeds(graph, platform, k: int = 2, iters: int = 400, params=None, exclud
         if len(out) >= k:
             break
     return out
+
+
+def find_record(doc):
+    """The first bench record (a dict with ``link_probe``) in ``doc``: a record, a list of them,
+    or any JSON nesting them (a driver's scaling file); None if there is none."""
+    if isinstance(doc, dict):
+        if "link_probe" in doc:
+            return doc
+        doc = list(doc.values())
+    if isinstance(doc, list):
+        for v in doc:
+            r = find_record(v)
+            if r is not None:
+                return r
+    return None
+
+
+def load_records(path: str) -> list:
+    """Every bench record with a ``link_probe`` in a file: one JSON document or JSON lines."""
+    import json
+
+    text = open(path).read()
+    try:
+        docs = [json.loads(text)]
+    except ValueError:
+        docs = [json.loads(x) for x in text.splitlines() if x.strip().startswith("{")]
+    out = []
+
+    def walk(o):
+        if isinstance(o, dict):
+            if "link_probe" in o:
+                out.append(o)
+                return
+            o = list(o.values())
+        if isinstance(o, list):
+            for v in o:
+                walk(v)
+    walk(docs)
+    return out
+
+
+def model_report(record: dict, params=None) -> dict:
+    """How well the link-aware replay model, calibrated on a multi-GPU bench record's own
+    ``link_probe`` / ``link_matrix``, predicts that record's measured seeds: for every remote
+    transport the bench seeded (one greedy schedule each, ``seeded_pct10_ms``), the model's time
+    of the same schedule on rank 0's graph beside the measured one, and the rank correlation of
+    the two orders. Needs no GPU (TZ_IPC_GRID is set to 0 for the receive-buffer transports)."""
+    import os
+
+    from ..utils.benchkit import remote_via
+
+    cfg = record.get("config") or {}
+    size = int(record.get("n_gpus") or 1)
+    streams = int(cfg.get("streams") or 4)
+    p = params if params is not None else link_sim_params(record.get("link_probe"),
+                                                          record.get("link_matrix"))
+    os.environ.setdefault("TZ_IPC_GRID", "0")
+    h, g = headline_graph(0, size, n=int(cfg.get("seq_len") or 512),
+                          neighbors=int(cfg.get("neighbors") or 26),
+                          order=cfg.get("storage_order") or "qxyz",
+                          wide_puts="on" if record.get("wide_puts_offered", True) else "off",
+                          relay="auto" if record.get("relay_offered", True) else "off",
+                          hostsplit="auto" if record.get("hostsplit_offered", True) else "off")
+    platform = _tz.Platform(streams)
+    seeds, _ = transport_seeds(g, platform, streams)
+    measured = record.get("seeded_pct10_ms") or {}
+    rows = []
+    for sq in seeds:
+        via = remote_via([o.name for o in sq.ops()]) or "none"
+        model_us = _tz.SimExecutor(streams, p).run_once(sq)
+        rows.append({"transport": via, "model_us": round(model_us, 1),
+                     "measured_us": round(measured[via] * 1e3, 1) if via in measured else None})
+    both = [r for r in rows if r["measured_us"] is not None]
+    for r in both:
+        r["measured_over_model"] = round(r["measured_us"] / r["model_us"], 3)
+
+    def ranks(v):
+        order = sorted(range(len(v)), key=lambda i: v[i])
+        out = [0.0] * len(v)
+        for k, i in enumerate(order):
+            out[i] = float(k)
+        return out
+
+    rho = None
+    if len(both) >= 3:
+        a, b = ranks([r["model_us"] for r in both]), ranks([r["measured_us"] for r in both])
+        n = len(both)
+        rho = 1 - 6 * sum((x - y) ** 2 for x, y in zip(a, b)) / (n * (n * n - 1))
+    best_model = min(rows, key=lambda r: r["model_us"])["transport"] if rows else None
+    best_meas = min(both, key=lambda r: r["measured_us"])["transport"] if both else None
+    return {"n_gpus": size, "streams": streams, "engine_GBps": dict(p.engine_GBps),
+            "resource_GBps": dict(p.resource_GBps), "seeds": rows, "spearman": rho,
+            "best_by_model": best_model, "best_measured": best_meas,
+            "record_value_ms": record.get("value"),
+            "record_transport": record.get("schedule_transport"),
+            "model_seeded": record.get("model_seeded")}
+
+
+def _main(argv=None) -> int:
+    import argparse
+    import json
+
+    ap = argparse.ArgumentParser(
+        prog="python -m tenzing_amd.parallel.linkmodel",
+        description="model vs measured for every multi-GPU bench record in a file")
+    ap.add_argument("record", help="bench JSON lines, one record, or a file nesting records")
+    a = ap.parse_args(argv)
+    recs = [r for r in load_records(a.record) if (r.get("n_gpus") or 1) > 1]
+    if not recs:
+        print(f"no multi-GPU bench record with a link_probe in {a.record}")
+        return 1
+    for r in recs:
+        print(json.dumps(model_report(r)), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(_main())

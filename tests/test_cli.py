@@ -284,8 +284,7 @@ def test_saved_wide_put_schedule_loads_where_auto_would_not_offer_it():
 def test_bench_names_the_transport_of_a_schedule():
     """bench.py's transport label per schedule (op-name prefixes): kernel puts of either width,
     copy engines, the mix, relay and host-split shares"""
-    sys.path.insert(0, ROOT)
-    import bench
+    from tenzing_amd.utils import benchkit as bench
 
     assert bench.remote_via(["he_direct_self", "he_put_ipc_all"]) == "ipc"
     assert bench.remote_via(["he_direct_self", "he_putw_w_all", "he_wait_w_remote"]) == "ipc_wide"

@@ -455,3 +455,34 @@ def test_graph_replay_sim_matches_the_measured_fork_join_costs(tz):
     replay = sim(2, False)
     p.graph = False
     assert sim(2, False) > replay
+
+
+def test_model_report_compares_a_records_seeds(tz, tmp_path, monkeypatch):
+    """linkmodel.model_report: the model calibrated on a (synthetic) 2-GPU bench record's own
+    link rates, beside the record's measured per-transport seeds, with their rank correlation;
+    the module's CLI finds the records in a file of JSON lines"""
+    import subprocess
+    import sys
+
+    from tenzing_amd.parallel.linkmodel import load_records, model_report
+
+    monkeypatch.setenv("TZ_IPC_GRID", "0")
+    rec = {"n_gpus": 2, "value": 0.3, "schedule_transport": "direct+ipc",
+           "config": {"seq_len": 32, "neighbors": 26, "storage_order": "qxyz", "streams": 2},
+           "link_probe": {"GBps": {"put": 70.0, "put_wide": 95.0, "sdma": 48.0, "memcpy": 45.0},
+                          "pair_GBps": {"put": 130.0}},
+           "link_matrix": {"why": "", "put_GBps": [[-1, 80.0], [80.0, -1]]},
+           "seeded_pct10_ms": {"ipc": 0.05, "sdma": 0.08, "memcpy": 0.09, "mixed": 0.07}}
+    r = model_report(rec)
+    got = {s["transport"]: s for s in r["seeds"]}
+    assert {"ipc", "sdma", "memcpy", "mixed"} <= set(got), got
+    assert all(got[t]["model_us"] > 0 and got[t]["measured_us"] > 0 for t in ("ipc", "sdma"))
+    assert r["best_measured"] == "ipc" and r["spearman"] is not None and -1 <= r["spearman"] <= 1
+    assert r["engine_GBps"]["put"] == 70.0 and r["resource_GBps"]["xgmi:1"] == 80.0
+    path = tmp_path / "bench.jsonl"
+    path.write_text('{"phase": "search"}\n' + json.dumps(rec) + "\n")
+    assert len(load_records(str(path))) == 1
+    out = subprocess.run([sys.executable, "-m", "tenzing_amd.parallel.linkmodel", str(path)],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert json.loads(out.stdout.strip().splitlines()[-1])["best_measured"] == "ipc"
