@@ -689,6 +689,17 @@ def main() -> int:
         post_phase("topology")
         from tenzing_amd.utils.env import xgmi_topology_summary
         post_done("topology", xgmi_topology=xgmi_topology_summary())
+        if args.link_probe_iters > 0 and not stuck:
+            # the link-aware model, calibrated on this run's own link rates, against this run's
+            # measured per-transport seeds (host-only, rank 0, under a second)
+            post_phase("model_check")
+            try:
+                from tenzing_amd.parallel.linkmodel import model_report
+                mc = model_report(out)
+                val = {k: mc[k] for k in ("seeds", "spearman", "best_by_model", "best_measured")}
+            except Exception as e:  # noqa: BLE001 (a diagnostic)
+                val = {"error": f"{type(e).__name__}: {e}"}
+            post_done("model_check", model_check=val)
 
     subrecords = args.subrecords == "on" or (args.subrecords == "auto" and world == 1)
     if subrecords and not stuck and halo.uses_direct():

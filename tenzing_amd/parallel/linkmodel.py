@@ -193,7 +193,7 @@ def model_report(record: dict, params=None) -> dict:
     ``link_probe`` / ``link_matrix``, predicts that record's measured seeds: for every remote
     transport the bench seeded (one greedy schedule each, ``seeded_pct10_ms``), the model's time
     of the same schedule on rank 0's graph beside the measured one, and the rank correlation of
-    the two orders. Needs no GPU (TZ_IPC_GRID is set to 0 for the receive-buffer transports)."""
+    the two orders. Needs no GPU."""
     import os
 
     from ..utils.benchkit import remote_via
@@ -203,13 +203,22 @@ def model_report(record: dict, params=None) -> dict:
     streams = int(cfg.get("streams") or 4)
     p = params if params is not None else link_sim_params(record.get("link_probe"),
                                                           record.get("link_matrix"))
-    os.environ.setdefault("TZ_IPC_GRID", "0")
-    h, g = headline_graph(0, size, n=int(cfg.get("seq_len") or 512),
-                          neighbors=int(cfg.get("neighbors") or 26),
-                          order=cfg.get("storage_order") or "qxyz",
-                          wide_puts="on" if record.get("wide_puts_offered", True) else "off",
-                          relay="auto" if record.get("relay_offered", True) else "off",
-                          hostsplit="auto" if record.get("hostsplit_offered", True) else "off")
+    # the record's IPC mode (puts into the peer's grid, or into receive buffers: the copy-engine,
+    # relay and host-split transports), for the graph's construction only
+    old = os.environ.get("TZ_IPC_GRID")
+    os.environ["TZ_IPC_GRID"] = "1" if record.get("ipc_mode") == "grid" else "0"
+    try:
+        h, g = headline_graph(0, size, n=int(cfg.get("seq_len") or 512),
+                              neighbors=int(cfg.get("neighbors") or 26),
+                              order=cfg.get("storage_order") or "qxyz",
+                              wide_puts="on" if record.get("wide_puts_offered", True) else "off",
+                              relay="auto" if record.get("relay_offered", True) else "off",
+                              hostsplit="auto" if record.get("hostsplit_offered", True) else "off")
+    finally:
+        if old is None:
+            os.environ.pop("TZ_IPC_GRID", None)
+        else:
+            os.environ["TZ_IPC_GRID"] = old
     platform = _tz.Platform(streams)
     seeds, _ = transport_seeds(g, platform, streams)
     measured = record.get("seeded_pct10_ms") or {}

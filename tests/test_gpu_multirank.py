@@ -301,6 +301,13 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     assert set(p["put_GBps_by_axis"]) == {"z"}
     assert (p["pair_GBps"]["sdma"] is not None) == (p["pair_GBps"]["mixed"] is not None) == (mode == "buffers")
     assert p["busiest_link_MB"] > p["face_MB"] > 0 and p["busiest_link_at_probe_rate_ms"] > 0
+    # the model calibrated on these rates, beside the measured per-transport seeds
+    assert j["post_timing"]["done"] == ["link_probe", "link_matrix", "topology", "model_check"]
+    mc = j["model_check"]
+    assert "error" not in mc, mc
+    seeded = {r["transport"]: r for r in mc["seeds"] if r["measured_us"] is not None}
+    assert set(seeded) == set(j["seeded_pct10_ms"]) and all(r["model_us"] > 0 for r in seeded.values()), mc
+    assert mc["best_measured"] in seeded
 
 
 def test_bench_two_ranks_under_mpiexec(gpu):
