@@ -306,8 +306,10 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     mc = j["model_check"]
     assert "error" not in mc, mc
     seeded = {r["transport"]: r for r in mc["seeds"] if r["measured_us"] is not None}
-    assert set(seeded) == set(j["seeded_pct10_ms"]) and all(r["model_us"] > 0 for r in seeded.values()), mc
-    assert mc["best_measured"] in seeded
+    # (grid mode offers the kernel puts alone: nothing seeded, nothing to compare)
+    assert set(seeded) == set(j["seeded_pct10_ms"] or {}), mc
+    assert mc["seeds"] and all(r["model_us"] > 0 for r in mc["seeds"]), mc
+    assert mc["best_measured"] in (seeded or {None: 0})
 
 
 def test_bench_two_ranks_under_mpiexec(gpu):
