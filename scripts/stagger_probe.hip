@@ -188,13 +188,32 @@ int main(int argc, char **argv) {
   for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (double us : {5.0, 20.0, 50.0}) {
     const long long ticks = (long long)(us / tick_us);
-    for (int serial = 0; serial < 2; ++serial) {
+    for (int serial = 0; serial < 3; ++serial) {
       for (int k : {1, 2, 3, 4}) {
-        if (serial && k == 1) continue;
+        if (serial == 1 && k == 1) continue;
         hipGraph_t g;
         hipStream_t s0 = streams[0];
         CK(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
+        std::vector<hipGraphNode_t> prev; // form 2: the previous copy's kernels
         for (int u = 0; u < U; ++u) {
+          if (serial == 2) {
+            // the runtime's form: every kernel captured on ONE stream behind exactly its
+            // dependencies (all kernels of the previous copy), set with
+            // hipStreamUpdateCaptureDependencies
+            std::vector<hipGraphNode_t> cur;
+            for (int i = 0; i < k; ++i) {
+              CK(hipStreamUpdateCaptureDependencies(s0, prev.empty() ? nullptr : prev.data(), prev.size(),
+                                                    hipStreamSetCaptureDependencies));
+              hipLaunchKernelGGL(stamp_k, 1, 64, 0, s0, ticks, du, u * k + i);
+              hipStreamCaptureStatus cs;
+              const hipGraphNode_t *d = nullptr;
+              size_t nd = 0;
+              CK(hipStreamGetCaptureInfo_v2(s0, &cs, nullptr, nullptr, &d, &nd));
+              cur.insert(cur.end(), d, d + nd);
+            }
+            prev = cur;
+            continue;
+          }
           if (serial) {
             for (int i = 0; i < k; ++i)
               hipLaunchKernelGGL(stamp_k, 1, 64, 0, s0, ticks, du, u * k + i);
@@ -242,7 +261,7 @@ int main(int argc, char **argv) {
         };
         std::printf("{\"form\": \"%s\", \"k\": %d, \"kernel_us\": %.0f, \"us_per_copy\": %.1f, "
                     "\"span_us\": %.1f, \"last_start_us\": %.1f, \"gap_to_next_us\": %.1f}\n",
-                    serial ? "unrolled_serial" : "unrolled_forkjoin", k, us, wall, med(span),
+                    serial == 2 ? "unrolled_origin" : serial ? "unrolled_serial" : "unrolled_forkjoin", k, us, wall, med(span),
                     med(last_start), med(gap));
         std::fflush(stdout);
         CK(hipGraphExecDestroy(ge));
