@@ -40,6 +40,8 @@ __global__ void stamp_k(long long ticks, long long *out, int slot) {
   }
 }
 
+__global__ void empty_join_k() {}
+
 __global__ void stamp_seq_k(long long ticks, long long *out, unsigned *counter) {
   // as stamp_k, the slot taken in completion order (a graph replays fixed arguments)
   const long long t0 = wall_clock64();
@@ -188,7 +190,7 @@ int main(int argc, char **argv) {
   for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (double us : {5.0, 20.0, 50.0}) {
     const long long ticks = (long long)(us / tick_us);
-    for (int serial = 0; serial < 3; ++serial) {
+    for (int serial = 0; serial < 4; ++serial) {
       for (int k : {1, 2, 3, 4}) {
         if (serial == 1 && k == 1) continue;
         hipGraph_t g;
@@ -196,6 +198,33 @@ int main(int argc, char **argv) {
         CK(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
         std::vector<hipGraphNode_t> prev; // form 2: the previous copy's kernels
         for (int u = 0; u < U; ++u) {
+          if (serial == 3) {
+            // a join kernel: one empty kernel behind all of the previous copy's kernels, the
+            // next copy's kernels behind it alone (k deps once instead of k x k)
+            if (!prev.empty()) {
+              CK(hipStreamUpdateCaptureDependencies(s0, prev.data(), prev.size(),
+                                                    hipStreamSetCaptureDependencies));
+              hipLaunchKernelGGL(empty_join_k, 1, 64, 0, s0);
+              hipStreamCaptureStatus cs;
+              const hipGraphNode_t *d = nullptr;
+              size_t nd = 0;
+              CK(hipStreamGetCaptureInfo_v2(s0, &cs, nullptr, nullptr, &d, &nd));
+              prev.assign(d, d + nd);
+            }
+            std::vector<hipGraphNode_t> cur;
+            for (int i = 0; i < k; ++i) {
+              CK(hipStreamUpdateCaptureDependencies(s0, prev.empty() ? nullptr : prev.data(), prev.size(),
+                                                    hipStreamSetCaptureDependencies));
+              hipLaunchKernelGGL(stamp_k, 1, 64, 0, s0, ticks, du, u * k + i);
+              hipStreamCaptureStatus cs;
+              const hipGraphNode_t *d = nullptr;
+              size_t nd = 0;
+              CK(hipStreamGetCaptureInfo_v2(s0, &cs, nullptr, nullptr, &d, &nd));
+              cur.insert(cur.end(), d, d + nd);
+            }
+            prev = cur;
+            continue;
+          }
           if (serial == 2) {
             // the runtime's form: every kernel captured on ONE stream behind exactly its
             // dependencies (all kernels of the previous copy), set with
@@ -261,7 +290,7 @@ int main(int argc, char **argv) {
         };
         std::printf("{\"form\": \"%s\", \"k\": %d, \"kernel_us\": %.0f, \"us_per_copy\": %.1f, "
                     "\"span_us\": %.1f, \"last_start_us\": %.1f, \"gap_to_next_us\": %.1f}\n",
-                    serial == 2 ? "unrolled_origin" : serial ? "unrolled_serial" : "unrolled_forkjoin", k, us, wall, med(span),
+                    serial == 3 ? "unrolled_joinkernel" : serial == 2 ? "unrolled_origin" : serial ? "unrolled_serial" : "unrolled_forkjoin", k, us, wall, med(span),
                     med(last_start), med(gap));
         std::fflush(stdout);
         CK(hipGraphExecDestroy(ge));
