@@ -98,7 +98,8 @@ struct FastDiv {
 struct DevDesc {
   double *buf;        // pack/unpack: dense buffer; move: destination array
   const double *src;  // move: source array (grid_off indexes it)
-  int64_t delta;      // move: destination offset - source offset
+  int64_t delta;      // move: destination offset - source offset; widened unpack (make_dev_unpack):
+                      // buffer row length << 32 | elements of padding before each grid row
   int64_t grid_off, s1, s2, s3;
   uint32_t lvec, n1, n2, items;
   FastDiv dl, d1, d2;
@@ -151,6 +152,35 @@ DevDesc make_dev(const BoxDesc &b) {
   d.dl = FastDiv(std::max<uint32_t>(d.lvec, 1));
   d.d1 = FastDiv(std::max<uint32_t>(d.n1, 1));
   d.d2 = FastDiv(std::max<uint32_t>(d.n2, 1));
+  return d;
+}
+
+// An unpack box whose rows may be widened over row padding (BoxDesc::lead / trail): grid rows of
+// lead + len + trail elements written with 16-B stores when that makes them 16-B aligned, each
+// element read from the dense buffer row (clamped into it for the padding elements, whose values
+// nobody reads). Otherwise the plain box.
+DevDesc make_dev_unpack(const BoxDesc &b) {
+  static const bool on = [] { // env TZ_UNPACK_WIDEN=0: exactly the box (A/B)
+    const char *v = std::getenv("TZ_UNPACK_WIDEN");
+    return !v || std::atoi(v) != 0;
+  }();
+  if (!on || (b.lead <= 0 && b.trail <= 0)) return make_dev(b);
+  const int64_t wlen = int64_t(b.lead) + b.len + b.trail;
+  const int64_t goff = b.grid_off - b.lead;
+  if (b.lead < 0 || b.trail < 0 || b.len <= 0 || wlen % 2 != 0 || goff % 2 != 0 || goff < 0 ||
+      b.s1 % 2 != 0 || b.s2 % 2 != 0 || b.s3 % 2 != 0)
+    return make_dev(b);
+  BoxDesc w = b;
+  w.grid_off = goff;
+  w.len = int32_t(wlen);
+  DevDesc d = make_dev(w);
+  d.vec = 2; // the grid side; the buffer is read one element at a time
+  d.lvec = uint32_t(wlen / 2);
+  const uint64_t items = uint64_t(d.lvec) * b.n1 * b.n2 * b.n3;
+  if (items >= (uint64_t(1) << 31)) throw std::runtime_error("box too large for 32-bit indexing");
+  d.items = uint32_t(items);
+  d.dl = FastDiv(std::max<uint32_t>(d.lvec, 1));
+  d.delta = int64_t((uint64_t(uint32_t(b.len)) << 32) | uint32_t(b.lead));
   return d;
 }
 
@@ -220,11 +250,45 @@ __device__ __forceinline__ void box_body(double *__restrict__ grid, const DevDes
   }
 }
 
+// widened unpack (make_dev_unpack): whole 16-B pairs of the widened grid rows, each element from
+// the dense buffer row, padding elements clamped to the row's ends
+template <int U, bool NT>
+__device__ __forceinline__ void unpack_wide_body(double *__restrict__ grid, const DevDesc &d, uint32_t tid,
+                                                 uint32_t nthreads) {
+  const double *__restrict__ buf = d.buf;
+  const uint32_t blen = uint32_t(uint64_t(d.delta) >> 32);
+  const int32_t lead = int32_t(uint32_t(uint64_t(d.delta)));
+  const int32_t last = int32_t(blen) - 1;
+  auto value = [&](uint32_t item) {
+    const uint32_t row = d.dl.div(item);
+    const int32_t x = int32_t(2 * (item - row * d.lvec)) - lead;
+    const double *r = buf + int64_t(row) * blen;
+    dbl2_t v;
+    v.x = r[min(max(x, 0), last)];
+    v.y = r[min(max(x + 1, 0), last)];
+    return v;
+  };
+  uint32_t it = tid;
+  for (; it + (U - 1) * nthreads < d.items; it += U * nthreads) {
+    dbl2_t v[U];
+    int64_t g[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) g[k] = grid_index<2>(d, it + k * nthreads);
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = value(it + k * nthreads);
+#pragma unroll
+    for (int k = 0; k < U; ++k) st<NT>(reinterpret_cast<dbl2_t *>(grid + g[k]), v[k]);
+  }
+  for (; it < d.items; it += nthreads)
+    st<NT>(reinterpret_cast<dbl2_t *>(grid + grid_index<2>(d, it)), value(it));
+}
+
 template <bool UNPACK, int U, bool NT>
 __global__ __launch_bounds__(kThreads) void box_copy_one_k(double *__restrict__ grid, DevDesc d) {
   const uint32_t tid = blockIdx.x * kThreads + threadIdx.x;
   const uint32_t nth = gridDim.x * kThreads;
-  if (d.vec == 2) box_body<2, UNPACK, U, NT>(grid, d, tid, nth);
+  if (UNPACK && d.delta) unpack_wide_body<U, NT>(grid, d, tid, nth);
+  else if (d.vec == 2) box_body<2, UNPACK, U, NT>(grid, d, tid, nth);
   else box_body<1, UNPACK, U, NT>(grid, d, tid, nth);
 }
 
@@ -236,7 +300,8 @@ __global__ __launch_bounds__(kThreads) void box_copy_many_k(double *__restrict__
   const uint32_t nb = b.block_start[box + 1] - b.block_start[box];
   const uint32_t tid = (blockIdx.x - b.block_start[box]) * kThreads + threadIdx.x;
   const uint32_t nth = nb * kThreads;
-  if (d.vec == 2) box_body<2, UNPACK, U, NT>(grid, d, tid, nth);
+  if (UNPACK && d.delta) unpack_wide_body<U, NT>(grid, d, tid, nth);
+  else if (d.vec == 2) box_body<2, UNPACK, U, NT>(grid, d, tid, nth);
   else box_body<1, UNPACK, U, NT>(grid, d, tid, nth);
 }
 
@@ -678,7 +743,7 @@ void halo_check(const double *grid, const HaloGeom &g, unsigned long long *count
 
 void box_copy(double *grid, const BoxDesc &b, bool unpack, void *stream) {
   if (!grid || !b.buf) throw std::runtime_error("box_copy: null grid or buffer");
-  DevDesc d = make_dev(b);
+  DevDesc d = unpack ? make_dev_unpack(b) : make_dev(b);
   if (d.items == 0) return;
   const dim3 grid_dim(blocks_for(d));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -696,7 +761,7 @@ void box_copy_many(double *grid, const BoxDesc *boxes, int n, bool unpack, void 
   if (!grid) throw std::runtime_error("box_copy_many: null grid");
   for (int i = 0; i < n; ++i) {
     if (!boxes[i].buf) throw std::runtime_error("box_copy_many: null buffer");
-    DevDesc d = make_dev(boxes[i]);
+    DevDesc d = unpack ? make_dev_unpack(boxes[i]) : make_dev(boxes[i]);
     if (d.items == 0) continue;
     b.d[b.n] = d;
     b.block_start[b.n] = total;

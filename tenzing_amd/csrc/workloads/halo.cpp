@@ -304,6 +304,8 @@ kern::BoxDesc HaloExchange::pack_box(int i) const {
 kern::BoxDesc HaloExchange::unpack_box(int i) const {
   kern::BoxDesc b = make_box(a_, dirs_[i], true, xoff_, sy_, sz_, sq_);
   if (!recv_.empty()) b.buf = recv_[i].as<double>();
+  // x ghost runs: the unpack's writes may cover the row padding beside them (whole sectors)
+  ghost_widening(dirs_[i].dx, b.grid_off, b.len, b.lead, b.trail);
   return b;
 }
 
@@ -1055,30 +1057,35 @@ std::vector<kern::MoveDesc> HaloExchange::pair_x_moves(const std::vector<kern::M
   return out;
 }
 
-void HaloExchange::widen_to_sectors(int ghostDx, kern::MoveDesc &m) const {
-  // A move whose destination is an x ghost run (side -x: ghost-low, +x: ghost-high) writes a
-  // few elements less than whole 64-B sectors; the rest of those sectors is row padding (x < 0
-  // or x >= n + 2g), whose contents nobody reads. Widening source and destination rows over
-  // that padding turns every x-face write into full-sector writes (a partially written sector
-  // costs the memory a read-modify-write). Row strides are multiples of 16 elements, so the
-  // alignment of the first row holds for every row.
-  if (ghostDx == 0) return;
+void HaloExchange::ghost_widening(int ghostDx, int64_t dstOff, int32_t len, int32_t &lead,
+                                  int32_t &trail) const {
+  // A write of an x ghost run (side -x: ghost-low, +x: ghost-high) covers a few elements less
+  // than whole 64-B sectors; the rest of those sectors is row padding (x < 0 or x >= n + 2g),
+  // whose contents nobody reads. Widening the rows over that padding turns every x-face write
+  // into full-sector writes (a partially written sector costs the memory a read-modify-write).
+  // Row strides are multiples of 16 elements, so the alignment of the first row holds for every
+  // row.
+  lead = trail = 0;
+  if (ghostDx == 0 || a_.ghost_align <= 0) return;
   const int64_t rowLen = pitch_; // elements per (y[,q]) row, a multiple of 16
+  const int64_t A = a_.ghost_align;
   if (ghostDx < 0) {
-    const int64_t A = a_.ghost_align;
-    const int64_t x0 = m.dst_off % rowLen; // ghost-low: padding [0, x0) before it
-    const int64_t e = m.dst_off % A;
-    if (e > x0) return;
-    m.src_off -= e;
-    m.dst_off -= e;
-    m.len += int32_t(e);
+    const int64_t x0 = dstOff % rowLen; // ghost-low: padding [0, x0) before it
+    const int64_t e = dstOff % A;
+    if (e <= x0) lead = int32_t(e);
   } else {
-    const int64_t A = a_.ghost_align;
-    const int64_t end = m.dst_off % rowLen + m.len; // ghost-high: padding [end, rowLen) after
-    const int64_t e = (A - (m.dst_off + m.len) % A) % A;
-    if (end + e > rowLen) return;
-    m.len += int32_t(e);
+    const int64_t end = dstOff % rowLen + len; // ghost-high: padding [end, rowLen) after
+    const int64_t e = (A - (dstOff + len) % A) % A;
+    if (end + e <= rowLen) trail = int32_t(e);
   }
+}
+
+void HaloExchange::widen_to_sectors(int ghostDx, kern::MoveDesc &m) const {
+  int32_t lead = 0, trail = 0;
+  ghost_widening(ghostDx, m.dst_off, m.len, lead, trail);
+  m.src_off -= lead;
+  m.dst_off -= lead;
+  m.len += lead + trail;
 }
 
 std::vector<int> HaloExchange::pipelined_dirs() const {

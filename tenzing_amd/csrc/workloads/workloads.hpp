@@ -575,6 +575,9 @@ private:
   std::vector<kern::MoveDesc> pair_x_moves(const std::vector<kern::MoveDesc> &ms) const;
   static bool move_pairs();
   void widen_to_sectors(int ghostDx, kern::MoveDesc &m) const;
+  /// elements of row padding an x ghost run's writes may also cover before / after each row
+  /// (whole ghost_align units); 0, 0 for other boxes or without line-aligned ghosts
+  void ghost_widening(int ghostDx, int64_t dstOff, int32_t len, int32_t &lead, int32_t &trail) const;
   static constexpr int kDefaultComms = 4;
   bool ipcGrid_ = true;
   std::vector<void *> peerGrid_, peerFlags_; // per rank (nullptr: not a neighbour / self)
