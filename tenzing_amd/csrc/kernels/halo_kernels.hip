@@ -98,7 +98,7 @@ struct FastDiv {
 struct DevDesc {
   double *buf;        // pack/unpack: dense buffer; move: destination array
   const double *src;  // move: source array (grid_off indexes it)
-  int64_t delta;      // move: destination offset - source offset; widened unpack (make_dev_unpack):
+  int64_t delta;      // move: destination offset - source offset; widened unpack (make_dev_wide):
                       // buffer row length << 32 | elements of padding before each grid row
   int64_t grid_off, s1, s2, s3;
   uint32_t lvec, n1, n2, items;
@@ -158,13 +158,13 @@ DevDesc make_dev(const BoxDesc &b) {
 // An unpack box whose rows may be widened over row padding (BoxDesc::lead / trail): grid rows of
 // lead + len + trail elements written with 16-B stores when that makes them 16-B aligned, each
 // element read from the dense buffer row (clamped into it for the padding elements, whose values
-// nobody reads). Otherwise the plain box.
-DevDesc make_dev_unpack(const BoxDesc &b) {
+// nobody reads). Anything else: the plain box.
+DevDesc make_dev_wide(const BoxDesc &b, bool unpack) {
   static const bool on = [] { // env TZ_UNPACK_WIDEN=0: exactly the box (A/B)
     const char *v = std::getenv("TZ_UNPACK_WIDEN");
     return !v || std::atoi(v) != 0;
   }();
-  if (!on || (b.lead <= 0 && b.trail <= 0)) return make_dev(b);
+  if (!unpack || !on || (b.lead <= 0 && b.trail <= 0)) return make_dev(b);
   const int64_t wlen = int64_t(b.lead) + b.len + b.trail;
   const int64_t goff = b.grid_off - b.lead;
   if (b.lead < 0 || b.trail < 0 || b.len <= 0 || wlen % 2 != 0 || goff % 2 != 0 || goff < 0 ||
@@ -250,7 +250,7 @@ __device__ __forceinline__ void box_body(double *__restrict__ grid, const DevDes
   }
 }
 
-// widened unpack (make_dev_unpack): whole 16-B pairs of the widened grid rows, each element from
+// widened unpack (make_dev_wide): whole 16-B pairs of the widened grid rows, each element from
 // the dense buffer row, padding elements clamped to the row's ends
 template <int U, bool NT>
 __device__ __forceinline__ void unpack_wide_body(double *__restrict__ grid, const DevDesc &d, uint32_t tid,
@@ -743,7 +743,7 @@ void halo_check(const double *grid, const HaloGeom &g, unsigned long long *count
 
 void box_copy(double *grid, const BoxDesc &b, bool unpack, void *stream) {
   if (!grid || !b.buf) throw std::runtime_error("box_copy: null grid or buffer");
-  DevDesc d = unpack ? make_dev_unpack(b) : make_dev(b);
+  DevDesc d = make_dev_wide(b, unpack);
   if (d.items == 0) return;
   const dim3 grid_dim(blocks_for(d));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -761,7 +761,7 @@ void box_copy_many(double *grid, const BoxDesc *boxes, int n, bool unpack, void 
   if (!grid) throw std::runtime_error("box_copy_many: null grid");
   for (int i = 0; i < n; ++i) {
     if (!boxes[i].buf) throw std::runtime_error("box_copy_many: null buffer");
-    DevDesc d = unpack ? make_dev_unpack(boxes[i]) : make_dev(boxes[i]);
+    DevDesc d = make_dev_wide(boxes[i], unpack);
     if (d.items == 0) continue;
     b.d[b.n] = d;
     b.block_start[b.n] = total;

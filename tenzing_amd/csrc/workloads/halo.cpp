@@ -298,6 +298,8 @@ kern::BoxDesc halo_detail::make_box(const HaloArgs &a, const HaloExchange::Dir &
 kern::BoxDesc HaloExchange::pack_box(int i) const {
   kern::BoxDesc b = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
   if (!send_.empty()) b.buf = send_[i].as<double>();
+  // (no widening: reading the x-face runs as whole 16-B sectors measured no faster, 48.5-50.1
+  // vs 48.4 us for the 26-box pack, profiles/r5_unpack/; partial reads cost no read-modify-write)
   return b;
 }
 

@@ -405,9 +405,7 @@ void HaloExchange::copy_put_group(const std::vector<int> &dirs, void *stream, bo
   for (int i : dirs) {
     TZ_CHECK(i >= 0 && i < ndirs() && ipc_[i] && send_[i].get() && peerRecv_[size_t(i)],
              "direction " << i << " is not a copy-engine put");
-    kern::BoxDesc b = make_box(a_, dirs_[i], false, xoff_, sy_, sz_, sq_);
-    b.buf = send_[i].as<double>();
-    bs.push_back(b);
+    bs.push_back(pack_box(i)); // into my send buffer of direction i
     arrive.push_back(static_cast<unsigned long long *>(peerFlags_[size_t(nbr_[i])]) + i);
   }
   kern::ipc_wait(static_cast<const unsigned long long *>(flags_) + ndirs(), sent_.as<unsigned long long>(),
