@@ -20,10 +20,9 @@ struct BoxDesc {
   int64_t grid_off = 0;
   int64_t s1 = 0, s2 = 0, s3 = 0;
   int32_t len = 0, n1 = 0, n2 = 0, n3 = 0;
-  /// box_copy / box_copy_many: elements before / after each grid row that the kernel may also
-  /// cover so that short rows (x-face runs of 9 doubles) become whole 16-B-aligned sectors
-  /// accessed with 16-B loads / stores. Unpack: row padding, written with undefined values;
-  /// pack: any cells of the row, only read. 0, 0: exactly the box
+  /// unpack only: elements of row padding before / after each grid row that the writes may
+  /// also cover (their values are undefined), so that short rows (x ghost runs of 9 doubles)
+  /// become whole 16-B-aligned sectors written with 16-B stores; 0, 0: exactly the box
   int32_t lead = 0, trail = 0;
 };
 
