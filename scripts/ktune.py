@@ -40,7 +40,8 @@ def main():
     prev = K.get_box_tuning()
     configs = list(itertools.product([4, 8], [False, True], [False, True], [4096]))
     if a.unrolls:
-        configs = [(int(u), True, ntu, 65535) for u in a.unrolls.split(",") for ntu in (False, True)]
+        configs = [(int(u), ntp, ntu, 65535) for u in a.unrolls.split(",") for ntp in (False, True)
+                   for ntu in (False, True)]
     res = {c: {"pack": [], "shift": [], "unpack": [], "iter": []} for c in configs}
     for _ in range(a.rounds):
         for c in configs:

@@ -130,6 +130,8 @@ py::dict box_to_dict(const kern::BoxDesc &b) {
   d["s2"] = b.s2;
   d["s3"] = b.s3;
   d["len"] = b.len;
+  d["lead"] = b.lead;
+  d["trail"] = b.trail;
   d["n1"] = b.n1;
   d["n2"] = b.n2;
   d["n3"] = b.n3;

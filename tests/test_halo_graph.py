@@ -445,3 +445,37 @@ def test_link_matrix_needs_pairs_and_whole_rows(tz):
     assert lm["why"] == "one rank: no pairs" and lm["put_GBps"] == [[-1.0]]
     with pytest.raises(Exception, match="multiple of 32768"):
         tz._tz.link_matrix(tz._tz.SelfCtrl(), 1000, 2)
+
+
+@pytest.mark.parametrize("order,align", [("qxyz", -2), ("xyzq", 16), ("xyzq", -1)])
+def test_unpack_widening_covers_only_row_padding(tz, order, align):
+    """the unpack's x-ghost rows may be widened to whole ghost_align units, over row padding
+    only: never into the interior, never past the row; none without line-aligned ghosts"""
+    a = tz.HaloArgs()
+    a.nx = a.ny = a.nz = 64
+    a.ghost, a.nq, a.neighbors, a.order, a.ghost_align = 3, 3, 26, order, align
+    h = tz.HaloExchange(a)
+    lay = h.layout()
+    pitch, q, g, xoff = lay["row_pitch_elems"], a.nq, a.ghost, lay["x_offset_cells"]
+    # elements of a row: padding [0, lo), ghost-low, interior, ghost-high, padding [hi, pitch)
+    if order == "qxyz":
+        lo, hi = q * xoff, q * (xoff + a.nx + 2 * g)
+    else:
+        lo, hi = xoff, xoff + a.nx + 2 * g
+    widened = 0
+    for i in range(h.ndirs()):
+        b = h.unpack_box(i)
+        dx = h.dir(i)[0]
+        x0 = b["grid_off"] % pitch
+        if dx == 0 or align == -1:
+            assert b["lead"] == b["trail"] == 0, (i, b)
+            continue
+        assert b["lead"] <= x0 - 0 and x0 - b["lead"] >= 0
+        if b["lead"]:
+            assert dx < 0 and x0 - b["lead"] >= 0 and x0 <= lo + (q * g if order == "qxyz" else g)
+        if b["trail"]:
+            assert dx > 0 and x0 + b["len"] + b["trail"] <= pitch and x0 + b["len"] >= hi
+        # whole units, 16-B aligned
+        assert (x0 - b["lead"]) % 2 == 0 and (b["lead"] + b["len"] + b["trail"]) % 2 == 0
+        widened += b["lead"] + b["trail"] > 0
+    assert (widened > 0) == (align != -1)
