@@ -730,6 +730,8 @@ PYBIND11_MODULE(_tz, m) {
       .def_property_readonly("pad_streams", &HipRuntime::pad_streams,
                              "streams this runtime owns at least (schedule streams + never-used spares)")
       .def("set_graph_unroll", &HipRuntime::set_graph_unroll)
+      .def("precompile", &HipRuntime::precompile, py::arg("n"),
+           "graph mode: compile the n % unroll remainder of a run(n) as one graph (before timing it)")
       .def_property_readonly("graph_unroll", &HipRuntime::graph_unroll)
       .def("set_mode", &HipRuntime::set_mode)
       .def_property_readonly("mode", &HipRuntime::mode)

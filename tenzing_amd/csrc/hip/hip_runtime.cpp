@@ -254,6 +254,11 @@ void HipRuntime::destroy_exec(void *exec) {
 }
 
 void HipRuntime::destroy_graph() {
+  if (graphExecR_) { // always owned here, never by a slot
+    destroy_exec(graphExecR_);
+    graphExecR_ = nullptr;
+    remR_ = 0;
+  }
   if (!slots_.empty()) {
     // the current graphs are borrowed from a slot
     for (Slot &s : slots_) {
@@ -651,6 +656,11 @@ void HipRuntime::prepare_many(const std::vector<Sequence> &seqs) {
 
 void HipRuntime::select(size_t k) {
   TZ_CHECK(k < slots_.size(), "slot " << k << " out of range (" << slots_.size() << ")");
+  if (graphExecR_ && k != slot_) { // the remainder graph belongs to the previous slot's schedule
+    destroy_exec(graphExecR_);
+    graphExecR_ = nullptr;
+    remR_ = 0;
+  }
   const Slot &s = slots_[k];
   seq_ = s.seq;
   graphExec_ = s.exec;
@@ -828,6 +838,20 @@ void HipRuntime::run(int64_t n) {
   if (!slots_.empty() && slot_ < slots_.size()) slots_[slot_].expected = expected_;
 }
 
+void HipRuntime::precompile(int64_t n) {
+  if (!graphExec_ || !graphExecU_ || unroll_ <= 1) return;
+  const int64_t r = n % unroll_;
+  if (r <= 1 || (graphExecR_ && remR_ == r)) return;
+  if (graphExecR_) {
+    destroy_exec(graphExecR_);
+    graphExecR_ = nullptr;
+    remR_ = 0;
+  }
+  size_t nodes = 0, edges = 0;
+  graphExecR_ = build_graph(int(r), nodes, edges);
+  remR_ = r;
+}
+
 void HipRuntime::run_impl(int64_t n) {
   if (graphExec_) {
     hipStream_t origin = S(streams_[0]);
@@ -835,6 +859,10 @@ void HipRuntime::run_impl(int64_t n) {
     if (graphExecU_)
       for (; i + unroll_ <= n; i += unroll_)
         TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExecU_), origin));
+    if (graphExecR_ && n - i == remR_) {
+      TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExecR_), origin));
+      i = n;
+    }
     for (; i < n; ++i) TZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphExec_), origin));
     stream_sync(0);
   } else {

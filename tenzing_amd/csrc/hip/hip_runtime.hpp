@@ -87,6 +87,12 @@ public:
   /// event, and the schedule's closing host syncs precede the last): device seconds
   double run_device_timed(int64_t n) override;
   int64_t batch_multiple() const override { return graphExecU_ ? unroll_ : 1; }
+  /// graph mode with unroll u > 1: also compile a graph of the n % u iterations a run(n) leaves
+  /// after its whole unrolled launches, so that run(n) launches ONE graph for them instead of
+  /// n % u one-iteration graphs (each launch boundary of a multi-stream graph costs ~20 us;
+  /// profiles/r5_branch/). Call it before a timed run(n); kept until the schedule, the unroll or
+  /// the selected slot changes.
+  void precompile(int64_t n);
   /// graph mode: every sequence is compiled once and kept; select() switches without rebuilding
   void prepare_many(const std::vector<Sequence> &seqs) override;
   void select(size_t k) override;
@@ -162,6 +168,8 @@ private:
   Sequence seq_;
   void *graphExec_ = nullptr;  // one iteration
   void *graphExecU_ = nullptr; // unroll_ iterations
+  void *graphExecR_ = nullptr; // remR_ iterations (precompile)
+  int64_t remR_ = 0;
   // the source graph of every instantiated exec, destroyed together with it (not right after
   // instantiation: some HIP releases keep referring to the source graph's nodes from the exec)
   std::unordered_map<void *, void *> graphOf_;

@@ -108,7 +108,9 @@ def run(graph, schedule, streams: int, iters: int = 100, warmup: int = 10, mode:
                         mode=_tz.ExecMode.Graph if mode == "graph" else _tz.ExecMode.Eager,
                         graph_unroll=graph_unroll)
     rt.prepare(schedule)
+    rt.precompile(warmup)
     rt.run(warmup)
+    rt.precompile(iters)  # the remainder of the unroll as one graph, compiled before timing
     rt.device_sync()
     ctrl.barrier()
     t0 = time.perf_counter()

@@ -174,7 +174,13 @@ def timed_replay(tz, rt, ctrl, seq, mode, steps: int, warmup: int):
         rt.set_mode(tz.ExecMode.Eager)
         rt.prepare(seq)
         return None, tz.ExecMode.Eager
+    # a step count that is no multiple of the graph unroll: its remainder runs as one graph too
+    # (compiled here, outside the timed region), not as one-iteration launches
+    if hasattr(rt, "precompile"):
+        rt.precompile(warmup)
     rt.run(warmup)
+    if hasattr(rt, "precompile"):
+        rt.precompile(steps)
     rt.device_sync()
     ctrl.barrier()
     t0 = time.perf_counter()

@@ -136,6 +136,16 @@ def test_graph_mode_iteration_count(tz, gpu, unroll):
         rt.run(7)
         rt.device_sync()
         assert torch.all(y == 7.0), y[:, 0]
+        # the unroll's remainder compiled as one graph (precompile): run(n) still executes n
+        # iterations, whether n has that remainder or another one
+        # (`runs`, not `n`: the ops' closures read `n`, the vector length)
+        for runs in (8, 7, 8, 11):
+            rt.precompile(8)
+            y.zero_()
+            torch.cuda.synchronize()
+            rt.run(runs)
+            rt.device_sync()
+            assert torch.all(y == float(runs)), (runs, y[:, 0])
 
 
 @pytest.mark.parametrize("kind", ["cu_partition", "priorities"])
