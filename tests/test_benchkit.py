@@ -124,3 +124,26 @@ def test_deadline_cancel_after_tighten():
             "print('alive')\n")
     r = _run(code)
     assert r.returncode == 0 and "alive" in r.stdout, (r.stdout, r.stderr)
+
+
+def test_scale_report_rows(tmp_path):
+    """the per-GPU-count table: the final line of each run (partial lines skipped), the floor
+    the run's own link probe gives, weak-scaling efficiency against the N=1 record"""
+    from tenzing_amd.utils.scale_report import records, rows
+
+    def rec(n, ms, partial=False, **kw):
+        return json.dumps({"metric": "m", "value": ms, "n_gpus": n, "partial": partial,
+                           "config": {"rank_grid": [1, 1, n]}, **kw})
+
+    (tmp_path / "n1.jsonl").write_text(rec(1, 0.09, True) + "\n" + rec(1, 0.045) + "\n")
+    (tmp_path / "n2.jsonl").write_text(rec(2, 0.4, link_probe={
+        "GBps": {"put": 70.0}, "busiest_link_at_probe_rate_ms": 0.25},
+        model_check={"spearman": 0.9}) + "\n")
+    rs = rows(records([str(tmp_path / "n2.jsonl"), str(tmp_path / "n1.jsonl")]))
+    assert [r["n_gpus"] for r in rs] == [1, 2] and rs[0]["ms"] == 0.045
+    assert rs[1]["ms_over_link_floor"] == 1.6 and rs[1]["model_spearman"] == 0.9
+    assert rs[1]["weak_efficiency"] == round(0.045 / 0.4, 3)
+    out = subprocess.run([sys.executable, "-m", "tenzing_amd.utils.scale_report",
+                          str(tmp_path / "n1.jsonl"), str(tmp_path / "n2.jsonl")],
+                         capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert out.returncode == 0 and "ms_over_link_floor" in out.stdout, out.stderr
