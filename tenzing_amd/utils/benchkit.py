@@ -17,6 +17,7 @@ halo_run_strategy.hpp:42-49 give the sub-record configurations.
 """
 from __future__ import annotations
 
+import sys
 import time
 
 # which transport an op of a halo schedule belongs to (by op-name prefix)
@@ -176,11 +177,17 @@ def timed_replay(tz, rt, ctrl, seq, mode, steps: int, warmup: int):
         return None, tz.ExecMode.Eager
     # a step count that is no multiple of the graph unroll: its remainder runs as one graph too
     # (compiled here, outside the timed region), not as one-iteration launches
+    def precompile(n):
+        try:
+            rt.precompile(n)
+        except Exception as e:  # noqa: BLE001 (then the remainder runs as one-iteration launches)
+            print(f"timed_replay: no remainder graph for {n} steps: {e}", file=sys.stderr)
+
     if hasattr(rt, "precompile"):
-        rt.precompile(warmup)
+        precompile(warmup)
     rt.run(warmup)
     if hasattr(rt, "precompile"):
-        rt.precompile(steps)
+        precompile(steps)
     rt.device_sync()
     ctrl.barrier()
     t0 = time.perf_counter()
