@@ -374,10 +374,14 @@ def main() -> int:
             # the link-aware model's own best structures (stream splits, transport mixes) as
             # extra seeds: 400 hardware-free iterations on this rank's graph, a fraction of a
             # second; a wrong model costs only these few measurements
-            from tenzing_amd.parallel.linkmodel import sim_seeds
+            from tenzing_amd.parallel.linkmodel import graph_params_from_probe, link_sim_params, sim_seeds
             try:
-                for sq, us in sim_seeds(graph, platform, args.sim_seeds, 400, exclude=seeds,
-                                        seed=args.seed):
+                # the replay model's join cost as this box's branch probe measured it
+                sim_params = graph_params_from_probe(link_sim_params(), branch)
+                report(model_params={"graph_join_us": round(sim_params.graph_join_us, 2),
+                                     "graph_wait_us": sim_params.graph_wait_us})
+                for sq, us in sim_seeds(graph, platform, args.sim_seeds, 400, params=sim_params,
+                                        exclude=seeds, seed=args.seed):
                     seeds.append(sq)
                     sim_seeded.append({"key": sq.canonical_key(), "model_us": round(us, 1),
                                        "transport": remote_via([o.name for o in sq.ops()])})

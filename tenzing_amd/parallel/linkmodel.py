@@ -63,6 +63,26 @@ def link_sim_params(probe: dict | None = None, matrix: dict | None = None, noise
     return p
 
 
+def graph_params_from_probe(params, branch: dict | None):
+    """``params`` with its hipGraph join cost taken from a bench record's ``graph_branch_probe``
+    (the padding in use): the unrolled 3-branch replay's time over the one-branch replay's is
+    one join of 3 streams, i.e. graph_join_us + graph_wait_us (SimParams.graph). Unchanged
+    without an unrolled probe."""
+    if not branch:
+        return params
+    probe = None
+    for t in branch.get("tried") or []:
+        if t.get("pad_streams") == branch.get("pad_streams") and t.get("probe"):
+            probe = t["probe"]
+    u = (probe or {}).get("unrolled") or {}
+    if not u.get("all_us") or not u.get("one_us") or (probe or {}).get("branches") != 3:
+        return params
+    join3 = float(u["all_us"]) - float(u["one_us"])
+    if join3 > 0:
+        params.graph_join_us = max(1.0, join3 - params.graph_wait_us)
+    return params
+
+
 def headline_graph(rank: int, size: int, n: int = 512, neighbors: int = 26, order: str = "qxyz",
                    wide_puts: str = "on", relay: str = "auto", hostsplit: str = "auto"):
     """(halo, graph) of one rank of the bench's N-rank tree, built without a GPU: every remote
@@ -190,7 +210,7 @@ def load_records(path: str) -> list:
 
 def model_report(record: dict, params=None) -> dict:
     """How well the link-aware replay model, calibrated on a multi-GPU bench record's own
-    ``link_probe`` / ``link_matrix``, predicts that record's measured seeds: for every remote
+    ``link_probe`` / ``link_matrix`` (and its join cost on ``graph_branch_probe``), predicts that record's measured seeds: for every remote
     transport the bench seeded (one greedy schedule each, ``seeded_pct10_ms``), the model's time
     of the same schedule on rank 0's graph beside the measured one, and the rank correlation of
     the two orders. Needs no GPU."""
@@ -201,8 +221,9 @@ def model_report(record: dict, params=None) -> dict:
     cfg = record.get("config") or {}
     size = int(record.get("n_gpus") or 1)
     streams = int(cfg.get("streams") or 4)
-    p = params if params is not None else link_sim_params(record.get("link_probe"),
-                                                          record.get("link_matrix"))
+    p = params if params is not None else graph_params_from_probe(
+        link_sim_params(record.get("link_probe"), record.get("link_matrix")),
+        record.get("graph_branch_probe"))
     # the record's IPC mode (puts into the peer's grid, or into receive buffers: the copy-engine,
     # relay and host-split transports), for the graph's construction only
     old = os.environ.get("TZ_IPC_GRID")

@@ -486,3 +486,19 @@ def test_model_report_compares_a_records_seeds(tz, tmp_path, monkeypatch):
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert json.loads(out.stdout.strip().splitlines()[-1])["best_measured"] == "ipc"
+
+
+def test_graph_params_from_the_branch_probe(tz):
+    """the replay model's join cost from a record's graph_branch_probe (the padding in use)"""
+    from tenzing_amd.parallel.linkmodel import graph_params_from_probe, link_sim_params
+
+    branch = {"pad_streams": 6, "tried": [
+        {"pad_streams": 6, "probe": {"branches": 3, "one_us": 207.8, "all_us": 245.1,
+                                     "unrolled": {"unroll": 10, "one_us": 201.4, "all_us": 213.6}}}]}
+    p = graph_params_from_probe(link_sim_params(), branch)
+    assert abs(p.graph_join_us - (213.6 - 201.4 - p.graph_wait_us)) < 1e-9
+    q = graph_params_from_probe(link_sim_params(), None)
+    assert q.graph_join_us == 5.5
+    q = graph_params_from_probe(link_sim_params(), {"pad_streams": 6, "tried": [
+        {"pad_streams": 6, "probe": {"branches": 3, "one_us": 207.8, "all_us": 245.1}}]})
+    assert q.graph_join_us == 5.5  # no unrolled form: the defaults stay
