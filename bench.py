@@ -20,14 +20,139 @@ ranks; the faster mode is reported. `value` = ms per halo-exchange iteration (lo
 """
 from __future__ import annotations
 
+import os
 import time
 
-T_START = time.time()  # the deadline counts from here (before the first, slow, import of torch)
+# the deadline counts from here (before the first, slow, import of torch); ranks this script
+# started itself count from their launcher's start
+T_START = float(os.environ.get("TZ_BENCH_T0", time.time()))
 
 import argparse  # noqa: E402
 import json  # noqa: E402
-import os  # noqa: E402
+import signal  # noqa: E402
+import subprocess  # noqa: E402
 import sys  # noqa: E402
+
+# what a launcher exports: torchrun / torch.distributed.run, MPICH hydra / PMI, MVAPICH, Open MPI,
+# Slurm srun (PMIx)
+_LAUNCHER_VARS = ("WORLD_SIZE", "PMI_SIZE", "PMI_RANK", "PMIX_RANK", "OMPI_COMM_WORLD_SIZE",
+                  "MV2_COMM_WORLD_SIZE")
+_RANK_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+              "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")
+
+
+def launched_world():
+    """The rank count a launcher started this process with, or None when no launcher did
+    (the same rules as the native control plane: parallel/dist.py, MpiCtrl::launcher_size)."""
+    e = os.environ
+    if "WORLD_SIZE" in e:
+        return int(e["WORLD_SIZE"])
+    for v in ("OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "MV2_COMM_WORLD_SIZE"):
+        if v in e:
+            return int(e[v])
+    if "PMIX_RANK" in e or "PMI_RANK" in e:
+        return int(e.get("SLURM_NTASKS", "1"))
+    return None
+
+
+def _free_port() -> int:
+    import socket
+
+    # the control plane listens on MASTER_PORT + 1 (or one of the next 8): keep the pair free
+    for _ in range(64):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        if p < 65000:
+            return p
+    return 29500
+
+
+def spawn_ranks(n: int, argv, deadline_s: float) -> int:
+    """Start `n` fresh rank processes of this script (one per GPU, RANK / WORLD_SIZE /
+    LOCAL_RANK / MASTER_* set, rendezvous over 127.0.0.1) and relay rank 0's result line.
+
+    Runs before anything imports torch or tenzing_amd: this process never touches the GPU and
+    never execs. Exit status: 0 when every rank exited 0; otherwise the first failing rank's
+    status (124 when the ranks outlived the deadline and were killed). A run whose rank 0 printed
+    no line gets a partial one from here, so the failure still says what happened."""
+    port = _free_port()
+    base = {k: v for k, v in os.environ.items() if k not in _RANK_VARS + _LAUNCHER_VARS}
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), TZ_BENCH_T0=repr(T_START), TZ_BENCH_SPAWNED="1")
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        # a session of its own per rank: the whole process group is signalled on the way out
+        procs.append(subprocess.Popen(
+            [sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+            stdout=subprocess.PIPE if r == 0 else sys.stderr, start_new_session=True, text=True))
+
+    def kill(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_signal(sig, _frame):
+        kill(sig)
+        raise SystemExit(128 + sig)
+
+    for s in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(s, on_signal)
+    # rank 0's stdout, line by line on a thread: progress passes through as it comes, and the
+    # JSON line goes to stdout exactly once
+    import threading
+
+    lines = []
+
+    def pump():
+        for line in procs[0].stdout:
+            if line.startswith("{"):
+                lines.append(line.strip())
+            else:
+                sys.stderr.write(line)
+                sys.stderr.flush()
+
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    # the ranks own their deadline (they print a partial line at it); this bound is the
+    # backstop for ranks that cannot even reach theirs
+    limit = (T_START + deadline_s + 30.0) if deadline_s > 0 else None
+    failed_at = None
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        now = time.time()
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad and failed_at is None:
+            failed_at = now  # peers of a failed rank get a grace period to report, then go
+        if (failed_at is not None and now - failed_at > 30.0) or (limit and now > limit):
+            rc = rc or (bad[0] if bad else 124)
+            kill(signal.SIGTERM)
+            time.sleep(5.0)
+            kill(signal.SIGKILL)
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    t.join(timeout=10.0)
+    codes = [p.returncode for p in procs]
+    rc = rc or next((c for c in codes if c != 0), 0)
+    if lines:
+        print(lines[-1], flush=True)
+    elif rc != 0:
+        print(json.dumps({"metric": _METRIC, "value": None, "n_gpus": n, "partial": True,
+                          "phase": "launch", "error": f"rank exit codes {codes}",
+                          "launcher": "bench.py"}), flush=True)
+    if rc != 0:
+        print(f"bench.py: rank exit codes {codes}", file=sys.stderr, flush=True)
+    return rc if rc > 0 else (128 - rc) if rc < 0 else 0
+
+
+_METRIC = "best-schedule iter time (ms) + MCTS search wall-clock, 3D halo-exchange 8 ranks"
 
 
 def link_probe(tz, halo, ctrl, iters, rccl=False):
@@ -140,6 +265,8 @@ def main() -> int:
                          "on other devices, i.e. puts cross xGMI)")
     ap.add_argument("--wide-put-blocks", type=int, default=256,
                     help="workgroups per box of the wide put")
+    ap.add_argument("--copy-puts", default="on", choices=["on", "off"],
+                    help="several ranks, ipc receive buffers: offer copy-engine puts")
     ap.add_argument("--fuse", default="choice",
                     help="choice: the search picks per-direction or fused ops per group")
     ap.add_argument("--mcts-iters", type=int, default=0,
@@ -203,11 +330,12 @@ def main() -> int:
     ap.add_argument("--ghost-align", type=int, default=-2,
                     help="x ghost runs aligned to 16 (line) / 8 (sector) elements, 0 = interior "
                          "rows sector-aligned, -1 = x=0 at the pitched row start (reference), "
-                         "-2 = auto (16 for qxyz, -1 for xyzq)")
+                         "-2 = auto (16, line-aligned, in both orders)")
     ap.add_argument("--subrecords", default="auto", choices=["auto", "on", "off"],
-                    help="after the headline: the reference's XYZQ layout and BASELINE configs 2 "
-                         "(SpMV) and 5 (SpMV + halo), each searched briefly, verified and timed "
-                         "(auto: on one rank only)")
+                    help="after the headline: BASELINE configs 2 (SpMV, band m / ranks) and 5 "
+                         "(SpMV + halo), each searched briefly over this run's transports, "
+                         "verified and timed, and on one rank also the reference's XYZQ layout "
+                         "and the move's roof (auto = on: every rank count; off: none)")
     ap.add_argument("--post-budget-s", type=float, default=150.0,
                     help="once the headline is final: wall-clock budget of the sub-records and "
                          "diagnostics after it; past it the complete line is printed and the run "
@@ -219,6 +347,16 @@ def main() -> int:
                     help="probe whether 3 independent branches of a hipGraph run at once with "
                          "this runtime's stream padding (else try other paddings); recorded")
     args = ap.parse_args()
+
+    # one process per GPU: a launcher (torchrun, mpiexec, srun) may have started the ranks;
+    # otherwise this process starts them itself, before anything touches the GPU
+    launched = launched_world()
+    if launched is None and args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:], args.deadline_s)
+    if (launched or 1) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus}, but the launcher started {launched} rank(s): "
+              "a scaling point must measure the rank count it names", file=sys.stderr)
+        return 2
 
     # one node (every rank local): RCCL's bootstrap over the loopback interface, which always
     # exists, instead of whichever interface it would pick (its data moves over xGMI either way)
@@ -239,10 +377,11 @@ def main() -> int:
     ctrl, device = init()
     rank, world = ctrl.rank, ctrl.size
     if device < 0:
-        print("bench.py: no GPU visible", file=sys.stderr)
+        print(f"bench.py: rank {rank}: no GPU visible", file=sys.stderr)
         return 2
-    if world != args.gpus and rank == 0:
-        print(f"bench.py: warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench.py: rank {rank}: --gpus {args.gpus} but {world} ranks joined", file=sys.stderr)
+        return 2
     cpus = []
     if world > 1:
         # one process per GPU: keep each rank's host threads on the CPUs next to its GPU
@@ -261,12 +400,12 @@ def main() -> int:
                      transport=args.transport, rank_grid=grid, stencil=args.stencil,
                      relay=args.relay, hostsplit=args.hostsplit,
                      hostsplit_chunks=args.hostsplit_chunks, wide_puts=args.wide_puts,
-                     wide_put_blocks=args.wide_put_blocks, ghost_align=args.ghost_align)
+                     wide_put_blocks=args.wide_put_blocks, ghost_align=args.ghost_align,
+                     copy_puts=args.copy_puts == "on")
 
     # the JSON line: every field known up front, so that the deadline can print it partially
     out = {
-        "metric": ("best-schedule iter time (ms) + MCTS search wall-clock, 3D halo-exchange 8 ranks"
-                   if not args.stencil else
+        "metric": (_METRIC if not args.stencil else
                    "best-schedule iter time (ms), 3D halo-exchange + 7-point stencil"),
         "value": None,
         "unit": "ms/iter",
@@ -296,6 +435,11 @@ def main() -> int:
         "partial": True,
         "phase": "setup",
         "deadline_s": args.deadline_s,
+        # who started the ranks: this script itself (no launcher in the environment), torchrun,
+        # or an MPI launcher
+        "launcher": ("bench.py" if os.environ.get("TZ_BENCH_SPAWNED") == "1" else
+                     "mpi" if "WORLD_SIZE" not in os.environ and world > 1 else
+                     "torchrun" if world > 1 else None),
     }
 
     _STATE.update(out=out, rank=rank, deadline=deadline)
@@ -649,6 +793,8 @@ def main() -> int:
                         "hostsplit_fracs": ",".join(str(f) for f in cfg.hostsplit_fracs),
                         "hostsplit_chunks": cfg.hostsplit_chunks,
                         "wide_puts": args.wide_puts, "wide_put_blocks": args.wide_put_blocks,
+                        "copy_puts": args.copy_puts,
+                        "ipc_grid": {"grid": "1", "buffers": "0"}.get(halo.ipc_mode(), "auto"),
                         "stencil": bool(args.stencil), "rank_grid": args.rank_grid},
                "schedule": json.loads(best.json(True))}
         with open(args.save_best, "w") as f:
@@ -689,6 +835,14 @@ def main() -> int:
         except Exception as e:  # noqa: BLE001
             matrix = {"why": str(e)}
         post_done("link_matrix", link_matrix=matrix)
+        if halo.uses_relay():
+            # the relayed share the link model balances with, at equal link rates (offered to
+            # the search) and at this run's own measured rates (for the record)
+            from tenzing_amd.parallel.linkmodel import relay_share, relay_share_from_record
+            f_meas = relay_share_from_record({"config": {"rank_grid": list(halo.rank_grid())},
+                                              "link_matrix": matrix})
+            report(relay_shares={"offered": list(cfg.relay_fracs), "f_star_equal_rates": relay_share(),
+                                 "f_star_link_matrix": round(f_meas, 3) if f_meas else None})
     if rank == 0 and world > 1:
         post_phase("topology")
         from tenzing_amd.utils.env import xgmi_topology_summary
@@ -705,8 +859,8 @@ def main() -> int:
                 val = {"error": f"{type(e).__name__}: {e}"}
             post_done("model_check", model_check=val)
 
-    subrecords = args.subrecords == "on" or (args.subrecords == "auto" and world == 1)
-    if subrecords and not stuck and halo.uses_direct():
+    subrecords = args.subrecords in ("on", "auto")
+    if subrecords and not stuck and world == 1 and halo.uses_direct():
         # the headline's move kernel against a kernel that touches exactly the same lines
         post_phase("move_roof")
         try:
@@ -715,16 +869,20 @@ def main() -> int:
             val = {"error": f"{type(e).__name__}: {e}"}
         post_done("move_roof", move_roof=val)
     if subrecords and not stuck:
-        # the reference driver's layout and the other BASELINE configs, each in this same run
+        # the other BASELINE configs (and, on one rank, the reference driver's layout), each in
+        # this same run; at N > 1 they run over the same transports as the headline
+        ctrl.barrier()  # no peer still reads or writes this rank's headline buffers
         del bench
         rt = None  # the headline's runtime and streams go before the sub-records' are made
         halo = None
-        for name, fn in (("reference_layout", _reference_layout), ("baseline_configs", _baseline_configs)):
+        subs = (("reference_layout", _reference_layout),) if world == 1 else ()
+        for name, fn in subs + (("baseline_configs", _baseline_configs),):
             post_phase(name)
             try:
                 val = fn(tz, args, ctrl, device, branch)
             except Exception as e:  # noqa: BLE001 (a sub-record never costs the headline)
                 val = {"error": f"{type(e).__name__}: {e}"}
+                print(f"bench.py: rank {rank}: {name}: {val['error']}", file=sys.stderr, flush=True)
             out[name] = val
             post_done(name)
 
@@ -793,18 +951,33 @@ def _reference_layout(tz, args, ctrl, device, branch):
     return rec
 
 
+def spmv_via(names):
+    """The x-halo transport of an SpMV schedule: "rccl" (the grouped exchange), "ipc" (kernel
+    puts into the peers' receive buffers) or "local" (one rank: no halo)."""
+    names = [n for n in names if not n.startswith("he_")]
+    if any(n.endswith("exchange") for n in names):
+        return "rccl"
+    if any(n.endswith("put") for n in names):
+        return "ipc"
+    return "local"
+
+
 def _baseline_configs(tz, args, ctrl, device, branch):
-    """BASELINE.json configs 2 and 5 on this GPU, each searched briefly (MCTS, hipGraph
+    """BASELINE.json configs 2 and 5 on this run's ranks, each searched briefly (MCTS, hipGraph
     candidates), verified and timed like the headline:
-      spmv_c2:  CSR SpMV, m = 150,000, nnz = 10 m, band m / ranks, f32, 2 streams
-                (tenzing-dfs/examples/spmv.cu:86-117, tenzing-mcts/examples/spmv_run_strategy.cuh:44-68;
-                BASELINE.md: 0.0094 ms, DFS over hipGraph candidates)
-      fused_c5: that SpMV + the 26-neighbour 512^3 halo in one graph, 4 streams
-                (0.0544 ms)"""
+      spmv_c2:  CSR SpMV, m = 150,000, nnz = 10 m, band m / ranks, f32, 2 streams; between ranks
+                the search chooses RCCL or IPC puts for the x halo
+                (tenzing-dfs/examples/spmv.cu:86-117, tenzing-mcts/examples/spmv_run_strategy.cuh:44-125;
+                BASELINE.md: 0.0094 ms on one rank, DFS over hipGraph candidates)
+      fused_c5: that SpMV + the 26-neighbour 512^3 halo in one graph, 4 streams, the halo over
+                the headline's transports (0.0544 ms on one rank)
+    Each sub-record names the transports its winner used, the matrix's actual nnz (summed over
+    ranks) and the RCCL communicator size."""
     from tenzing_amd.models import HaloConfig, SpmvConfig, build_fused, build_spmv
-    from tenzing_amd.utils.benchkit import search_record
+    from tenzing_amd.utils.benchkit import remote_via, search_record
 
     recs = {}
+    world = ctrl.size
     steps, warmup = max(args.steps, 20), max(args.warmup, 5)
 
     def spmv_verify(rt, s):
@@ -819,17 +992,32 @@ def _baseline_configs(tz, args, ctrl, device, branch):
             return 0 if err < 1e-4 else 1
         return verify
 
+    def spmv_facts(s, rec):
+        names = [n for n in rec.get("schedule_gpu_ops", [])]
+        via = spmv_via(names) if world > 1 else "local"
+        return {"spmv_transport": via,
+                "nnz": int(ctrl.allreduce_sum([float(s.local_nnz() + s.remote_nnz())])[0]),
+                "nnz_target": s.args.nnz, "bw": s.args.bw, "ranks": world,
+                "rccl_nranks": world if via == "rccl" else None,
+                "spmv_transports_offered": ("rccl+ipc" if s.uses_rccl() and s.uses_ipc() else
+                                            "rccl" if s.uses_rccl() else
+                                            "ipc" if s.uses_ipc() else "local")}
+
     sc = SpmvConfig(m=150_000)
     s, g = build_spmv(sc, ctrl, device)
     rt = _sub_runtime(tz, args, device, branch, 2)
     rec = search_record(tz, ctrl, rt, g, 2, spmv_verify(rt, s), steps, warmup, mcts_iters=60,
                         search_unroll=8, seed=args.seed)
-    rec["config"] = {"m": sc.m, "nnz": s.local_nnz() + s.remote_nnz(), "streams": 2,
-                     "dtype": "fp32", "baseline_ms": 0.0094}
+    rec["config"] = {"m": sc.m, "streams": 2, "dtype": "fp32",
+                     "baseline_ms": 0.0094 if world == 1 else None, **spmv_facts(s, rec)}
     recs["spmv_c2"] = rec
     del rt, s, g
 
-    hc = HaloConfig(n=args.n, neighbors=26, order="qxyz", fuse="choice")
+    grid = tuple(int(v) for v in args.rank_grid.lower().split("x")) if args.rank_grid else ()
+    hc = HaloConfig(n=args.n, neighbors=26, order="qxyz", fuse="choice", transport=args.transport,
+                    rank_grid=grid, relay=args.relay, hostsplit=args.hostsplit,
+                    wide_puts=args.wide_puts, wide_put_blocks=args.wide_put_blocks,
+                    copy_puts=args.copy_puts == "on")
     h, s, g = build_fused(hc, SpmvConfig(m=150_000), ctrl, device)
     rt = _sub_runtime(tz, args, device, branch, 4)
     # the largest tree of the BASELINE configs: one greedy seed with every group fused (the
@@ -846,8 +1034,13 @@ def _baseline_configs(tz, args, ctrl, device, branch):
         return b + sv(None)
     rec = search_record(tz, ctrl, rt, g, 4, both, steps, warmup, mcts_iters=60, search_unroll=8,
                         seed=args.seed, seeds=[seed])
+    names = rec.get("schedule_gpu_ops", [])
     rec["config"] = {"halo": f"{args.n}^3 x 3q ghost 3, 26 neighbours, qxyz", "spmv_m": 150_000,
-                     "streams": 4, "baseline_ms": 0.0544}
+                     "streams": 4, "baseline_ms": 0.0544 if world == 1 else None,
+                     "rank_grid": list(h.rank_grid()),
+                     "halo_transport": remote_via(names) or "direct",
+                     "halo_rccl_nranks": h.rccl_nranks() or None,
+                     **spmv_facts(s, rec)}
     recs["fused_c5"] = rec
     del rt
     return recs

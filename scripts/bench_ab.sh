@@ -2,7 +2,7 @@
 # Two settings of the driver's 1-GPU bench, alternating (A B A B ...): the timed value, the
 # search wall-clock and the search's view of the best schedule.
 #   A="--target-secs 0.002" B="--target-secs 0.001" REPS=3 bash scripts/bench_ab.sh
-# (an entry may also start with ENV=value pairs, e.g. A="TZ_HALF_GAP_SIZING=1")
+# (an entry may also start with ENV=value pairs, e.g. A="TZ_PREFLIGHT_S=5")
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/bench_ab

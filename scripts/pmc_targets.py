@@ -20,7 +20,11 @@ def main():
     torch.zeros(1, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     order = os.environ.get("TZ_PMC_ORDER", "qxyz")  # xyzq: the reference driver's layout
-    hd, _ = build_halo(HaloConfig(n=512, neighbors=26, order=order, transport="direct"),
+    # ghost alignment (-1: x = 0 at the row start, the reference's) and extra row pitch
+    align = int(os.environ.get("TZ_PMC_ALIGN", "16"))
+    pad = int(os.environ.get("TZ_PMC_PITCH_PAD", "0"))
+    hd, _ = build_halo(HaloConfig(n=512, neighbors=26, order=order, transport="direct",
+                                  ghost_align=align, pitch_pad=pad),
                        tz.SelfCtrl(), device=0)
     if len(sys.argv) > 2 and sys.argv[1] == "--only-move":
         # steady state of the headline: the 26-direction move back to back, as in the hipGraph

@@ -7,6 +7,7 @@ line per layout. Under `rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --kernel-trace` th
 both kernels (box_move_many_k, line_roof_k) come out per dispatch.
 
   python3 scripts/roof_probe.py [--n 512] [--iters 20] [--layouts qxyz:16,xyzq:-1,xyzq:16]
+  python3 scripts/roof_probe.py --layouts xyzq:-1:0,xyzq:-1:8,xyzq:-1:16,xyzq:-1:32   # pitch sweep
 """
 import argparse
 import json
@@ -22,19 +23,24 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--neighbors", type=int, default=26)
     ap.add_argument("--layouts", default="qxyz:16,xyzq:-1,xyzq:16",
-                    help="order:ghost_align pairs (-1: x = 0 at the row start, the reference)")
+                    help="order:ghost_align[:pitch_pad] (-1: x = 0 at the row start, the reference; "
+                         "pitch_pad: extra row-pitch elements, 528 + pad for 512^3 XYZQ)")
+    ap.add_argument("--pairs", default="on", choices=["on", "off"],
+                    help="XYZQ x self-wrap moves as row pairs (HaloConfig.move_pairs)")
     a = ap.parse_args()
     import tenzing_amd as tz
     from tenzing_amd.models import HaloConfig, build_halo
 
     for spec in a.layouts.split(","):
-        order, align = spec.split(":")
+        order, align, *pad = spec.split(":")
+        pad = int(pad[0]) if pad else 0
         halo, _ = build_halo(HaloConfig(n=a.n, neighbors=a.neighbors, order=order,
-                                        ghost_align=int(align), transport="direct"),
+                                        ghost_align=int(align), transport="direct",
+                                        move_pairs=a.pairs == "on", pitch_pad=pad),
                              tz.SelfCtrl(), 0)
         r = halo.move_roof(a.iters)
-        r.update(order=order, ghost_align=int(align), layout=halo.layout(),
-                 pairs_env=os.environ.get("TZ_MOVE_PAIRS", "1"))
+        r.update(order=order, ghost_align=int(align), pitch_pad=pad, layout=halo.layout(),
+                 move_pairs=a.pairs)
         r["move_over_roof"] = min(r["move_us"], r["move_us_again"]) / r["roof_us"]
         print(json.dumps(r), flush=True)
         del halo

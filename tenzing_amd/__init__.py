@@ -125,6 +125,23 @@ from ._tz import (  # noqa: E402,F401
 
 from .search import run, search  # noqa: E402,F401
 
+
+def _apply_env_options():
+    """Process-wide runtime options from the environment, for programs (bench.py, the CLIs'
+    subprocess tests) that cannot call the setters themselves: TZ_GRAPH_CAPTURE (schedule |
+    child | auto) and TZ_PAD_STREAMS (streams a runtime owns at least). The native library reads
+    neither: both are plain runtime options (``_tz.set_graph_capture``,
+    ``_tz.set_default_pad_streams``) that one process can flip both ways."""
+    v = os.environ.get("TZ_GRAPH_CAPTURE", "")
+    if v:
+        _tz.set_graph_capture(v)
+    v = os.environ.get("TZ_PAD_STREAMS", "")
+    if v:
+        _tz.set_default_pad_streams(max(0, int(v)))
+
+
+_apply_env_options()
+
 __version__ = _tz.version()
 
 NATIVE_PATH = _tz.__file__

@@ -40,7 +40,10 @@ def _build_workload(a, ctrl, device, setup):
                     hostsplit=a.hostsplit,
                     hostsplit_fracs=tuple(float(f) for f in a.hostsplit_fracs.split(",")),
                     hostsplit_chunks=a.hostsplit_chunks, rank_grid=grid,
-                    wide_puts=a.wide_puts, wide_put_blocks=a.wide_put_blocks)
+                    wide_puts=a.wide_puts, wide_put_blocks=a.wide_put_blocks,
+                    ipc_grid=None if a.ipc_grid == "auto" else int(a.ipc_grid),
+                    copy_puts=a.copy_puts == "on", copy_engines=a.copy_engines,
+                    move_pairs=a.move_pairs == "on")
     sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport,
                     matrix=a.spmv_matrix, library=a.spmv_library, distribute=a.spmv_distribute)
     if a.workload == "halo":
@@ -206,6 +209,7 @@ def cmd_search(a) -> int:
 _WORKLOAD_KEYS = ("workload", "noop_width", "streams", "halo_n", "nq", "ghost", "neighbors",
                   "order", "fuse", "transport", "relay", "relay_fracs", "hostsplit",
                   "hostsplit_fracs", "hostsplit_chunks", "wide_puts", "wide_put_blocks",
+                  "ipc_grid", "copy_puts", "copy_engines", "move_pairs",
                   "stencil", "rank_grid",
                   "spmv_m", "spmv_matrix", "spmv_form", "spmv_transport", "spmv_library",
                   "spmv_distribute",
@@ -257,7 +261,7 @@ def load_schedule(doc: dict, ctrl, device: int, setup: bool):
             and not wl["halo"].uses_wide_puts():
         raise SystemExit("the saved schedule uses wide IPC puts (he_putw_*), which this launch "
                          "does not offer: " + wl["halo"].transport_report()["wide_put"] +
-                         " (e.g. TZ_PUT_MAX_BLOCKS equal to --wide-put-blocks, or its preflight "
+                         " (e.g. the put block cap equal to --wide-put-blocks, or its preflight "
                          "failed on this node)")
     seq = tz.OpIndex(g).sequence_from_json(json.dumps(doc["schedule"]))
     bad = tz.verify(seq, tz.resolve_graph(g, seq), w.streams)
@@ -460,7 +464,7 @@ def _parser() -> argparse.ArgumentParser:
     s.add_argument("--transport", default="auto")
     s.add_argument("--relay", default="auto", choices=["auto", "off", "force"],
                    help="halo, 2x2x2 ranks: route a share of every face through the corner peer")
-    s.add_argument("--relay-fracs", default="0.15,0.2",
+    s.add_argument("--relay-fracs", default="0.15,0.2,0.25",
                    help="relayed shares offered to the search (comma-separated)")
     s.add_argument("--hostsplit", default="auto", choices=["auto", "off", "force"],
                    help="halo, ipc receive buffers: send a share of every face through node "
@@ -474,6 +478,15 @@ def _parser() -> argparse.ArgumentParser:
                         "beside the default (auto: when peers sit on other devices)")
     s.add_argument("--wide-put-blocks", type=int, default=256,
                    help="workgroups per box of the wide put")
+    s.add_argument("--ipc-grid", default="auto", choices=["auto", "0", "1"],
+                   help="halo, ipc: puts into the peer's grid (1) or receive buffers (0); auto: "
+                        "TZ_IPC_GRID if set, else the grid below 2 GiB")
+    s.add_argument("--copy-puts", default="on", choices=["on", "off"],
+                   help="halo, ipc receive buffers: offer copy-engine puts")
+    s.add_argument("--copy-engines", type=int, default=1,
+                   help="halo: copy-engine puts of one group over this many streams")
+    s.add_argument("--move-pairs", default="on", choices=["on", "off"],
+                   help="halo, xyzq: x self-wrap moves as row pairs")
     s.add_argument("--stencil", action="store_true",
                    help="halo: add the 7-point stencil (interior beside / shell after the exchange)")
     s.add_argument("--rank-grid", default="", help="halo rank grid PXxPYxPZ (default: prime factors)")

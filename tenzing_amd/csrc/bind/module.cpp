@@ -119,6 +119,9 @@ kern::BoxDesc box_from_dict(const py::dict &d) {
   b.n1 = d["n1"].cast<int>();
   b.n2 = d["n2"].cast<int>();
   b.n3 = d["n3"].cast<int>();
+  // an unpack box's widening over row padding (unpack_box); absent: exactly the box
+  if (d.contains("lead")) b.lead = d["lead"].cast<int>();
+  if (d.contains("trail")) b.trail = d["trail"].cast<int>();
   return b;
 }
 
@@ -217,11 +220,15 @@ PYBIND11_MODULE(_tz, m) {
     d["mode"] = std::string(capture_mode_name(capture_mode()));
     d["forced"] = capture_mode_forced();
     d["rccl_mode"] = std::string(capture_mode_name(rccl_capture_mode()));
-    d["root"] = std::string(graph_root_mode());
     d["pad_streams"] = pad_streams();
     return d;
   }, "how schedules become hipGraphs: capture mode (schedules with RCCL between ranks: the mode "
-     "the RCCL preflight settled on), capture root, stream padding");
+     "the RCCL preflight settled on), default stream padding");
+  m.def("set_graph_capture", &set_graph_capture, py::arg("mode"),
+        "schedule | child: every schedule captured that way; auto: whole-schedule capture, RCCL "
+        "schedules as their preflight found exact (process-wide)");
+  m.def("set_default_pad_streams", &set_default_pad_streams, py::arg("n"),
+        "streams a runtime created with pad_streams=-1 owns at least (process-wide, default 6)");
   m.def("device_by_pci_bus_id", [](const std::string &bus) {
     int d = -1;
     return hipDeviceGetByPCIBusId(&d, bus.c_str()) == hipSuccess ? d : -1;
@@ -972,6 +979,10 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("hostsplit_chunks", &HaloArgs::hostsplit_chunks)
       .def_readwrite("wide_puts", &HaloArgs::wide_puts)
       .def_readwrite("wide_put_blocks", &HaloArgs::wide_put_blocks)
+      .def_readwrite("ipc_grid", &HaloArgs::ipc_grid)
+      .def_readwrite("copy_puts", &HaloArgs::copy_puts)
+      .def_readwrite("copy_engines", &HaloArgs::copy_engines)
+      .def_readwrite("move_pairs", &HaloArgs::move_pairs)
       .def_readwrite("device", &HaloArgs::device)
       .def("json", [](const HaloArgs &a) { return a.json().dump(); });
   py::class_<HaloExchange, std::shared_ptr<HaloExchange>>(m, "HaloExchange")
@@ -1268,6 +1279,12 @@ PYBIND11_MODULE(_tz, m) {
     kern::box_tuning().move_items = n;
   }, py::arg("items"));
   k.def("get_move_items", []() { return kern::box_tuning().move_items; });
+  k.def("set_peel_moves", [](bool on) { kern::box_tuning().peel_moves = on; }, py::arg("on"),
+        "moves of rows one element past a 16-B boundary: peel it and move the rest 16 B at a time");
+  k.def("get_peel_moves", []() { return kern::box_tuning().peel_moves; });
+  k.def("set_widen_unpack", [](bool on) { kern::box_tuning().widen_unpack = on; }, py::arg("on"),
+        "unpack boxes with lead / trail write their widened rows with 16-B stores");
+  k.def("get_widen_unpack", []() { return kern::box_tuning().widen_unpack; });
   k.def("get_box_tuning", []() {
     const auto &t = kern::box_tuning();
     return py::make_tuple(t.unroll, t.nt_pack, t.nt_unpack, t.max_blocks, t.nt_move);

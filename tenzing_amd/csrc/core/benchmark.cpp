@@ -50,9 +50,7 @@ Json BenchOpts::json() const {
 // ---------------------------------------------------------------- Empirical
 
 EmpiricalBenchmarker::EmpiricalBenchmarker(ExecutorRunner &runner, Ctrl &ctrl)
-    : runner_(runner), ctrl_(ctrl) {
-  if (const char *e = std::getenv("TZ_HALF_GAP_SIZING")) halfGapSizing_ = std::atoi(e) != 0;
-}
+    : runner_(runner), ctrl_(ctrl) {}
 
 EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, double targetSecs,
                                                                 bool deviceTimer) {
@@ -84,17 +82,13 @@ EmpiricalBenchmarker::Measurement EmpiricalBenchmarker::measure(int64_t nHint, d
     if (elapsed < targetSecs) {
       const double perSample = std::max(elapsed / double(m.n), 1e-9);
       const double est = targetSecs / perSample * 1.1;
-      if (halfGapSizing_) {
-        m.n += int64_t(std::ceil((est - double(m.n)) * 0.5));
-      } else {
-        // a batch that ran for an eighth of the target or more is long enough to time, so it
-        // sizes the next batch directly (the 10 % margin lands it past the target); a shorter
-        // one is dominated by launch latency and grows 8x at most. A candidate is sized in ~3
-        // runs (about 1.3x the target) instead of ~6 runs (about 4.5x) when closing half the
-        // gap per run.
-        const int64_t jump = int64_t(std::ceil(est));
-        m.n = elapsed >= targetSecs / 8 ? jump : std::min(jump, m.n * 8);
-      }
+      // a batch that ran for an eighth of the target or more is long enough to time, so it
+      // sizes the next batch directly (the 10 % margin lands it past the target); a shorter
+      // one is dominated by launch latency and grows 8x at most. A candidate is sized in ~3
+      // runs (about 1.3x the target) instead of ~6 runs (about 4.5x) when closing half the gap
+      // per run (the round-1 rule, retired after its A/B)
+      const int64_t jump = int64_t(std::ceil(est));
+      m.n = elapsed >= targetSecs / 8 ? jump : std::min(jump, m.n * 8);
       m.n = std::max<int64_t>(m.n, 1);
       const int64_t k = std::max<int64_t>(1, runner_.batch_multiple());
       m.n = (m.n + k - 1) / k * k;
@@ -255,21 +249,27 @@ double SimExecutor::link_duration(const GpuOp &op, double start) {
   std::map<std::pair<std::string, std::string>, double> per;
   for (const Traffic &t : tr)
     if (t.bytes > 0) per[{t.resource, t.engine}] += t.bytes;
-  double slowest = 0;
-  for (const auto &kv : per) {
-    const std::vector<double> &ends = active_[kv.first.first];
-    int k = 0;
-    for (double e : ends) k += e > start;
-    const double rate = std::min(p_.rate_GBps(kv.first.second),
-                                 p_.capacity_GBps(kv.first.first) / double(k + 1));
-    slowest = std::max(slowest, kv.second / (rate * 1e3)); // GB/s = 1e3 bytes per us
-  }
-  const double d = dur(op.latency_us() + slowest);
-  for (const auto &kv : per) {
-    std::vector<double> &ends = active_[kv.first.first];
-    ends.erase(std::remove_if(ends.begin(), ends.end(), [&](double e) { return e <= start; }), ends.end());
-    ends.push_back(start + d);
-  }
+  // A transfer shares its resource with the transfers whose [start, end) overlaps its own.
+  // Ops are simulated in program order, not in start-time order (an op issued earlier on another
+  // stream may start later), so every interval is kept and tested for overlap; the op's own
+  // end depends on how many it shares with, so the estimate is refined once (alone -> with the
+  // overlaps of that window -> with the overlaps of the longer window).
+  auto duration = [&](double window) {
+    double slowest = 0;
+    for (const auto &kv : per) {
+      int k = 0;
+      for (const auto &iv : active_[kv.first.first]) k += iv.first < start + window && iv.second > start;
+      const double rate = std::min(p_.rate_GBps(kv.first.second),
+                                   p_.capacity_GBps(kv.first.first) / double(k + 1));
+      slowest = std::max(slowest, kv.second / (rate * 1e3)); // GB/s = 1e3 bytes per us
+    }
+    return op.latency_us() + slowest;
+  };
+  double est = duration(0.0); // (window 0: nothing overlaps an empty window)
+  est = duration(est);
+  est = duration(est);
+  const double d = dur(est);
+  for (const auto &kv : per) active_[kv.first.first].push_back({start, start + d});
   return d;
 }
 

@@ -120,9 +120,6 @@ private:
   double best_ = 0.0; // best complete pct10 seen (racing); identical on every rank
   int64_t raced_ = 0;
   int64_t settled_ = 0;
-  // batch sizing closes half the gap to the target per run (round-1 rule, env
-  // TZ_HALF_GAP_SIZING=1 for A/B runs; must be the same on every rank)
-  bool halfGapSizing_ = false;
 };
 
 /// Host-only executor: GPU ops are launched with a null stream, synchronously (tests/CPU runs).
@@ -217,7 +214,8 @@ private:
   std::mt19937_64 rng_;
   double host_ = 0;
   std::vector<double> streamFree_;
-  std::map<std::string, std::vector<double>> active_; // resource -> end times of its transfers
+  // resource -> [start, end) of every transfer of this run on it
+  std::map<std::string, std::vector<std::pair<double, double>>> active_;
   std::vector<double> events_;
   std::vector<Span> trace_;
   // graph mode: end of each stream's last op, its pending cross-stream dependencies, and

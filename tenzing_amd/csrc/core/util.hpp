@@ -58,7 +58,7 @@ struct Counters {
 
 /// RAII timer that adds its lifetime into a Counters entry.
 /// Optional trace-range hooks. The core stays free of ROCm dependencies; the HIP layer installs
-/// roctx push/pop here (env TZ_ROCTX=1), so rocprofv3 --marker-trace shows MCTS phases and
+/// roctx push/pop here (env TZ_TRACE=roctx), so rocprofv3 --marker-trace shows MCTS phases and
 /// schedule ops as named ranges next to the kernels.
 struct TraceHooks {
   void (*push)(const char *) = nullptr;

@@ -49,9 +49,13 @@ static hipEvent_t E(void *p) { return static_cast<hipEvent_t>(p); }
 HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
     : mode_(opts.mode), unroll_(std::max(1, opts.graph_unroll)), spinSync_(opts.spin_sync),
       watchdogS_(opts.watchdog_s), watchdogK_(opts.watchdog_k) {
-  if (const char *v = std::getenv("TZ_SPIN_SYNC")) spinSync_ = std::atoi(v) != 0;
-  if (const char *v = std::getenv("TZ_ROCTX")) enable_roctx(std::atoi(v) != 0);
-  if (const char *v = std::getenv("TZ_TRACE_OPS")) traceOps_ = std::atoi(v) != 0;
+  // TZ_TRACE: comma-separated "roctx" (the core's trace ranges to roctx) and / or "ops" (name
+  // every op on stderr as eager mode issues it: hang diagnosis)
+  if (const char *v = std::getenv("TZ_TRACE")) {
+    const std::string t = std::string(",") + v + ",";
+    if (t.find(",roctx,") != std::string::npos) enable_roctx(true);
+    if (t.find(",ops,") != std::string::npos) traceOps_ = true;
+  }
   TZ_CHECK(opts.n_streams >= 1, "need at least one stream");
   if (opts.device >= 0) TZ_HIP(hipSetDevice(opts.device));
   TZ_HIP(hipGetDevice(&device_));
@@ -421,24 +425,22 @@ void *HipRuntime::build_graph(int iterations, size_t &nodesOut, size_t &edgesOut
   }
 }
 
-CaptureMode capture_mode() {
-  static const CaptureMode m = [] {
-    const char *v = std::getenv("TZ_GRAPH_CAPTURE");
-    const std::string how = v ? v : "schedule";
-    if (how == "child") return CaptureMode::Child;
-    TZ_CHECK(how == "schedule", "TZ_GRAPH_CAPTURE must be schedule or child (got " << how << ")");
-    return CaptureMode::Schedule;
-  }();
-  return m;
-}
-
-bool capture_mode_forced() {
-  static const bool forced = std::getenv("TZ_GRAPH_CAPTURE") != nullptr;
-  return forced;
-}
-
 namespace {
+std::atomic<int> g_capture{int(CaptureMode::Schedule)};
+std::atomic<bool> g_captureForced{false};
 std::atomic<int> g_rcclCapture{int(CaptureMode::Schedule)};
+std::atomic<int> g_padStreams{6};
+} // namespace
+
+CaptureMode capture_mode() { return CaptureMode(g_capture.load()); }
+
+bool capture_mode_forced() { return g_captureForced.load(); }
+
+void set_graph_capture(const std::string &how) {
+  TZ_CHECK(how == "schedule" || how == "child" || how == "auto",
+           "graph capture must be schedule, child or auto (got " << how << ")");
+  g_capture = int(how == "child" ? CaptureMode::Child : CaptureMode::Schedule);
+  g_captureForced = how != "auto";
 }
 
 CaptureMode rccl_capture_mode() {
@@ -469,48 +471,13 @@ GraphBuilder::GraphBuilder(const std::vector<void *> &streams, CaptureMode mode)
   TZ_LOG(Debug, "capture: begin");
   TZ_HIP(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
   capturing_ = true;
-  const std::string root = graph_root_mode();
-  if (root == "none") return;
-  try {
-    if (root == "kernel") {
-      kern::empty(origin);
-    } else {
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      hipGraph_t g = nullptr;
-      TZ_HIP(hipStreamGetCaptureInfo_v2(origin, &cs, nullptr, &g, nullptr, nullptr));
-      hipGraphNode_t n = nullptr;
-      TZ_HIP(hipGraphAddEmptyNode(&n, g, nullptr, 0));
-      TZ_HIP(hipStreamUpdateCaptureDependencies(origin, &n, 1, hipStreamSetCaptureDependencies));
-    }
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    const hipGraphNode_t *d = nullptr;
-    size_t nd = 0;
-    TZ_HIP(hipStreamGetCaptureInfo_v2(origin, &cs, nullptr, nullptr, &d, &nd));
-    TZ_CHECK(nd == 1, "graph root: " << nd << " capture dependencies after the root");
-    root_ = d[0];
-  } catch (...) {
-    abandon();
-    throw;
-  }
 }
 
-int pad_streams() {
-  static const int n = [] {
-    const char *v = std::getenv("TZ_PAD_STREAMS");
-    return v ? std::max(0, std::atoi(v)) : 6;
-  }();
-  return n;
-}
+int pad_streams() { return g_padStreams.load(); }
 
-const char *graph_root_mode() {
-  static const std::string m = [] {
-    const char *v = std::getenv("TZ_GRAPH_ROOT");
-    const std::string how = v ? v : "none";
-    TZ_CHECK(how == "kernel" || how == "empty" || how == "none",
-             "TZ_GRAPH_ROOT must be kernel, empty or none (got " << how << ")");
-    return how;
-  }();
-  return m.c_str();
+void set_default_pad_streams(int n) {
+  TZ_CHECK(n >= 0 && n <= 64, "pad streams must be in [0, 64] (got " << n << ")");
+  g_padStreams = n;
 }
 
 GraphBuilder::~GraphBuilder() { abandon(); }
@@ -569,7 +536,6 @@ std::vector<void *> GraphBuilder::add(int stream, const std::vector<void *> &dep
   // recursed without end when RCCL's streams had joined the capture through other forked
   // streams (profiles/r4_capture/self_torchrt2.log)
   hipStream_t origin = S(streams_[0]);
-  if (deps.empty() && root_) deps.push_back(static_cast<hipGraphNode_t>(root_)); // one root
   TZ_LOG(Debug, "capture: op of stream " << stream << " behind " << deps.size() << " node(s)");
   TZ_HIP(hipStreamUpdateCaptureDependencies(origin, deps.empty() ? nullptr : deps.data(), deps.size(),
                                             hipStreamSetCaptureDependencies));

@@ -50,7 +50,7 @@ struct HipRuntimeOpts {
   double watchdog_s = 0;       // deadline floor per run, seconds (0 = no watchdog)
   double watchdog_k = 50;      // ... plus this many times the expected time of the run
   int graph_unroll = 1;        // iterations per hipGraph launch in Graph mode
-  bool spin_sync = true;       // host syncs busy-poll (env TZ_SPIN_SYNC=0/1 overrides)
+  bool spin_sync = true;       // host syncs busy-poll (blocking waits measured no faster)
   int pad_streams = -1;        // streams owned at least (spares never used); -1: pad_streams()
 };
 
@@ -198,14 +198,14 @@ private:
   std::shared_ptr<std::atomic<int>> abortsPending_ = std::make_shared<std::atomic<int>>(0);
   std::atomic<bool> stop_{false};
   std::thread watchdog_;
-  bool traceOps_ = false; // env TZ_TRACE_OPS: name every op on stderr as eager mode issues it
+  bool traceOps_ = false; // TZ_TRACE=ops: name every op on stderr as eager mode issues it
 };
 
 /// Chrome trace-event JSON (chrome://tracing, Perfetto) of a traced timeline: one track per
 /// stream plus a host track
 Json chrome_trace(const std::vector<HipRuntime::Span> &spans);
 
-/// How a schedule becomes a hipGraph (env TZ_GRAPH_CAPTURE):
+/// How a schedule becomes a hipGraph (set_graph_capture; python: TZ_GRAPH_CAPTURE at import):
 ///  * Schedule (default): ONE stream capture for the whole schedule. It begins on the origin
 ///    stream, is forked to the other streams by an event, every op is enqueued in issue order
 ///    on its own stream with that stream's capture dependencies set to exactly the nodes the
@@ -217,10 +217,14 @@ Json chrome_trace(const std::vector<HipRuntime::Span> &spans);
 ///    node. Kept only for A/B diagnosis: HIP runs child-graph nodes one after another, so it
 ///    costs all branch concurrency (profiles/r3b_rccl_loopback/child_graph_overlap.jsonl).
 enum class CaptureMode { Schedule, Child };
-/// the mode for schedules without RCCL between ranks (env TZ_GRAPH_CAPTURE, default Schedule)
+/// the mode for schedules without RCCL between ranks (default Schedule)
 CaptureMode capture_mode();
-/// whether TZ_GRAPH_CAPTURE was set (then it holds for every schedule, RCCL ones included)
+/// whether a mode was forced by set_graph_capture (then it holds for every schedule, RCCL ones
+/// included)
 bool capture_mode_forced();
+/// "schedule" or "child": force that mode for every schedule; "auto": Schedule, and for RCCL
+/// schedules whatever the RCCL preflight found exact (process-wide)
+void set_graph_capture(const std::string &mode);
 /// the mode for schedules with RCCL ops between ranks: whichever the RCCL preflight found exact
 /// on every rank (Schedule first, Child as the fallback); Schedule until a preflight sets it
 CaptureMode rccl_capture_mode();
@@ -258,16 +262,15 @@ private:
   CaptureMode mode_;
   void *graph_ = nullptr; // Child: the graph being assembled
   bool capturing_ = false;
-  void *root_ = nullptr;  // Schedule: the single root every op without dependencies follows
 };
 
-/// The root of a whole-schedule capture (env TZ_GRAPH_ROOT): "none" (default) = the ops without
-/// dependencies are the graph's roots, "kernel" = an empty kernel that every such op follows,
-/// "empty" = a graph empty node. A/B on one MI355X (profiles/r4_root/): a single root changes
-/// neither the branch probes nor the RCCL probe, and costs the headline 0.2-0.9 %
-const char *graph_root_mode();
-/// streams a runtime owns at least (env TZ_PAD_STREAMS, default 6; the spare ones are never used)
+/// streams a runtime owns at least when its options say -1 (default 6; the spare ones are never
+/// used: they keep hipGraph branch streams off the launch stream's hardware queue,
+/// profiles/r4_pad/). (A single root node per captured schedule was measured too and retired:
+/// it changed neither the branch probes nor the RCCL probe, profiles/r4_root/.)
 int pad_streams();
+/// set the default above (process-wide; python: TZ_PAD_STREAMS at import)
+void set_default_pad_streams(int n);
 
 /// route the core's trace ranges (MCTS phases, schedule ops in eager runs) to roctx
 void enable_roctx(bool on);

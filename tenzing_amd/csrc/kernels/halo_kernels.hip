@@ -36,34 +36,10 @@ namespace tz {
 namespace kern {
 
 BoxTuning &box_tuning() {
-  static BoxTuning t = [] {
-    BoxTuning v;
-    if (const char *e = std::getenv("TZ_PUT_MAX_BLOCKS")) v.put_max_blocks = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("TZ_NT_MOVE_STORE")) v.nt_move_store = std::atoi(e) != 0;
-    if (const char *e = std::getenv("TZ_NT_MOVE_LOAD")) v.nt_move = std::atoi(e) != 0;
-    if (const char *e = std::getenv("TZ_MOVE_UNROLL")) {
-      const int u = std::atoi(e);
-      if (u == 1 || u == 2 || u == 4) v.move_unroll = u;
-      else std::fprintf(stderr, "[tz] warning: TZ_MOVE_UNROLL=%s is not 1, 2 or 4; using %d\n", e, v.move_unroll);
-    }
-    if (const char *e = std::getenv("TZ_NT_PACK")) v.nt_pack = std::atoi(e) != 0;
-    if (const char *e = std::getenv("TZ_NT_UNPACK")) v.nt_unpack = std::atoi(e) != 0;
-    if (const char *e = std::getenv("TZ_XCD_REMAP")) {
-      const int m = std::atoi(e);
-      if (m >= 0 && m <= 2) v.xcd_remap = m;
-      else std::fprintf(stderr, "[tz] warning: TZ_XCD_REMAP=%s is not 0, 1 or 2; using 0\n", e);
-    }
-    return v;
-  }();
+  // process-wide launch tuning, changed only through its setters (bindings: kernels.set_*);
+  // no environment overrides: every option can be flipped both ways inside one process
+  static BoxTuning t;
   return t;
-}
-
-bool peel_moves() {
-  static const bool on = [] {
-    const char *v = std::getenv("TZ_MOVE_PEEL");
-    return !v || std::atoi(v) != 0;
-  }();
-  return on;
 }
 
 void set_xcd_remap(int mode) {
@@ -160,11 +136,7 @@ DevDesc make_dev(const BoxDesc &b) {
 // element read from the dense buffer row (clamped into it for the padding elements, whose values
 // nobody reads). Anything else: the plain box.
 DevDesc make_dev_wide(const BoxDesc &b, bool unpack) {
-  static const bool on = [] { // env TZ_UNPACK_WIDEN=0: exactly the box (A/B)
-    const char *v = std::getenv("TZ_UNPACK_WIDEN");
-    return !v || std::atoi(v) != 0;
-  }();
-  if (!unpack || !on || (b.lead <= 0 && b.trail <= 0)) return make_dev(b);
+  if (!unpack || !box_tuning().widen_unpack || (b.lead <= 0 && b.trail <= 0)) return make_dev(b);
   const int64_t wlen = int64_t(b.lead) + b.len + b.trail;
   const int64_t goff = b.grid_off - b.lead;
   if (b.lead < 0 || b.trail < 0 || b.len <= 0 || wlen % 2 != 0 || goff % 2 != 0 || goff < 0 ||
@@ -973,7 +945,7 @@ DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vec
     }
     // rows that start one element past a 16-B boundary on both sides (strides even): peel the
     // first element (and an odd last one), move the rest 16 B at a time
-    if (d.vec == 1 && peel_moves() && m.len >= 3 && m.src_off % 2 != 0 && m.dst_off % 2 != 0 &&
+    if (d.vec == 1 && box_tuning().peel_moves && m.len >= 3 && m.src_off % 2 != 0 && m.dst_off % 2 != 0 &&
         m.s1 % 2 == 0 && m.s2 % 2 == 0 && m.s3 % 2 == 0 &&
         reinterpret_cast<uintptr_t>(m.src) % 16 == 0 && reinterpret_cast<uintptr_t>(m.dst) % 16 == 0) {
       const uint32_t tail = uint32_t((m.len - 1) % 2), pairs = uint32_t((m.len - 1) / 2);

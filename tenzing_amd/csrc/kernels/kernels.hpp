@@ -41,8 +41,7 @@ struct BoxTuning {
   // ms, scripts/nt_multi_ab.sh, profiles/archive/r2_nt/)
   bool nt_unpack = true;
   int max_blocks = 4096;  // cap per box (grid-stride beyond)
-  // cap per box of the signalling put kernels, whose stores cross xGMI (env
-  // TZ_PUT_MAX_BLOCKS): one link moves ~77 GB/s per direction, which 64 blocks of posted 16-B
+  // cap per box of the signalling put kernels, whose stores cross xGMI: one link moves ~77 GB/s per direction, which 64 blocks of posted 16-B
   // stores cover with a wide margin, while thousands of blocks stalled on a link would hold the
   // CU slots that the concurrent local moves, relay kernels and unpacks need
   int put_max_blocks = 64;
@@ -50,10 +49,10 @@ struct BoxTuning {
   // are written once per exchange and nobody reads them inside it, so streaming them past the
   // caches leaves L2 / Infinity Cache to the interior slabs, which every exchange reads again:
   // 47.7 -> 44.4 us for the 26-direction move at 512^3 x 3 (scripts/move_ab.py; non-temporal
-  // loads plus stores: 57.7 us). Env TZ_NT_MOVE_LOAD / TZ_NT_MOVE_STORE override.
+  // loads plus stores: 57.7 us).
   bool nt_move = false;
   bool nt_move_store = true;
-  // box_move (direct transfers): items in flight per lane (1, 2 or 4; env TZ_MOVE_UNROLL) and
+  // box_move (direct transfers): items in flight per lane (1, 2 or 4) and
   // items per lane the grid is sized for (>= in flight; the lane loops over them). One in
   // flight, two per lane (twice the workgroups of 4 x 4) moves the 26 directions at 512^3 x 3
   // in 43.5 us against 44.1 us, the best of 10 shapes (scripts/move_ab.py --blocks,
@@ -62,13 +61,17 @@ struct BoxTuning {
   int move_items = 2;
   int xcd_remap = 0; // box_move block order: 0 round-robin, 1 one contiguous range per XCD,
                      // 2 every box split into 8 contiguous per-XCD shares
+  // moves of rows that start one element past a 16-B boundary peel that element and move the
+  // rest with 16-B accesses (false: 8-B accesses throughout; XYZQ row-start layout, 26
+  // directions: 92.0 -> 88.8 us, profiles/r5_roof/)
+  bool peel_moves = true;
+  // unpack boxes with lead / trail (BoxDesc) write their widened rows with 16-B stores (false:
+  // exactly the box; the 26-direction unpack 66 -> 37 us, profiles/r5_unpack/)
+  bool widen_unpack = true;
 };
 BoxTuning &box_tuning();
 /// set BoxTuning::xcd_remap; throws std::invalid_argument unless mode is 0, 1 or 2
 void set_xcd_remap(int mode);
-/// moves of rows that start one element past a 16-B boundary peel that element and move the
-/// rest with 16-B accesses (env TZ_MOVE_PEEL=0: 8-B accesses throughout)
-bool peel_moves();
 
 /// A box-to-box move between two arrays of the SAME pitched layout: element (x,i1,i2,i3) of
 /// the box at `src + src_off` goes to the same element of the box at `dst + dst_off`

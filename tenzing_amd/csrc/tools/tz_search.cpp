@@ -64,6 +64,7 @@ void usage() {
          "  [--relay auto|off|force] [--relay-fracs F1,F2]\n"
          "  [--hostsplit auto|off|force] [--hostsplit-fracs F1,F2,...] [--hostsplit-chunks N]\n"
          "  [--wide-puts auto|on|off] [--wide-put-blocks N]\n"
+         "  [--ipc-grid auto|0|1] [--copy-puts on|off] [--copy-engines N] [--move-pairs on|off]\n"
          "  [--ctrl auto|tcp|mpi|self] [--mpi-lib PATH] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--seed-schedule PATH] [--watchdog S]\n"
@@ -237,7 +238,7 @@ int main(int argc, char **argv) {
       h.relay = opt("relay", "auto");
       {
         // comma-separated relayed shares, e.g. 0.15,0.2
-        const std::string fr = opt("relay-fracs", "0.15,0.2");
+        const std::string fr = opt("relay-fracs", "0.15,0.2,0.25");
         if (!fr.empty()) {
           h.relay_fracs.clear();
           std::stringstream ss(fr);
@@ -259,6 +260,18 @@ int main(int argc, char **argv) {
       h.hostsplit_chunks = std::stoi(opt("hostsplit-chunks", "1"));
       h.wide_puts = opt("wide-puts", "auto");
       h.wide_put_blocks = int(optn("wide-put-blocks", 256));
+      {
+        const std::string ig = opt("ipc-grid", "auto");
+        TZ_CHECK(ig == "auto" || ig == "0" || ig == "1", "--ipc-grid must be auto, 0 or 1");
+        h.ipc_grid = ig == "auto" ? -1 : std::stoi(ig);
+        const std::string cp = opt("copy-puts", "on");
+        TZ_CHECK(cp == "on" || cp == "off", "--copy-puts must be on or off");
+        h.copy_puts = cp == "on";
+        h.copy_engines = int(optn("copy-engines", 1));
+        const std::string mp = opt("move-pairs", "on");
+        TZ_CHECK(mp == "on" || mp == "off", "--move-pairs must be on or off");
+        h.move_pairs = mp == "on";
+      }
       TZ_CHECK(h.order == "xyzq" || h.order == "qxyz", "--order must be xyzq or qxyz");
       h.rank = rank;
       h.size = size;
@@ -334,7 +347,7 @@ int main(int argc, char **argv) {
           saved.at("schedule").dump().find("he_putw_") != std::string::npos)
         TZ_THROW("the saved schedule uses wide IPC puts (he_putw_*), which this launch does not "
                  "offer: " << halo->transport_report().at("wide_put")
-                           << " (e.g. TZ_PUT_MAX_BLOCKS equal to --wide-put-blocks, or its preflight "
+                           << " (e.g. the put block cap equal to --wide-put-blocks, or its preflight "
                               "failed on this node)");
       const Sequence seq = OpIndex(*g).sequence_from_json(saved.at("schedule"));
       const auto bad = verify(seq, *resolve_graph(*g, seq), streams);

@@ -46,6 +46,10 @@ Json HaloArgs::json() const {
   j["hostsplit_chunks"] = hostsplit_chunks;
   j["wide_puts"] = wide_puts;
   j["wide_put_blocks"] = wide_put_blocks;
+  j["ipc_grid"] = ipc_grid;
+  j["copy_puts"] = copy_puts;
+  j["copy_engines"] = copy_engines;
+  j["move_pairs"] = move_pairs;
   return j;
 }
 
@@ -64,14 +68,20 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   TZ_CHECK(a_.neighbors == 6 || a_.neighbors == 26, "neighbors must be 6 or 26");
   TZ_CHECK(a_.order == "xyzq" || a_.order == "qxyz", "order must be xyzq or qxyz");
   TZ_CHECK(a_.rank >= 0 && a_.rank < a_.size, "bad rank");
-  TZ_CHECK(a_.pitch_pad >= 0 && a_.pitch_pad % 16 == 0, "pitch_pad must be a multiple of 16");
   TZ_CHECK(a_.ghost_align >= -2 && (a_.ghost_align <= 0 || a_.ghost_align == 8 || a_.ghost_align == 16),
            "ghost_align must be -2 (auto), -1 (x = 0 at the row start), 0, 8 or 16");
-  // auto: QXYZ with line-aligned ghost runs (a row's ghost and source runs, 9 doubles each,
-  // cannot share a line: each on a line of its own is the minimum traffic); XYZQ with x = 0 at
-  // the row start, where a row's 3-double ghost and source runs share lines that the row-pair
-  // move reads and writes together (profiles/r5_roof/: 90 us vs 93 line-aligned)
-  if (a_.ghost_align == -2) a_.ghost_align = a_.order == "qxyz" ? 16 : -1;
+  // auto: line-aligned ghost runs in both orders. In QXYZ a row's ghost and source runs (9
+  // doubles each) cannot share a line, so each on a line of its own is the minimum traffic. In
+  // XYZQ the one-GPU self move is 3 % faster with x = 0 at the row start (profiles/r5_roof/: 90
+  // vs 93 us), but line-aligned runs are what the remote puts' sector widening, the widened
+  // unpack and the stencil's 16-B interior path rely on; the reference layout (-1) is asked for
+  // explicitly where it is wanted (bench.py's reference_layout sub-record)
+  if (a_.ghost_align == -2) a_.ghost_align = 16;
+  // extra row pitch: whole 64-B sectors (even strides keep the 16-B paths); with line-aligned
+  // ghosts whole 128-B lines, which the widened x-ghost writes assume of every row stride
+  const int padUnit = a_.ghost_align == 16 ? 16 : 8;
+  TZ_CHECK(a_.pitch_pad >= 0 && a_.pitch_pad % padUnit == 0,
+           "pitch_pad must be a multiple of " << padUnit << " elements here (got " << a_.pitch_pad << ")");
   TZ_CHECK(a_.wide_puts == "auto" || a_.wide_puts == "on" || a_.wide_puts == "off",
            "wide_puts must be auto, on or off");
   TZ_CHECK(a_.wide_put_blocks >= 1 && a_.wide_put_blocks <= 4096,
@@ -119,7 +129,7 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
     // driver lays it out: halo_run_strategy.hpp:49, 63-64)
     const int64_t al = a_.ghost_align > 8 ? a_.ghost_align : 8;
     xoff_ = a_.ghost_align < 0 ? 0 : (al - a_.ghost % al) % al;
-    pitch_ = round_up(xoff_ + X, 16) + a_.pitch_pad; // rows are whole 128-B lines
+    pitch_ = round_up(xoff_ + X, 16) + a_.pitch_pad; // whole 128-B lines (+ pitch_pad)
     sy_ = pitch_;
     sz_ = pitch_ * Y;
     sq_ = sz_ * Z;
@@ -183,8 +193,9 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
     if (pipe_[i] && t != "copy" && t != "host") useRccl_ = true;
     if (pipe_[i] && t == "host") useHost_ = true;
   }
-  ipcGrid_ = gridElems_ * sizeof(double) < (size_t(2) << 30);
-  if (const char *v = std::getenv("TZ_IPC_GRID")) ipcGrid_ = std::atoi(v) != 0;
+  TZ_CHECK(a_.ipc_grid >= -1 && a_.ipc_grid <= 1, "ipc_grid must be -1 (auto), 0 or 1");
+  TZ_CHECK(a_.copy_engines >= 1 && a_.copy_engines <= 8, "copy_engines must be in [1, 8]");
+  ipcGrid_ = a_.ipc_grid < 0 ? gridElems_ * sizeof(double) < (size_t(2) << 30) : a_.ipc_grid != 0;
   // In grid mode a receiver hands the credit back as soon as the ghosts arrived, so a sender
   // one iteration ahead may overwrite them. That is fine while nothing reads them between
   // exchanges, but the stencil does: it takes buffers mode, where puts land in receive buffers
@@ -192,10 +203,9 @@ HaloExchange::HaloExchange(HaloArgs a) : a_(std::move(a)) {
   // exchange's start removes the slack that keeps puts from waiting on the peer's current
   // iteration; with several ranks time-slicing one GPU that stalled waits for seconds.)
   if (a_.stencil) ipcGrid_ = false;
-  // copy-engine puts (buffers mode only): on unless TZ_IPC_COPY=0
-  useCopy_ = useIpc_;
-  if (const char *v = std::getenv("TZ_IPC_COPY")) useCopy_ = useCopy_ && std::atoi(v) != 0;
-  if (const char *v = std::getenv("TZ_COPY_ENGINES")) copyEngines_ = std::max(1, std::min(8, std::atoi(v)));
+  // copy-engine puts (buffers mode only)
+  useCopy_ = useIpc_ && a_.copy_puts;
+  copyEngines_ = a_.copy_engines;
 
   // relay routing through the corner peer: a 2x2x2 grid (the only single-node grid where the
   // corner and edge-diagonal links idle while both faces of an axis share one link), ipc puts
@@ -574,8 +584,7 @@ std::string HaloExchange::rccl_preflight(Ctrl &ctrl) {
   double none = remote.empty() || comms_.empty() ? 1.0 : 0.0;
   ctrl.allreduce_max(&none, 1);
   if (none != 0.0) return "";
-  double limit = 20.0;
-  if (const char *v = std::getenv("TZ_RCCL_PREFLIGHT_S")) limit = std::atof(v);
+  const double limit = preflight_limit_s(20.0);
   const std::string failEnv = std::getenv("TZ_FAIL_TRANSPORTS") ? std::getenv("TZ_FAIL_TRANSPORTS") : "";
   const bool simHang = ("," + failEnv + ",").find(",rccl_hang,") != std::string::npos;
   const bool simGraph = ("," + failEnv + ",").find(",rccl_graph_schedule,") != std::string::npos;
@@ -648,10 +657,10 @@ std::string HaloExchange::rccl_preflight(Ctrl &ctrl) {
   // next, a hang drops RCCL.
   auto graph_step = [&](CaptureMode mode) -> std::string {
     std::string wrong;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    try {
-      for (int form = 0; form < 2 && why.empty() && wrong.empty(); ++form) {
+    for (int form = 0; form < 2 && why.empty() && wrong.empty(); ++form) {
+      hipGraph_t graph = nullptr;
+      hipGraphExec_t exec = nullptr;
+      try {
         TZ_LOG(Debug, "rccl preflight: graph step, " << capture_mode_name(mode) << " capture, form " << form);
         {
           GraphBuilder gb({s, side[0], side[1]}, mode);
@@ -675,6 +684,18 @@ std::string HaloExchange::rccl_preflight(Ctrl &ctrl) {
         }
         TZ_LOG(Debug, "rccl preflight: instantiate");
         TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      } catch (const std::exception &e) {
+        // a capture or instantiation error is not a broken transport: RCCL stays for eager runs
+        wrong = e.what();
+        drain_after_error(wrong);
+      }
+      // launch only where every rank built the graph: a rank launching alone would wait for
+      // peers that never join, report a hang and abort the communicators instead of trying the
+      // next capture mode
+      double built = wrong.empty() ? 0.0 : 1.0;
+      ctrl.allreduce_max(&built, 1);
+      if (built != 0.0 && wrong.empty()) wrong = "capture or instantiation failed on another rank";
+      try {
         TZ_LOG(Debug, "rccl preflight: launch");
         const char *what = form == 0 ? "fused hipGraph exchange" : "per-direction hipGraph exchange";
         const int gens[2][2] = {{1, 2}, {3, 1}}; // (generations are 0..3; 0 is the search's)
@@ -691,18 +712,18 @@ std::string HaloExchange::rccl_preflight(Ctrl &ctrl) {
                       std::to_string(bad) + " wrong cells";
           }
         }
-        (void)hipGraphExecDestroy(exec);
-        exec = nullptr;
-        (void)hipGraphDestroy(graph);
-        graph = nullptr;
+      } catch (const std::exception &e) {
+        wrong = e.what();
+        drain_after_error(wrong);
       }
-    } catch (const std::exception &e) {
-      // a capture or instantiation error is not a broken transport: RCCL stays for eager runs
-      wrong = e.what();
-      drain_after_error(wrong);
+      if (exec) (void)hipGraphExecDestroy(exec);
+      if (graph) (void)hipGraphDestroy(graph);
+      // every rank goes on to the next form (or stops) together
+      double f[2] = {why.empty() ? 0.0 : 1.0, wrong.empty() ? 0.0 : 1.0};
+      ctrl.allreduce_max(f, 2);
+      if (f[0] != 0.0 && why.empty()) why = "failed on another rank";
+      if (f[1] != 0.0 && wrong.empty()) wrong = "wrong data on another rank";
     }
-    if (exec) (void)hipGraphExecDestroy(exec);
-    if (graph) (void)hipGraphDestroy(graph);
     return wrong;
   };
   std::vector<CaptureMode> modes;
@@ -900,7 +921,7 @@ std::vector<kern::MoveDesc> HaloExchange::direct_moves(const std::vector<int> &d
     if (a_.ghost_align > 0) widen_to_sectors(dirs_[opp_[i]].dx, m);
     ms.push_back(m);
   }
-  if (a_.order == "xyzq" && move_pairs()) ms = pair_x_moves(ms);
+  if (a_.order == "xyzq" && a_.move_pairs) ms = pair_x_moves(ms);
   return ms;
 }
 
@@ -1004,14 +1025,6 @@ std::map<std::string, double> HaloExchange::move_roof(int iters) {
   r["lines_TBps_at_move"] = (rd + wr) / (std::min(r["move_us"], r["move_us_again"]) * 1e-6) / 1e12;
   init_grid(nullptr, gen_);
   return r;
-}
-
-bool HaloExchange::move_pairs() {
-  static const bool on = [] {
-    const char *v = std::getenv("TZ_MOVE_PAIRS");
-    return !v || std::atoi(v) != 0;
-  }();
-  return on;
 }
 
 std::vector<kern::MoveDesc> HaloExchange::pair_x_moves(const std::vector<kern::MoveDesc> &ms) const {

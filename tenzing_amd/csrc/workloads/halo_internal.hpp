@@ -23,13 +23,8 @@ namespace halo_detail {
 /// side d (ghost = true), in grid element offsets
 kern::BoxDesc make_box(const HaloArgs &a, const HaloExchange::Dir &d, bool ghost, int64_t xoff,
                        int64_t sy, int64_t sz, int64_t sq);
-/// the device-side wait limit of the transport preflights (seconds): env TZ_PREFLIGHT_WAIT_S,
-/// default 3 (a healthy exchange of the preflight's size takes milliseconds)
-inline double preflight_wait_s() {
-  const char *e = std::getenv("TZ_PREFLIGHT_WAIT_S");
-  const double v = e ? std::atof(e) : 0.0;
-  return v > 0 ? v : 3.0;
-}
+/// the device-side wait limit of the transport preflights (seconds; preflight_limit_s)
+inline double preflight_wait_s() { return preflight_limit_s(3.0); }
 } // namespace halo_detail
 using halo_detail::preflight_wait_s;
 using halo_detail::make_box;

@@ -24,13 +24,11 @@ namespace tz {
 
 namespace {
 // wait for `e` for at most `limit_s` (polling; hipEventSynchronize has no bound): false if it did
-// not complete in time. Env TZ_LINK_MATRIX_STALL=1 (tests) treats every wait as one that never
-// completes.
+// not complete in time. TZ_FAIL_TRANSPORTS containing "link_matrix_stall" (tests) treats every
+// wait as one that never completes.
 bool wait_event_bounded(hipEvent_t e, double limit_s) {
-  static const bool stall = [] {
-    const char *v = std::getenv("TZ_LINK_MATRIX_STALL");
-    return v && std::atoi(v) != 0;
-  }();
+  const char *f = std::getenv("TZ_FAIL_TRANSPORTS");
+  const bool stall = f && (std::string(",") + f + ",").find(",link_matrix_stall,") != std::string::npos;
   const double end = wtime() + limit_s;
   for (;;) {
     const hipError_t q = stall ? hipErrorNotReady : hipEventQuery(e);

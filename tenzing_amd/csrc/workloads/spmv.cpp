@@ -388,26 +388,41 @@ DistSpmv::DistSpmv(SpmvArgs a, Ctrl *ctrl) : a_(std::move(a)) {
     // the reference's setup (include/tenzing/spmv/row_part_spmv.cuh:24-90, :322-403): rank 0
     // builds (or reads) the matrix and sends every rank its row block; then every rank tells
     // each owner which of its columns it needs, and each owner builds its send plan from that
+    // A failure on rank 0 (a missing or malformed matrix file, nnz above the band's capacity,
+    // fewer rows than ranks) travels in the row-block header (hdr[4] = 1, then the message), so
+    // every rank throws the same error right after this exchange instead of waiting in it
     std::vector<std::string> out(size_t(a_.size));
     if (a_.rank == 0) {
-      const CsrHost A = build_matrix();
-      TZ_CHECK(a_.m >= a_.size, "fewer matrix rows (" << a_.m << ") than ranks (" << a_.size << ")");
-      for (int q = 0; q < a_.size; ++q) {
-        auto [q0, q1] = row_partition(a_.m, q, a_.size);
-        const CsrHost B = row_block(A, q0, q1);
-        std::string &m = out[size_t(q)];
-        const int64_t hdr[5] = {a_.m, a_.nnz, a_.bw, a_.nnz_actual, 0};
-        m.append(reinterpret_cast<const char *>(hdr), sizeof(hdr));
-        put_vec(m, B.rowPtr);
-        put_vec(m, B.colInd);
-        put_vec(m, B.val);
+      std::string err;
+      try {
+        const CsrHost A = build_matrix();
+        TZ_CHECK(a_.m >= a_.size, "fewer matrix rows (" << a_.m << ") than ranks (" << a_.size << ")");
+        for (int q = 0; q < a_.size; ++q) {
+          auto [q0, q1] = row_partition(a_.m, q, a_.size);
+          const CsrHost B = row_block(A, q0, q1);
+          std::string &m = out[size_t(q)];
+          const int64_t hdr[5] = {a_.m, a_.nnz, a_.bw, a_.nnz_actual, 0};
+          m.append(reinterpret_cast<const char *>(hdr), sizeof(hdr));
+          put_vec(m, B.rowPtr);
+          put_vec(m, B.colInd);
+          put_vec(m, B.val);
+        }
+      } catch (const std::exception &e) {
+        err = e.what();
       }
+      if (!err.empty())
+        for (std::string &m : out) {
+          const int64_t hdr[5] = {0, 0, 0, 0, 1};
+          m.assign(reinterpret_cast<const char *>(hdr), sizeof(hdr));
+          m += err;
+        }
     }
     const std::vector<std::string> in = ctrl->alltoallv(out);
     const std::string &msg = in[0];
     int64_t hdr[5];
     TZ_CHECK(msg.size() >= sizeof(hdr), "spmv setup: no row block from rank 0");
     std::memcpy(hdr, msg.data(), sizeof(hdr));
+    TZ_CHECK(hdr[4] == 0, "spmv setup on rank 0 failed: " << msg.substr(sizeof(hdr)));
     a_.m = hdr[0];
     a_.nnz = hdr[1];
     a_.bw = hdr[2];
@@ -740,8 +755,7 @@ std::string DistSpmv::rccl_preflight_local() {
   // under a bounded wait (a hang releases spinning kernels, aborts the communicator and
   // reports), then every received entry checked
   if (!comm_) return "";
-  double limit = 20.0;
-  if (const char *v = std::getenv("TZ_RCCL_PREFLIGHT_S")) limit = std::atof(v);
+  const double limit = preflight_limit_s(20.0);
   hipStream_t s = nullptr;
   TZ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   std::string why;
@@ -792,8 +806,7 @@ void DistSpmv::rccl_graph_preflight(Ctrl &ctrl) {
   // a workload's preflight has settled it (the halo's, in a fused graph), only that mode is
   // verified here; otherwise whole-schedule capture first, then child capture. No mode works:
   // RCCL exchanges stay out of hipGraphs (their candidates run eagerly). Every rank in step.
-  double limit = 20.0;
-  if (const char *v = std::getenv("TZ_RCCL_PREFLIGHT_S")) limit = std::atof(v);
+  const double limit = preflight_limit_s(20.0);
   const std::string failEnv = std::getenv("TZ_FAIL_TRANSPORTS") ? std::getenv("TZ_FAIL_TRANSPORTS") : "";
   const bool simGraph = ("," + failEnv + ",").find(",rccl_graph_schedule,") != std::string::npos;
   std::vector<CaptureMode> modes;
@@ -832,6 +845,15 @@ void DistSpmv::rccl_graph_preflight(Ctrl &ctrl) {
         graph = static_cast<hipGraph_t>(gb.finish());
       }
       TZ_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    } catch (const std::exception &e) {
+      wrong = e.what(); // a capture or instantiation error: RCCL stays for eager runs
+    }
+    // launch only where every rank built the graph: a rank launching alone would wait for peers
+    // that never join, report a hang and abort the communicator instead of trying the next mode
+    double built = wrong.empty() ? 0.0 : 1.0;
+    ctrl.allreduce_max(&built, 1);
+    if (built != 0.0 && wrong.empty()) wrong = "capture or instantiation failed on another rank";
+    try {
       for (int gen = 1; gen <= 2 && wrong.empty() && !hung; ++gen) {
         upload_x(gen);
         TZ_HIP(hipMemsetAsync(dXr_.get(), 0, dXr_.bytes(), s));

@@ -38,6 +38,11 @@ namespace tz {
 class RcclComm;
 class RocsparseCsr;
 
+/// the wait bound of a transport preflight (seconds): env TZ_PREFLIGHT_S if set, else `dflt`
+/// (RCCL preflight exchanges 20 s, device-side IPC / relay / host-split waits 3 s: a healthy
+/// exchange of a preflight's size takes milliseconds)
+double preflight_limit_s(double dflt);
+
 /// hipMalloc'd memory (RAII)
 class DeviceBuffer {
 public:
@@ -47,7 +52,7 @@ public:
   /// allocated fine-grained, so the reading kernels see those stores through the caches rather
   /// than lines the local L2 kept from the previous exchange (coarse-grained memory is only
   /// coherent with other agents at dispatch boundaries whose fences the device-side arrival
-  /// waits bypass). Env TZ_IPC_FINE=0 allocates it coarse-grained like any other buffer.
+  /// waits bypass).
   DeviceBuffer(size_t bytes, bool peerWritten);
   ~DeviceBuffer();
   DeviceBuffer(DeviceBuffer &&o) noexcept : p_(o.p_), bytes_(o.bytes_) {
@@ -201,14 +206,24 @@ struct HaloArgs {
   int comms = 0;
   int rank = 0, size = 1;
   int px = 0, py = 0, pz = 0;     // rank grid (0 = from prime factors, reference style)
-  int pitch_pad = 0;              // extra row-pitch elements (multiple of 16: keeps alignment)
+  int pitch_pad = 0;              // extra row-pitch elements (multiple of 8; of 16 with ghost_align 16)
   // 8 or 16: the x padding puts the inner ends of the x ghost runs (ghost-low end, ghost-high
   // start) on 8-element (64-B sector) / 16-element (128-B line) boundaries, and direct moves
   // widen their x ghost writes over the neighbouring row padding to whole sectors / lines (no
   // partially written sectors or lines on the x faces). 0: line-optimal padding, exact runs.
-  // -1: no padding, x = 0 at the row start (the reference's layout). -2 (default): 16 for
-  // QXYZ, -1 for XYZQ.
+  // -1: no padding, x = 0 at the row start (the reference's layout). -2 (default): 16.
   int ghost_align = -2;
+  // IPC puts land in the peer's grid (1) or in receive buffers that the peer unpacks (0);
+  // -1 (default): the grid below 2 GiB (measured, scripts/ipc_probe.py), buffers above
+  int ipc_grid = -1;
+  // copy-engine puts (SDMA, hipMemcpy) offered beside the kernel puts (buffers mode only)
+  bool copy_puts = true;
+  // copy-engine puts of one group spread over this many streams (1..8): one engine moves
+  // ~60 GB/s, independent copies on 2 / 4 streams reach more on one device
+  int copy_engines = 1;
+  // XYZQ self-wrap moves of the x axis as row pairs (one lane moves a row's +x and -x runs,
+  // which share lines in the row-start layout); false: separate moves (A/B)
+  bool move_pairs = true;
   // also run a 7-point stencil over the interior after the exchange (into a second grid): the
   // search may update the ghost-free interior while ghosts are in flight and the one-cell
   // boundary shell afterwards, or the whole domain after the exchange (a ChoiceOp)
@@ -222,7 +237,7 @@ struct HaloArgs {
   // f = 0.2 with forwarding after arrival (what is built). "auto": offered to the search as a
   // transport alternative when applicable; "off"; "force": the only remote transport (tests)
   std::string relay = "auto";
-  std::vector<double> relay_fracs = {0.15, 0.2}; // relayed shares offered (a ChoiceOp)
+  std::vector<double> relay_fracs = {0.15, 0.2, 0.25}; // relayed shares offered (a ChoiceOp; 0.25: f* at equal link rates)
   // host split (IPC "buffers" mode, several ranks): a share of every face goes GPU -> node
   // shared host memory -> peer GPU over each GPU's own PCIe link, while the rest goes over
   // xGMI as an IPC put; the PCIe links are otherwise idle during an exchange. "auto": offered
@@ -235,7 +250,7 @@ struct HaloArgs {
   // link sees the same store / read-back mix as one GPU's link on a node (profiles/r3_hs_chunks)
   int hostsplit_chunks = 1;
   // wide kernel puts: the IPC put kernels with `wide_put_blocks` workgroups per box instead of
-  // the global cap (TZ_PUT_MAX_BLOCKS, 64), offered to the search as a transport alternative.
+  // the global cap (BoxTuning::put_max_blocks, 64), offered to the search as a transport alternative.
   // One loopback GPU has no link to fill, so 64 won there; whether more workgroups in flight
   // fill an xGMI link better is the node's to measure. "auto": offered when a peer's memory
   // sits on another device (agreed by every rank); "on": always (tests); "off"
@@ -570,10 +585,9 @@ private:
   unsigned long long *peer_slot(int rank, int set, int i) const;
   std::vector<unsigned long long *> credit_ptrs(const std::vector<int> &dirs) const;
   const RcclComm &comm_for(int streamIdx, int dir) const;
-  /// XYZQ direct moves: the +x / -x moves of one (dy, dz) as one row-pair move (env
-  /// TZ_MOVE_PAIRS=0: off)
+  /// XYZQ direct moves: the +x / -x moves of one (dy, dz) as one row-pair move
+  /// (HaloArgs::move_pairs)
   std::vector<kern::MoveDesc> pair_x_moves(const std::vector<kern::MoveDesc> &ms) const;
-  static bool move_pairs();
   void widen_to_sectors(int ghostDx, kern::MoveDesc &m) const;
   /// elements of row padding an x ghost run's writes may also cover before / after each row
   /// (whole ghost_align units); 0, 0 for other boxes or without line-aligned ghosts

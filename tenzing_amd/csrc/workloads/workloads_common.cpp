@@ -26,12 +26,14 @@ DeviceBuffer::DeviceBuffer(size_t bytes) : bytes_(bytes) {
 
 DeviceBuffer::DeviceBuffer(size_t bytes, bool peerWritten) : bytes_(bytes) {
   if (!bytes) return;
-  static const bool fine = [] {
-    const char *e = std::getenv("TZ_IPC_FINE");
-    return !e || std::atoi(e) != 0;
-  }();
-  if (peerWritten && fine) TZ_HIP(hipExtMallocWithFlags(&p_, bytes, hipDeviceMallocFinegrained));
+  if (peerWritten) TZ_HIP(hipExtMallocWithFlags(&p_, bytes, hipDeviceMallocFinegrained));
   else TZ_HIP(hipMalloc(&p_, bytes));
+}
+
+double preflight_limit_s(double dflt) {
+  const char *e = std::getenv("TZ_PREFLIGHT_S");
+  const double v = e ? std::atof(e) : 0.0;
+  return v > 0 ? v : dflt;
 }
 
 SharedHostBuffer SharedHostBuffer::create(const std::string &name, size_t bytes) {

@@ -17,6 +17,23 @@ import dataclasses
 from .. import _tz
 
 
+def ipc_grid_mode(value=None) -> int:
+    """HaloArgs.ipc_grid: `value` if given, else TZ_IPC_GRID (1 grid, 0 receive buffers) from
+    the environment, else -1 (auto). The environment is read here, where a config becomes
+    native arguments, so one process can build both modes."""
+    import os
+
+    if value is None:
+        v = os.environ.get("TZ_IPC_GRID", "")
+        if v == "":
+            return -1
+        value = 1 if int(v) != 0 else 0
+    value = int(value)
+    if value not in (-1, 0, 1):
+        raise ValueError(f"ipc_grid must be -1 (auto), 0 or 1 (got {value})")
+    return value
+
+
 @dataclasses.dataclass
 class HaloConfig:
     n: int = 512          # interior cells per rank per axis (nX = nY = nZ)
@@ -27,16 +44,18 @@ class HaloConfig:
     transport: str = "auto"  # rccl | copy | direct | auto (direct on 1 rank, else rccl)
     fuse: str = "none"    # none | pack | all | groups | choice
     comms: int = 0        # RCCL communicators (0 = one per direction)
-    pitch_pad: int = 0    # extra row-pitch elements (multiple of 16)
+    pitch_pad: int = 0    # extra row-pitch elements (multiple of 8; of 16 with line-aligned ghosts)
     rank_grid: tuple = ()  # (px, py, pz); () = reference rule (prime factors, smallest dim first)
     # x ghost runs aligned to 8 (sector) / 16 (line) elements, 0 = off, -1 = x = 0 at the row
-    # start (the reference's layout), -2 = auto (16 for qxyz, -1 for xyzq)
+    # start (the reference's layout), -2 = auto (16, line-aligned, in both orders)
     ghost_align: int = -2
     stencil: bool = False  # add a 7-point stencil (interior beside / shell after the exchange)
     # two-hop routing of a share of every face through the corner peer (2x2x2 rank grid, ipc
     # receive buffers): "auto" offers it to the search, "off", "force" (only transport)
     relay: str = "auto"
-    relay_fracs: tuple = (0.15, 0.2)  # relayed shares offered (ChoiceOp)
+    # relayed shares offered (ChoiceOp): 0.2 balances the links when the forward waits for the
+    # whole share, 0.25 is the link model's f* at equal link rates (parallel/linkmodel.relay_share)
+    relay_fracs: tuple = (0.15, 0.2, 0.25)
     # a share of every face through node shared host memory over the GPUs' PCIe links, beside
     # the xGMI IPC put of the rest (ipc receive buffers): "auto" offers it, "off", "force"
     hostsplit: str = "auto"
@@ -46,6 +65,12 @@ class HaloConfig:
     # (when peers sit on other devices), "on", "off"
     wide_puts: str = "auto"
     wide_put_blocks: int = 256
+    # IPC puts into the peer's grid (1) or into receive buffers (0); None: the environment's
+    # TZ_IPC_GRID if set, else auto (-1: the grid below 2 GiB)
+    ipc_grid: int | None = None
+    copy_puts: bool = True   # copy-engine puts offered (receive buffers only)
+    copy_engines: int = 1    # copy-engine puts of one group spread over this many streams
+    move_pairs: bool = True  # XYZQ x self-wrap moves as row pairs
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":
         a = _tz.HaloArgs()
@@ -67,6 +92,10 @@ class HaloConfig:
         a.hostsplit_chunks = int(self.hostsplit_chunks)
         a.wide_puts = self.wide_puts
         a.wide_put_blocks = int(self.wide_put_blocks)
+        a.ipc_grid = ipc_grid_mode(self.ipc_grid)
+        a.copy_puts = bool(self.copy_puts)
+        a.copy_engines = int(self.copy_engines)
+        a.move_pairs = bool(self.move_pairs)
         if self.rank_grid:
             a.px, a.py, a.pz = (int(v) for v in self.rank_grid)
         a.rank, a.size, a.device = rank, size, device

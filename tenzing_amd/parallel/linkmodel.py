@@ -63,6 +63,48 @@ def link_sim_params(probe: dict | None = None, matrix: dict | None = None, noise
     return p
 
 
+def relay_share(face_GBps: float = 1.0, corner_GBps: float = 1.0) -> float:
+    """The relayed share f* of every face that balances the 2x2x2 grid's busiest links.
+
+    Without relaying, each face link carries both faces of its axis (2 B per exchange, B = one
+    face). Relaying a share f of all 6 faces through the corner peer puts 6 f B on the corner link
+    and leaves (1 - f) 2 B on each face link, so the busiest link takes
+    max((1 - f) 2 B / r_face, 6 f B / r_corner), smallest at f* = r_corner / (r_corner + 3 r_face):
+    0.25 at equal link rates, i.e. 0.75 of a face pair on every busy link. (The second hop runs
+    over a yz-style diagonal link, which otherwise carries only edges: 2 f B, never the busiest.)"""
+    if face_GBps <= 0 or corner_GBps <= 0:
+        raise ValueError("link rates must be positive")
+    return corner_GBps / (corner_GBps + 3.0 * face_GBps)
+
+
+def relay_fracs_offered(f_star: float, base=(0.15, 0.2)) -> tuple:
+    """The relay shares the search chooses among: the fixed ones (0.2 balances the links when the
+    forward waits for the whole share to arrive, docs/RESULTS.md) and the link model's f*,
+    clamped into the range the relay accepts, (0, 0.5)."""
+    f = min(0.45, max(0.05, round(float(f_star), 3)))
+    return tuple(sorted(set(base) | {f}))
+
+
+def relay_share_from_record(record: dict):
+    """f* from a multi-GPU bench record's own link matrix (rank 0's put rates to its face peers
+    and to its corner peer, every pair sending at once), or None when the record has no 2x2x2
+    grid or no matrix."""
+    cfg = record.get("config") or {}
+    if list(cfg.get("rank_grid") or []) != [2, 2, 2]:
+        return None
+    m = (record.get("link_matrix") or {}).get("put_GBps")
+    if not m or (record.get("link_matrix") or {}).get("why"):
+        return None
+    row = m[0]
+    # rank r = x + 2 y + 4 z in the 2x2x2 grid (HaloExchange's rank order): rank 0's face peers
+    # are 1, 2 and 4, its corner peer 7
+    face = [row[q] for q in (1, 2, 4) if row[q] and row[q] > 0]
+    corner = row[7] if row[7] and row[7] > 0 else None
+    if not face or corner is None:
+        return None
+    return relay_share(sum(face) / len(face), corner)
+
+
 def graph_params_from_probe(params, branch: dict | None):
     """``params`` with its hipGraph join cost taken from a bench record's ``graph_branch_probe``
     (the padding in use): the unrolled 3-branch replay's time over the one-branch replay's is
@@ -84,15 +126,16 @@ def graph_params_from_probe(params, branch: dict | None):
 
 
 def headline_graph(rank: int, size: int, n: int = 512, neighbors: int = 26, order: str = "qxyz",
-                   wide_puts: str = "on", relay: str = "auto", hostsplit: str = "auto"):
+                   wide_puts: str = "on", relay: str = "auto", hostsplit: str = "auto",
+                   ipc_grid=None):
     """(halo, graph) of one rank of the bench's N-rank tree, built without a GPU: every remote
     transport offered (RCCL, kernel / wide / copy-engine puts, their mix, relays, host split)
-    as the top-level ChoiceOp, per-direction or fused groups below it. Set TZ_IPC_GRID=0 first
-    for the receive-buffer transports (copy engines, relay, host split)."""
+    as the top-level ChoiceOp, per-direction or fused groups below it. ipc_grid=0 (or
+    TZ_IPC_GRID=0) for the receive-buffer transports (copy engines, relay, host split)."""
     from ..models import HaloConfig
 
     cfg = HaloConfig(n=n, neighbors=neighbors, order=order, fuse="choice", transport="auto",
-                     wide_puts=wide_puts, relay=relay, hostsplit=hostsplit)
+                     wide_puts=wide_puts, relay=relay, hostsplit=hostsplit, ipc_grid=ipc_grid)
     h = _tz.HaloExchange(cfg.args(rank, size, -1))
     g = _tz.Graph()
     h.add_to_graph(g)
@@ -214,8 +257,6 @@ def model_report(record: dict, params=None) -> dict:
     transport the bench seeded (one greedy schedule each, ``seeded_pct10_ms``), the model's time
     of the same schedule on rank 0's graph beside the measured one, and the rank correlation of
     the two orders. Needs no GPU."""
-    import os
-
     from ..utils.benchkit import remote_via
 
     cfg = record.get("config") or {}
@@ -225,21 +266,14 @@ def model_report(record: dict, params=None) -> dict:
         link_sim_params(record.get("link_probe"), record.get("link_matrix")),
         record.get("graph_branch_probe"))
     # the record's IPC mode (puts into the peer's grid, or into receive buffers: the copy-engine,
-    # relay and host-split transports), for the graph's construction only
-    old = os.environ.get("TZ_IPC_GRID")
-    os.environ["TZ_IPC_GRID"] = "1" if record.get("ipc_mode") == "grid" else "0"
-    try:
-        h, g = headline_graph(0, size, n=int(cfg.get("seq_len") or 512),
-                              neighbors=int(cfg.get("neighbors") or 26),
-                              order=cfg.get("storage_order") or "qxyz",
-                              wide_puts="on" if record.get("wide_puts_offered", True) else "off",
-                              relay="auto" if record.get("relay_offered", True) else "off",
-                              hostsplit="auto" if record.get("hostsplit_offered", True) else "off")
-    finally:
-        if old is None:
-            os.environ.pop("TZ_IPC_GRID", None)
-        else:
-            os.environ["TZ_IPC_GRID"] = old
+    # relay and host-split transports)
+    h, g = headline_graph(0, size, n=int(cfg.get("seq_len") or 512),
+                          neighbors=int(cfg.get("neighbors") or 26),
+                          order=cfg.get("storage_order") or "qxyz",
+                          wide_puts="on" if record.get("wide_puts_offered", True) else "off",
+                          relay="auto" if record.get("relay_offered", True) else "off",
+                          hostsplit="auto" if record.get("hostsplit_offered", True) else "off",
+                          ipc_grid=1 if record.get("ipc_mode") == "grid" else 0)
     platform = _tz.Platform(streams)
     seeds, _ = transport_seeds(g, platform, streams)
     measured = record.get("seeded_pct10_ms") or {}

@@ -17,6 +17,7 @@ halo_run_strategy.hpp:42-49 give the sub-record configurations.
 """
 from __future__ import annotations
 
+import json
 import sys
 import time
 
@@ -223,22 +224,31 @@ def search_record(tz, ctrl, rt, graph, streams: int, verify, steps: int, warmup:
     if seeds and ctrl.rank == 0:
         o.seed_schedules = list(seeds)
     res = tz.mcts_explore(graph, plat, bench, ctrl, o)
-    rec = {"mcts_candidates": len(res.sims), "mcts_skipped": res.failed,
+    # only rank 0 holds the results: its finalists go to every rank (by op name), so that all
+    # ranks re-rank, verify and time the same schedules in the same collectives
+    payload = ""
+    if ctrl.rank == 0:
+        order = sorted(range(len(res.sims)), key=lambda i: res.sims[i].res.pct10)
+        top, keys = [], set()
+        for i in order:
+            k = res.sims[i].seq.canonical_key()
+            if k not in keys:
+                keys.add(k)
+                top.append(i)
+            if len(top) >= max(1, rerank):
+                break
+        payload = json.dumps({"seqs": [res.sims[i].seq.json() for i in top],
+                              "pct10": [res.sims[i].res.pct10 for i in top],
+                              "n": len(res.sims), "failed": res.failed})
+    payload = json.loads(ctrl.bcast(payload, 0).decode())
+    rec = {"mcts_candidates": payload["n"], "mcts_skipped": payload["failed"],
            "search_wall_s": round(res.wall_s, 3), "seeded": len(seeds)}
-    if not res.sims:
+    if not payload["seqs"]:
         rec["error"] = "the search measured no candidate"
         return rec
-    order = sorted(range(len(res.sims)), key=lambda i: res.sims[i].res.pct10)
-    top, keys = [], set()
-    for i in order:
-        k = res.sims[i].seq.canonical_key()
-        if k not in keys:
-            keys.add(k)
-            top.append(i)
-        if len(top) >= max(1, rerank):
-            break
-    cands = [res.sims[i].seq for i in top]
-    rec["search_best_pct10_ms"] = res.sims[top[0]].res.pct10 * 1e3
+    index = tz.OpIndex(graph)
+    cands = [index.sequence_from_json(j) for j in payload["seqs"]]
+    rec["search_best_pct10_ms"] = payload["pct10"][0] * 1e3
     ranked = list(range(len(cands)))
     if len(cands) > 1:
         rr = bench.benchmark_many(cands, tz.BenchOpts(n_iters=bench_iters, max_retries=1,

@@ -45,7 +45,8 @@ def main():
                                             hostsplit=hostsplit,
                                             wide_puts=os.environ.get("TZ_TEST_WIDE", "auto"),
                                             comms=int(os.environ.get("TZ_TEST_COMMS", "0")),
-                                            hostsplit_chunks=int(os.environ.get("TZ_TEST_HS_CHUNKS", "1"))),
+                                            hostsplit_chunks=int(os.environ.get("TZ_TEST_HS_CHUNKS", "1")),
+                                            copy_engines=int(os.environ.get("TZ_TEST_COPY_ENGINES", "1"))),
                                ctrl, dev)
             out["relay_ready"] = halo.uses_relay()
             out["transports"] = halo.transport_report()

@@ -8,6 +8,8 @@ import subprocess
 import sys
 import time
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 BODY = r"""
@@ -296,16 +298,15 @@ def test_foreign_listener_with_one_candidate_port_fails_fast():
 
 def test_graph_capture_info_defaults():
     """the record of how schedules become hipGraphs (bench.py's `graph_capture`): whole-schedule
-    capture, no extra root, 6 streams owned at least; env overrides are reported as forced"""
+    capture, 6 streams owned at least; env settings (applied at import) are reported as forced"""
     code = ("import sys, json; sys.path.insert(0, %r); import tenzing_amd as tz; "
             "print(json.dumps(tz._tz.graph_capture_info()))" % ROOT)
     env = {k: v for k, v in os.environ.items()
-           if k not in ("TZ_GRAPH_CAPTURE", "TZ_GRAPH_ROOT", "TZ_PAD_STREAMS")}
+           if k not in ("TZ_GRAPH_CAPTURE", "TZ_PAD_STREAMS")}
     env["TZ_NO_TORCH"] = "1"
     j = json.loads(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True,
                                   text=True, timeout=120).stdout.strip().splitlines()[-1])
-    assert j == {"mode": "schedule", "forced": False, "rccl_mode": "schedule", "root": "none",
-                 "pad_streams": 6}, j
+    assert j == {"mode": "schedule", "forced": False, "rccl_mode": "schedule", "pad_streams": 6}, j
     env.update(TZ_GRAPH_CAPTURE="child", TZ_PAD_STREAMS="0")
     j = json.loads(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True,
                                   text=True, timeout=120).stdout.strip().splitlines()[-1])
@@ -410,3 +411,56 @@ print("JOINED", c.allreduce_max([float(c.rank)])[0])
                 p.kill()
     assert all(p.returncode == 0 for p in ps), outs
     assert all("JOINED 2.0" in o[0] for o in outs), outs
+
+
+def test_runtime_options_flip_both_ways_in_one_process(tz):
+    """the kept tuning options are runtime options, not environment
+    variables cached in statics: each is set both ways and read back inside one process
+    (capture mode, default stream padding, the box kernels' peel / widened unpack / cache
+    policies / block order / put cap, and the halo's IPC mode, copy-engine puts, copy engines and
+    row-pair moves as HaloArgs fields)"""
+    k = tz._tz.kernels
+    info = tz._tz.graph_capture_info
+    try:
+        for mode, forced in (("child", True), ("schedule", True), ("auto", False)):
+            tz._tz.set_graph_capture(mode)
+            i = info()
+            assert i["forced"] is forced and i["mode"] == ("child" if mode == "child" else "schedule")
+        for n in (0, 9, 6):
+            tz._tz.set_default_pad_streams(n)
+            assert info()["pad_streams"] == n
+        with pytest.raises(Exception):
+            tz._tz.set_graph_capture("bogus")
+    finally:
+        tz._tz.set_graph_capture("auto")
+        tz._tz.set_default_pad_streams(6)
+    pairs = ((k.set_peel_moves, k.get_peel_moves), (k.set_widen_unpack, k.get_widen_unpack),
+             (k.set_nt_move_store, k.get_nt_move_store))
+    for setter, getter in pairs:
+        prev = getter()
+        for v in (not prev, prev):
+            setter(v)
+            assert getter() == v
+    for setter, getter, vals in ((k.set_xcd_remap, k.get_xcd_remap, (2, 1, 0)),
+                                 (k.set_put_max_blocks, k.get_put_max_blocks, (16, 64)),
+                                 (k.set_move_unroll, k.get_move_unroll, (2, 1))):
+        for v in vals:
+            setter(v)
+            assert getter() == v
+    prev = k.get_box_tuning()
+    k.set_box_tuning(prev[0], not prev[1], not prev[2], prev[3], not prev[4])
+    assert k.get_box_tuning()[1:3] == (not prev[1], not prev[2])
+    k.set_box_tuning(*prev)
+    assert k.get_box_tuning() == prev
+    # halo options: fields of the arguments, so one process builds both sides
+    from tenzing_amd.models import HaloConfig
+
+    for grid in (0, 1):
+        for copy in (True, False):
+            h = tz._tz.HaloExchange(HaloConfig(n=16, ipc_grid=grid, copy_puts=copy, copy_engines=2,
+                                               transport="ipc").args(0, 2, -1))
+            assert h.ipc_mode() == ("grid" if grid else "buffers")
+            assert h.args.copy_engines == 2 and h.args.copy_puts is copy
+    for pairs_on in (True, False):
+        a = HaloConfig(n=16, order="xyzq", move_pairs=pairs_on).args(0, 1, -1)
+        assert a.move_pairs is pairs_on and '"move_pairs":%s' % str(pairs_on).lower() in a.json().replace(" ", "")

@@ -241,3 +241,71 @@ def test_box_move_cache_policies(tz, gpu, ntload, ntstore):
         k.set_box_tuning(*prev)
         k.set_nt_move_store(prev_st)
     assert torch.equal(out, exp)
+
+
+def _rows(box, lead=0, trail=0):
+    """(offset, length) of every grid row of a box, widened by lead / trail elements"""
+    for i3 in range(box["n3"]):
+        for i2 in range(box["n2"]):
+            for i1 in range(box["n1"]):
+                yield (box["grid_off"] + i1 * box["s1"] + i2 * box["s2"] + i3 * box["s3"] - lead,
+                       lead + box["len"] + trail)
+
+
+def _mask(n, boxes, widened):
+    m = torch.zeros(n, dtype=torch.bool)
+    for b in boxes:
+        for off, ln in _rows(b, *((b["lead"], b["trail"]) if widened else (0, 0))):
+            m[off:off + ln] = True
+    return m.to("cuda")
+
+
+@pytest.mark.parametrize("align", [16, 8])
+@pytest.mark.parametrize("order", ["xyzq", "qxyz"])
+@pytest.mark.parametrize("neighbors", [6, 26])
+def test_widened_unpack_matches_torch(tz, gpu, order, neighbors, align):
+    """the unpack through unpack_box(i), whose x-ghost rows are widened over
+    the row padding (lead / trail > 0), from a random buffer, one box at a time and all boxes in
+    one batch. Every logical ghost cell is exact (torch strided reference), nothing outside
+    [row start - lead, row end + trail) changes, and the widened elements are padding: no pack
+    or unpack box of any direction covers them."""
+    a = tz.HaloArgs()
+    a.nx, a.ny, a.nz, a.nq, a.ghost = 20, 12, 9, 3, 3
+    a.neighbors, a.order, a.ghost_align = neighbors, order, align
+    h = tz.HaloExchange(a)
+    n = h.grid_elems()
+    grid = torch.randn(n, dtype=torch.float64, device="cuda")
+    ub = [h.unpack_box(i) for i in range(h.ndirs())]
+    pb = [h.pack_box(i) for i in range(h.ndirs())]
+    assert any(b["lead"] > 0 or b["trail"] > 0 for b in ub), "no widened box: the test is void"
+    logical_all = _mask(n, ub + pb, False)
+    srcs, exp_all = [], grid.clone()
+    for i, b in enumerate(ub):
+        cnt = b["len"] * b["n1"] * b["n2"] * b["n3"]
+        src = torch.randn(cnt, dtype=torch.float64, device="cuda")
+        srcs.append(src)
+        b["buf"] = src.data_ptr()
+        # one box: exact ghost cells, changes only inside the widened rows
+        g2 = grid.clone()
+        tz._tz.kernels.box_copy(g2.data_ptr(), b, True, _stream())
+        exp = grid.clone()
+        srcv = src.view(b["n3"], b["n2"], b["n1"], b["len"])
+        for i3 in range(b["n3"]):
+            for i2 in range(b["n2"]):
+                base = b["grid_off"] + i2 * b["s2"] + i3 * b["s3"]
+                for e in (exp, exp_all):
+                    e.as_strided((b["n1"], b["len"]), (b["s1"], 1), base).copy_(srcv[i3, i2])
+        torch.cuda.synchronize()
+        mine, allowed = _mask(n, [b], False), _mask(n, [b], True)
+        assert torch.equal(g2[mine], exp[mine]), f"ghost cells wrong, box {h.dir_name(i)}"
+        assert torch.equal(g2[~allowed], grid[~allowed]), "unpack wrote outside its widened rows"
+        # the widening covers row padding only
+        assert not (allowed & ~mine & logical_all).any(), "widened over a logical cell"
+    # all boxes in one batch launch
+    g3 = grid.clone()
+    tz._tz.kernels.box_copy_many(g3.data_ptr(), ub, True, _stream())
+    torch.cuda.synchronize()
+    allowed = _mask(n, ub, True)
+    ghosts = _mask(n, ub, False)
+    assert torch.equal(g3[ghosts], exp_all[ghosts])
+    assert torch.equal(g3[~allowed], grid[~allowed])

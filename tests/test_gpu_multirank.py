@@ -152,11 +152,11 @@ def test_mixed_engines_loopback(gpu, world):
 
 
 def test_copy_puts_over_two_engines_loopback(gpu):
-    """copy-engine puts cut over two engine streams (TZ_COPY_ENGINES=2: a fork to a side stream
+    """copy-engine puts cut over two engine streams (copy_engines=2: a fork to a side stream
     and a join back inside the op): exact eager and inside whole-schedule hipGraph captures,
     where the side stream's capture dependencies are set per op (no false edge between copy ops
     of different schedule streams)"""
-    extra = {"TZ_IPC_GRID": "0", "TZ_COPY_ENGINES": "2", "TZ_TEST_FUSES": "choice",
+    extra = {"TZ_IPC_GRID": "0", "TZ_TEST_COPY_ENGINES": "2", "TZ_TEST_FUSES": "choice",
              "TZ_TEST_REQUIRE": "he_copyput_", "TZ_TEST_SEEDS": "3", "TZ_TEST_NO_MCTS": "1"}
     res = _launch("ipc_halo", 2, extra_env=extra)
     for r in res:
@@ -238,7 +238,7 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
-           "--cells", "64", "--mcts-iters", "6", "--bench-iters", "3", "--deadline-s", "240"]
+           "--cells", "64", "--mcts-iters", "6", "--bench-iters", "3", "--deadline-s", "240", "--subrecords", "off"]
     env = dict(os.environ, TZ_IPC_GRID="1" if mode == "grid" else "0")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=160, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
@@ -325,7 +325,7 @@ def test_bench_two_ranks_under_mpiexec(gpu):
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     cmd = [mpiexec, "-n", "2", sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
            "--steps", "6", "--warmup", "2", "--cells", "64", "--mcts-iters", "6",
-           "--bench-iters", "3", "--deadline-s", "240", "--link-probe-iters", "0"]
+           "--bench-iters", "3", "--deadline-s", "240", "--subrecords", "off", "--link-probe-iters", "0"]
     r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=160, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -425,9 +425,9 @@ def test_bench_host_fallback_loopback(gpu, tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
-           "--cells", "48", "--mcts-iters", "6", "--bench-iters", "2", "--deadline-s", "240",
-           "--link-probe-iters", "0"]
-    env = dict(os.environ, TZ_IPC_COPY="0", TZ_FAIL_TRANSPORTS="ipc")
+           "--cells", "48", "--mcts-iters", "6", "--bench-iters", "2", "--deadline-s", "240", "--subrecords", "off",
+           "--link-probe-iters", "0", "--copy-puts", "off"]
+    env = dict(os.environ, TZ_FAIL_TRANSPORTS="ipc")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=160, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     j = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
@@ -466,7 +466,7 @@ def test_bench_rejected_finalist_loopback(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
-           "--cells", "48", "--mcts-iters", "8", "--bench-iters", "2", "--deadline-s", "240",
+           "--cells", "48", "--mcts-iters", "8", "--bench-iters", "2", "--deadline-s", "240", "--subrecords", "off",
            "--link-probe-iters", "0", "--hostsplit", "off"]
     env = dict(os.environ, TZ_IPC_GRID="0", TZ_BENCH_REJECT="1")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=160, env=env)
@@ -492,8 +492,7 @@ def test_rccl_node_overlaps_kernels_loopback(gpu):
     res = _launch("rccl_overlap", 2, extra_env={"TZ_RCCL_LOOPBACK": "1"})
     for r in res:
         assert r["effective_mode"] == "ExecMode.Graph" and r["bad"] == [0, 0, 0], r
-        # 2 busy kernels + the RCCL kernel (+ the capture root, an empty kernel, unless TZ_GRAPH_ROOT
-        # says otherwise)
+        # 2 busy kernels + the RCCL kernel (RCCL may add a kernel node of its own)
         assert r["node_types"].get("kernel") in (3, 4) and "child_graph" not in r["node_types"], r
         # concurrent kernels: never the serial sum of the two
         assert r["iter_us"] < 1.75 * r["one_kernel_us"], r
@@ -542,7 +541,7 @@ def test_bench_rccl_across_ranks_loopback(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
-           "--cells", "48", "--mcts-iters", "8", "--bench-iters", "2", "--deadline-s", "240",
+           "--cells", "48", "--mcts-iters", "8", "--bench-iters", "2", "--deadline-s", "240", "--subrecords", "off",
            "--link-probe-iters", "2", "--link-probe-rccl", "--hostsplit", "off"]
     env = dict(os.environ, TZ_IPC_GRID="0", TZ_RCCL_LOOPBACK="1")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=160, env=env)
@@ -595,7 +594,7 @@ def test_bench_stall_after_headline_loopback(gpu, how):
     if how == "phase":
         env["TZ_BENCH_STALL"] = "link_matrix"
     else:
-        env["TZ_LINK_MATRIX_STALL"] = "1"
+        env["TZ_FAIL_TRANSPORTS"] = "link_matrix_stall"
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=170, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -609,3 +608,39 @@ def test_bench_stall_after_headline_loopback(gpu, how):
         lm = j["link_matrix"]
         assert lm["stuck"] is True and "did not complete" in lm["why"], lm
         assert "link_matrix" in j["post_timing"]["done"]
+
+
+def test_bench_self_launched_two_ranks_with_subrecords_loopback(gpu):
+    """`bench.py --gpus 2` with no launcher in the environment starts
+    its own two rank processes (one line, n_gpus 2, rank grid 1x1x2), and the multi-GPU record
+    carries BASELINE configs 2 and 5 searched over the ranks' transports, each verified exact,
+    with the transport its winner used, the matrix's nnz summed over ranks and the RCCL
+    communicator size (RCCL is refused for two ranks on one device, so the SpMV halo goes over
+    IPC puts here)"""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                        "MASTER_PORT", "PMI_SIZE", "PMI_RANK", "PMIX_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+           "--warmup", "5", "--cells", "64", "--mcts-iters", "6", "--bench-iters", "3",
+           "--deadline-s", "280", "--link-probe-iters", "2"]
+    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["launcher"] == "bench.py" and j["config"]["rank_grid"] == [1, 1, 2]
+    assert j["partial"] is False and j["verified_bad_cells"] == 0
+    assert j["verified_bad_cells_after_timing"] == 0
+    assert "baseline_configs" in j["post_timing"]["done"], j["post_timing"]
+    assert "reference_layout" not in j  # one-rank only
+    bc = j["baseline_configs"]
+    assert "error" not in bc, bc
+    sp, fu = bc["spmv_c2"], bc["fused_c5"]
+    for rec in (sp, fu):
+        assert "error" not in rec, rec
+        assert rec["verified_bad"] == 0 and rec["verified_bad_after_timing"] == 0, rec
+        assert rec["ms_per_step"] > 0 and rec["config"]["ranks"] == 2
+        assert rec["config"]["nnz"] == 1_500_000 and rec["config"]["bw"] == 75_000
+        assert rec["config"]["spmv_transport"] in ("ipc", "rccl"), rec["config"]
+    assert sp["config"]["rccl_nranks"] is None  # (loopback: RCCL refused)
+    assert fu["config"]["halo_transport"] not in (None, "direct"), fu["config"]

@@ -114,12 +114,12 @@ def test_rccl_graph_preflight_falls_back_to_child_capture(tz, gpu, monkeypatch):
 
 def test_rccl_preflight_hang_is_bounded(tz, gpu, monkeypatch):
     """a preflight exchange that never completes (simulated: a spinning kernel ahead of it) is
-    cut off after TZ_RCCL_PREFLIGHT_S: the communicators are aborted and a forced RCCL transport
+    cut off after TZ_PREFLIGHT_S: the communicators are aborted and a forced RCCL transport
     fails setup with the reason instead of hanging"""
     from tenzing_amd.models import HaloConfig, build_halo
 
     monkeypatch.setenv("TZ_FAIL_TRANSPORTS", "rccl_hang")
-    monkeypatch.setenv("TZ_RCCL_PREFLIGHT_S", "3")
+    monkeypatch.setenv("TZ_PREFLIGHT_S", "3")
     t0 = time.time()
     with pytest.raises(Exception, match="preflight"):
         build_halo(HaloConfig(n=32, neighbors=26, transport="rccl"), tz.SelfCtrl(), device=gpu)

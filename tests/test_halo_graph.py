@@ -7,13 +7,14 @@ pack-free direct move each and remote directions keep pack -> RCCL shift -> unpa
 import pytest
 
 
-def _halo(tz, size, transport="auto", fuse="none", neighbors=26, rank=0, hostsplit="off"):
+def _halo(tz, size, transport="auto", fuse="none", neighbors=26, rank=0, hostsplit="off",
+          ipc_grid=-1):
     # (host split off unless asked for: its alternatives would thin out the random rollouts
     # the older tests count transports in)
     a = tz.HaloArgs()
     a.nx = a.ny = a.nz = 16
     a.neighbors, a.transport, a.fuse = neighbors, transport, fuse
-    a.rank, a.size, a.hostsplit = rank, size, hostsplit
+    a.rank, a.size, a.hostsplit, a.ipc_grid = rank, size, hostsplit, ipc_grid
     h = tz.HaloExchange(a)
     g = tz.Graph()
     h.add_to_graph(g)
@@ -98,8 +99,7 @@ def test_copy_and_direct_need_self_neighbours(tz):
 def test_ipc_transport_graph(tz, fuse, size, mode, monkeypatch):
     """ipc: self-neighbour moves, pack-free puts for remote directions, one arrival wait that
     every put precedes (and, in "buffers" mode, one unpack after the wait)"""
-    monkeypatch.setenv("TZ_IPC_GRID", "1" if mode == "grid" else "0")
-    h, g = _halo(tz, size, transport="ipc", fuse=fuse)
+    h, g = _halo(tz, size, transport="ipc", fuse=fuse, ipc_grid=1 if mode == "grid" else 0)
     assert h.ipc_mode() == mode
     n_ipc = sum(h.is_ipc(i) for i in range(h.ndirs()))
     assert n_ipc == 26 - sum(h.is_direct(i) for i in range(h.ndirs()))
@@ -189,7 +189,7 @@ def test_relay_routing_graph(tz, transport, monkeypatch):
         js = seq.json(True)
         for other in graphs[1:]:
             tz.OpIndex(other).sequence_from_json(js)
-    assert fracs == {"he_rl15", "he_rl20"} and fwds == {"fwd", "fwdcp"}
+    assert fracs == {"he_rl15", "he_rl20", "he_rl25"} and fwds == {"fwd", "fwdcp"}
     # forced: the only remote transport
     a = HaloConfig(n=16, neighbors=6, order="qxyz", fuse="choice", transport="ipc", relay="force",
                    relay_fracs=(0.25,)).args(3, 8, -1)
@@ -285,8 +285,7 @@ def test_hostsplit_graph(tz, size, monkeypatch):
     """buffers mode offers host split (a share of every face through node shared host memory,
     the rest as IPC puts), one alternative per share: both puts precede the one wait, the
     unpack follows it; forced, it is the only remote transport"""
-    monkeypatch.setenv("TZ_IPC_GRID", "0")
-    h, g = _halo(tz, size, fuse="choice", hostsplit="auto")
+    h, g = _halo(tz, size, fuse="choice", hostsplit="auto", ipc_grid=0)
     assert h.uses_hostsplit()
     from tenzing_amd.search import choice_alternatives, greedy_schedule
     alts = choice_alternatives(g, "he_remote")
@@ -303,13 +302,13 @@ def test_hostsplit_graph(tz, size, monkeypatch):
     a = tz.HaloArgs()
     a.nx = a.ny = a.nz = 16
     a.neighbors, a.fuse, a.rank, a.size, a.hostsplit = 26, "choice", 0, size, "force"
+    a.ipc_grid = 0
     hf = tz.HaloExchange(a)
     gf = tz.Graph()
     hf.add_to_graph(gf)
     assert choice_alternatives(gf, "he_remote") == ["he_via_hs10", "he_via_hs20", "he_via_hs30", "he_via_hs40"]
     # grid mode has no receive buffers: not offered
-    monkeypatch.setenv("TZ_IPC_GRID", "1")
-    hg, _ = _halo(tz, size, hostsplit="auto")
+    hg, _ = _halo(tz, size, hostsplit="auto", ipc_grid=1)
     assert not hg.uses_hostsplit()
 
 
@@ -378,8 +377,8 @@ def test_wide_puts_are_a_transport_alternative(tz, monkeypatch, fuse, grid_mode)
     default put's. Graph-only builds offer it only when asked ("auto" decides at setup)."""
     from tenzing_amd.search import choice_alternatives, greedy_schedule
 
-    monkeypatch.setenv("TZ_IPC_GRID", grid_mode)
     a = tz.HaloArgs()
+    a.ipc_grid = int(grid_mode)
     a.nx = a.ny = a.nz = 16
     a.neighbors, a.fuse, a.rank, a.size, a.hostsplit, a.relay = 26, fuse, 0, 8, "off", "off"
     h0 = tz.HaloExchange(a)

@@ -440,3 +440,30 @@ def test_spmv_root_distribution_matches_local_derivation(tmp_path):
         # band of half-width m / 3: the middle rank's rows reach both neighbours, the ends one
         assert r["root"]["nnz"] == 300_000 and r["root"]["peers"] == (2 if r["rank"] == 1 else 1)
     assert sum(r["root"]["local"] + r["root"]["remote"] for r in rs) == 300_000
+
+
+def body_spmv_root_error_reaches_every_rank():
+    """rank 0 fails to read the matrix under root distribution; every rank throws the
+    same error right after the row-block exchange (no rank waits in it), and the control plane
+    stays in step for the next collective"""
+    import tenzing_amd as tz
+    from tenzing_amd.models import SpmvConfig
+    from tenzing_amd.parallel import init_ctrl
+
+    c = init_ctrl(timeout_s=30)
+    err = ""
+    try:
+        tz._tz.DistSpmv(SpmvConfig(m=3_000, matrix="/nonexistent/m.mtx",
+                                   distribute="root").args(c.rank, c.size, -1), c)
+    except Exception as e:  # noqa: BLE001
+        err = str(e)
+    # the next collective lines up: a fresh root-distributed setup succeeds on every rank
+    s = tz._tz.DistSpmv(SpmvConfig(m=3_000, distribute="root").args(c.rank, c.size, -1), c)
+    return {"rank": c.rank, "err": err, "nnz": s.args.nnz_actual}
+
+
+def test_spmv_root_error_reaches_every_rank(tmp_path):
+    rs = _run("body_spmv_root_error_reaches_every_rank", 3, tmp_path)
+    for r in rs:
+        assert "rank 0 failed" in r["err"] and "m.mtx" in r["err"], r
+        assert r["nnz"] == 30_000, r

@@ -75,11 +75,11 @@ def rccl_positions(seq):
     return [p for p, op in enumerate(seq.ops()) if op.order_domain == "rccl"]
 
 
-def _halo(tz, size, transport="auto", fuse="choice", wide_puts="auto"):
+def _halo(tz, size, transport="auto", fuse="choice", wide_puts="auto", ipc_grid=-1):
     a = tz.HaloArgs()
     a.nx = a.ny = a.nz = 16
     a.neighbors, a.transport, a.fuse, a.wide_puts = 26, transport, fuse, wide_puts
-    a.rank, a.size = 0, size
+    a.rank, a.size, a.ipc_grid = 0, size, ipc_grid
     h = tz.HaloExchange(a)
     g = tz.Graph()
     h.add_to_graph(g)
@@ -296,8 +296,7 @@ def test_one_seed_per_transport(tz, monkeypatch):
     transport; measured as seeds, every one lands in the tree"""
     from tenzing_amd.search import choice_alternatives, greedy_schedule
 
-    monkeypatch.setenv("TZ_IPC_GRID", "0")
-    h, g = _halo(tz, 8, wide_puts="on")
+    h, g = _halo(tz, 8, wide_puts="on", ipc_grid=0)
     alts = choice_alternatives(g, "he_remote")
     assert {"he_via_rccl", "he_via_ipc", "he_via_ipcw", "he_via_sdma", "he_via_memcpy",
             "he_via_mixed"} <= set(alts)

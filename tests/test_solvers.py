@@ -502,3 +502,31 @@ def test_graph_params_from_the_branch_probe(tz):
     q = graph_params_from_probe(link_sim_params(), {"pad_streams": 6, "tried": [
         {"pad_streams": 6, "probe": {"branches": 3, "one_us": 207.8, "all_us": 245.1}}]})
     assert q.graph_join_us == 5.5  # no unrolled form: the defaults stay
+
+
+def test_link_model_counts_only_transfers_that_overlap_in_time(tz):
+    """ops are simulated in program order, not start-time order. A transfer issued
+    first but starting later (behind a long op on its stream) must not slow a transfer that is
+    issued after it, runs earlier and is over before it starts; one that does overlap still
+    shares the link"""
+    from tenzing_amd.parallel.linkmodel import link_sim_params
+
+    p = link_sim_params(put=100)
+    p.resource_GBps = {"hbm": 5000.0, "xgmi": 100.0, "pcie": 50.0}
+    mb = 10e6  # 100 us alone
+
+    def run(wait_us):
+        seq = tz._tz.Sequence()
+        seq.append(tz.BoundGpuOp(tz.SimGpuOp("w", wait_us), 0))
+        seq.append(tz.BoundGpuOp(tz.SimGpuOp("late", 0.0, traffic=[("xgmi:1", "put", mb)]), 0))
+        seq.append(tz.BoundGpuOp(tz.SimGpuOp("early", 0.0, traffic=[("xgmi:1", "put", mb)]), 1))
+        ex = tz.SimExecutor(2, p)
+        ex.run_once(seq)
+        return {n: (t0, t1) for n, s, t0, t1 in ex.trace()}
+
+    apart = run(300.0)  # "late" starts at ~300 us, "early" is done by ~100 us
+    assert apart["late"][0] > apart["early"][1], apart
+    for n in ("late", "early"):
+        assert abs(apart[n][1] - apart[n][0] - 100.0) < 1.0, apart
+    both = run(50.0)  # "late" starts at ~50 us while "early" still runs: they share the link
+    assert both["early"][1] - both["early"][0] > 140.0, both
