@@ -203,17 +203,20 @@ def search_record(tz, ctrl, rt, graph, streams: int, verify, steps: int, warmup:
                   mcts_iters: int = 40, bench_iters: int = 6, target_secs: float = 0.002,
                   search_unroll: int = 10, graph_unroll: int = 20, seed: int = 0,
                   time_budget_s: float = 30.0, strategy: str = "FastMin", rerank: int = 4,
-                  seeds=()):
+                  seeds=(), bench=None):
     """Search ``graph`` briefly (MCTS, hipGraph candidates, racing and settling as the headline),
     re-rank the ``rerank`` best distinct candidates interleaved, verify the winner with
     ``verify(seq) -> bad count`` (the next finalist if it fails), then time it eagerly and as a
     hipGraph exactly as the headline is timed. ``seeds``: schedules measured before the search
-    (they count as results). Returns the sub-record dict."""
+    (they count as results); ``bench``: the benchmarker (default: an EmpiricalBenchmarker on
+    ``rt``; tests pass a simulator). Every rank must call it together. Returns the sub-record
+    dict."""
     t_start = time.time()
     plat = tz.Platform(streams)
     rt.set_mode(tz.ExecMode.Graph)
     rt.set_graph_unroll(search_unroll)
-    bench = tz.EmpiricalBenchmarker(rt, ctrl)
+    if bench is None:
+        bench = tz.EmpiricalBenchmarker(rt, ctrl)
     o = tz.MctsOpts()
     o.n_iters = mcts_iters
     o.time_budget_s = time_budget_s
@@ -251,8 +254,11 @@ def search_record(tz, ctrl, rt, graph, streams: int, verify, steps: int, warmup:
     rec["search_best_pct10_ms"] = payload["pct10"][0] * 1e3
     ranked = list(range(len(cands)))
     if len(cands) > 1:
-        rr = bench.benchmark_many(cands, tz.BenchOpts(n_iters=bench_iters, max_retries=1,
-                                                      target_secs=target_secs), seed)
+        ro = tz.BenchOpts(n_iters=bench_iters, max_retries=1, target_secs=target_secs)
+        if hasattr(bench, "benchmark_many"):  # interleaved
+            rr = bench.benchmark_many(cands, ro, seed)
+        else:
+            rr = [bench.benchmark(c, ro) for c in cands]
         ranked = sorted(range(len(rr)), key=lambda i: rr[i].pct10)
         rec["rerank_pct10_ms"] = [round(r.pct10 * 1e3, 5) for r in rr]
     rt.set_mode(tz.ExecMode.Eager)

@@ -467,3 +467,59 @@ def test_spmv_root_error_reaches_every_rank(tmp_path):
     for r in rs:
         assert "rank 0 failed" in r["err"] and "m.mtx" in r["err"], r
         assert r["nnz"] == 30_000, r
+
+
+def body_search_record_in_step():
+    """bench.py's sub-record flow (search, re-rank, verify, eager and graph timing) on 2 ranks:
+    only rank 0 holds the search results, so the finalists travel from rank 0 and every rank
+    re-ranks, verifies and times the same schedules in the same collectives (round 6: a rank
+    without results left early and the control plane fell out of step)"""
+    import tenzing_amd as tz
+    from tenzing_amd.parallel import init_ctrl
+    from tenzing_amd.utils.benchkit import search_record
+
+    c = init_ctrl(timeout_s=60)
+
+    class FakeRuntime:  # the HipRuntime calls search_record / timed_replay make
+        mode = tz.ExecMode.Graph
+
+        def set_mode(self, m):
+            self.mode = m
+
+        @property
+        def effective_mode(self):
+            return self.mode
+
+        def set_graph_unroll(self, n):
+            pass
+
+        def prepare(self, seq):
+            self.seq = seq
+
+        def run(self, n):
+            pass
+
+        def device_sync(self):
+            pass
+
+    verified = []
+
+    def verify(seq):
+        verified.append(None if seq is None else seq.canonical_key())
+        return int(c.allreduce_sum([0.0])[0])  # a collective, like the real checks
+
+    g = _diamond()
+    rec = search_record(tz, c, FakeRuntime(), g, 2, verify, steps=4, warmup=1, mcts_iters=8,
+                        bench=tz.SimBenchmarker(2, tz.SimParams(), c))
+    return {"rank": c.rank, "rec": {k: v for k, v in rec.items() if k not in ("wall_s", "search_wall_s")},
+            "verified": verified}
+
+
+def test_search_record_keeps_every_rank_in_step(tmp_path):
+    rs = _run("body_search_record_in_step", 2, tmp_path)
+    assert "error" not in rs[0]["rec"], rs[0]
+    assert rs[0]["rec"]["mcts_candidates"] >= 1 and rs[0]["rec"]["verified_bad"] == 0
+    # the same finalists, verified in the same order, and the same record on both ranks
+    assert rs[0]["verified"] == rs[1]["verified"] and rs[0]["verified"][-1] is None
+    assert {k: v for k, v in rs[0]["rec"].items() if "ms" not in k} == \
+           {k: v for k, v in rs[1]["rec"].items() if "ms" not in k}
