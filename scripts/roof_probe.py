@@ -17,6 +17,23 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _time_move(halo, iters):
+    """us per 26-direction move, event-timed over `iters` back-to-back launches after 3 warm-up"""
+    import torch
+
+    st = torch.cuda.current_stream()
+    dirs = list(range(halo.ndirs()))
+    for _ in range(3):
+        halo.direct_group(dirs, st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        halo.direct_group(dirs, st.cuda_stream)
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=512)
@@ -27,23 +44,40 @@ def main():
                          "pitch_pad: extra row-pitch elements, 528 + pad for 512^3 XYZQ)")
     ap.add_argument("--pairs", default="on", choices=["on", "off"],
                     help="XYZQ x self-wrap moves as row pairs (HaloConfig.move_pairs)")
+    ap.add_argument("--prealloc-mb", default="0",
+                    help="comma list: before each layout's grid is allocated, hold this many MB "
+                         "of device memory, so the grid lands on other physical memory (one "
+                         "JSON line per layout and size)")
     a = ap.parse_args()
+    import torch
+
     import tenzing_amd as tz
     from tenzing_amd.models import HaloConfig, build_halo
 
-    for spec in a.layouts.split(","):
+    specs = [(spec, int(mb)) for mb in a.prealloc_mb.split(",") for spec in a.layouts.split(",")]
+    for spec, mb in specs:
+        hold = torch.empty(mb << 20, dtype=torch.uint8, device="cuda") if mb > 0 else None
         order, align, *pad = spec.split(":")
         pad = int(pad[0]) if pad else 0
         halo, _ = build_halo(HaloConfig(n=a.n, neighbors=a.neighbors, order=order,
                                         ghost_align=int(align), transport="direct",
                                         move_pairs=a.pairs == "on", pitch_pad=pad),
                              tz.SelfCtrl(), 0)
-        r = halo.move_roof(a.iters)
+        try:
+            r = halo.move_roof(a.iters)
+            r["move_over_roof"] = min(r["move_us"], r["move_us_again"]) / r["roof_us"]
+        except RuntimeError as e:
+            # no line-shaped roof for this layout (row strides not whole 128-B lines): the move
+            # alone, event-timed, back to back on one stream
+            r = {"roof": str(e), "move_us": _time_move(halo, a.iters),
+                 "move_us_again": _time_move(halo, a.iters)}
+        va = halo.grid_ptr()
         r.update(order=order, ghost_align=int(align), pitch_pad=pad, layout=halo.layout(),
-                 move_pairs=a.pairs)
-        r["move_over_roof"] = min(r["move_us"], r["move_us_again"]) / r["roof_us"]
+                 move_pairs=a.pairs, prealloc_mb=mb, grid_va=hex(va),
+                 grid_va_mod_2MB=va % (2 << 20), grid_va_mod_1GB=va % (1 << 30))
         print(json.dumps(r), flush=True)
-        del halo
+        del halo, hold
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
