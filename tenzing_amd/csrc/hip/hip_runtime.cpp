@@ -85,7 +85,7 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
   // own; with 3 schedule streams one of those landed on the launch stream's queue (three
   // independent 200 us kernels: 447 us per launch; with 4-8 streams owned: 241-244 us; a host
   // node then a kernel beside two kernels: 319 -> 241 us). 6: the RCCL probe between two
-  // loopback ranks also stays at its unpadded time (profiles/r4_pad/)
+  // loopback ranks also stays at its unpadded time (profiles/archive/r4_pad/)
   pad_ = opts.pad_streams >= 0 ? opts.pad_streams : tz::pad_streams();
   for (int i = opts.n_streams; i < pad_; ++i) {
     hipStream_t s = nullptr;
@@ -534,7 +534,7 @@ std::vector<void *> GraphBuilder::add(int stream, const std::vector<void *> &dep
   // capture stream suffices. It also keeps every side stream an op forks internally (RCCL's
   // own streams, copy engines) joined to the origin itself: HIP 7.0's hipStreamEndCapture
   // recursed without end when RCCL's streams had joined the capture through other forked
-  // streams (profiles/r4_capture/self_torchrt2.log)
+  // streams (profiles/archive/r4_capture/self_torchrt2.log)
   hipStream_t origin = S(streams_[0]);
   TZ_LOG(Debug, "capture: op of stream " << stream << " behind " << deps.size() << " node(s)");
   TZ_HIP(hipStreamUpdateCaptureDependencies(origin, deps.empty() ? nullptr : deps.data(), deps.size(),

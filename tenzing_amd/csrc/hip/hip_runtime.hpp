@@ -215,7 +215,7 @@ Json chrome_trace(const std::vector<HipRuntime::Span> &spans);
 ///    capture id and ties its lifetime to the captured graph (which lives as long as its exec).
 ///  * Child ("child"): every op captured alone into a graph of its own and added as a child-graph
 ///    node. Kept only for A/B diagnosis: HIP runs child-graph nodes one after another, so it
-///    costs all branch concurrency (profiles/r3b_rccl_loopback/child_graph_overlap.jsonl).
+///    costs all branch concurrency (profiles/archive/r3b_rccl_loopback/child_graph_overlap.jsonl).
 enum class CaptureMode { Schedule, Child };
 /// the mode for schedules without RCCL between ranks (default Schedule)
 CaptureMode capture_mode();
@@ -266,8 +266,8 @@ private:
 
 /// streams a runtime owns at least when its options say -1 (default 6; the spare ones are never
 /// used: they keep hipGraph branch streams off the launch stream's hardware queue,
-/// profiles/r4_pad/). (A single root node per captured schedule was measured too and retired:
-/// it changed neither the branch probes nor the RCCL probe, profiles/r4_root/.)
+/// profiles/archive/r4_pad/). (A single root node per captured schedule was measured too and retired:
+/// it changed neither the branch probes nor the RCCL probe, profiles/archive/r4_root/.)
 int pad_streams();
 /// set the default above (process-wide; python: TZ_PAD_STREAMS at import)
 void set_default_pad_streams(int n);

@@ -17,8 +17,8 @@ namespace tz {
 //                                  the receive buffer behind A; inbox credits (store ++count
 //                                  into r's inbox credit i); unpack the chunks
 // With several chunks the receiver's DMA of chunk c can overlap the sender's stores of chunk
-// c + 1 (a PCIe link carries 68 GB/s both ways at once vs 55 / 39 one way, profiles/r3_pcie);
-// measured, the per-chunk hand-offs cost more than that wins (profiles/r3_hs_chunks), so the
+// c + 1 (a PCIe link carries 68 GB/s both ways at once vs 55 / 39 one way, profiles/archive/r3_pcie);
+// measured, the per-chunk hand-offs cost more than that wins (profiles/archive/r3_hs_chunks), so the
 // default is one chunk: all stores, then one DMA.
 // Every host-memory counter has exactly one writer, so plain release stores publish them (no
 // PCIe AtomicOps). Same induction as IPC puts: puts wait only for credits of the previous

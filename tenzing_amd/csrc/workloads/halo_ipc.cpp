@@ -396,7 +396,7 @@ void HaloExchange::copy_put_group(const std::vector<int> &dirs, void *stream, bo
   // runtime picks the engine (hipMemcpyDeviceToDevice: blit kernels within one device, its
   // peer-copy path between devices). On loopback ranks (one GPU) the forced SDMA engines are
   // several times slower than the blit kernels (N=4: 0.49 ms vs 2.2 ms per exchange,
-  // profiles/r3_regress/), which is why both variants are offered and the search picks.
+  // profiles/archive/r3_regress/), which is why both variants are offered and the search picks.
   TZ_CHECK(ready() && ipcReady_ && useCopy_ && !ipcGrid_, "ipc copy-engine puts not set up");
   TZ_CHECK(!dirs.empty() && dirs.size() <= size_t(kern::kMaxBoxes), "bad copy-put group");
   hipStream_t s = static_cast<hipStream_t>(stream);

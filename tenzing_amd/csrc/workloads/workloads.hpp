@@ -247,7 +247,7 @@ struct HaloArgs {
   // the host share of a face travels in this many chunks, each signalled on its own, so the
   // receiver's DMA of one chunk can overlap the sender's PCIe stores of the next. Default 1 (all
   // stores, then one DMA): 4 chunks measured 7-17 % slower on 2 loopback ranks, whose PCIe
-  // link sees the same store / read-back mix as one GPU's link on a node (profiles/r3_hs_chunks)
+  // link sees the same store / read-back mix as one GPU's link on a node (profiles/archive/r3_hs_chunks)
   int hostsplit_chunks = 1;
   // wide kernel puts: the IPC put kernels with `wide_put_blocks` workgroups per box instead of
   // the global cap (BoxTuning::put_max_blocks, 64), offered to the search as a transport alternative.

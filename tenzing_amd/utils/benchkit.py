@@ -3,7 +3,7 @@
 * ``branch_probe`` / ``choose_pad``: does HIP's graph executor run three independent branches of
   a captured schedule at once on this box, with this runtime's stream padding? (round 4 found a
   3-branch graph serializing unless the process owns spare streams: 449 vs 232 us,
-  ``profiles/r4_capture/README.md:42-57``). The bench probes the runtime it is about to search
+  ``profiles/archive/r4_capture/README.md:42-57``). The bench probes the runtime it is about to search
   with, retries other paddings if the branches serialize, and records what it found.
 * ``timed_replay``: the timing contract of every number the bench reports (W untimed warm-up
   iterations, then K timed ones bracketed by barrier + device sync, max over ranks).

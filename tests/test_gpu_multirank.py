@@ -488,7 +488,7 @@ def test_rccl_node_overlaps_kernels_loopback(gpu):
     branch of the graph, so the two kernels still overlap (round 3's child graphs serialized
     every node: 424 us for the two kernels alone). HIP's graph executor runs a third branch of
     any kind partly behind the first two (~295 us with a 50 us kernel instead of RCCL,
-    profiles/r4_capture/), which the bound allows for"""
+    profiles/archive/r4_capture/), which the bound allows for"""
     res = _launch("rccl_overlap", 2, extra_env={"TZ_RCCL_LOOPBACK": "1"})
     for r in res:
         assert r["effective_mode"] == "ExecMode.Graph" and r["bad"] == [0, 0, 0], r
@@ -502,7 +502,7 @@ def test_rccl_node_overlaps_kernels_one_process(gpu):
     """the same probe in one process (a 1-rank communicator sending to itself): no second process
     shares the GPU and RCCL needs no network proxy, so its captured node is one kernel. The RCCL
     node beside two independent 200 us kernels then costs what any short third branch does:
-    231.6-244.4 us per launch measured on different boxes (profiles/r4_self_overlap/), within
+    231.6-244.4 us per launch measured on different boxes (profiles/archive/r4_self_overlap/), within
     VERDICT r3's 250 us; the assertion leaves box-to-box variance some room (1.3 x one kernel)"""
     res = _launch("rccl_overlap", 1, extra_env={"TZ_TEST_COMMS": "1"})
     r = res[0]
