@@ -1020,11 +1020,15 @@ def _baseline_configs(tz, args, ctrl, device, branch):
                     copy_puts=args.copy_puts == "on")
     h, s, g = build_fused(hc, SpmvConfig(m=150_000), ctrl, device)
     rt = _sub_runtime(tz, args, device, branch, 4)
-    # the largest tree of the BASELINE configs: one greedy seed with every group fused (the
-    # halo as one move on a stream of its own beside the SpMV), measured before the search
-    from tenzing_amd.search import greedy_schedule
-    seed = greedy_schedule(g, tz.Platform(4), {"*": ["allfused", "fused", "accum", "w16"]},
-                           stream_for=lambda n: 1 if n.startswith("he_") else 0)
+    # the largest tree of the BASELINE configs: greedy seeds measured before the search, one
+    # with every group fused (the halo as one move on a stream of its own beside the SpMV)
+    from tenzing_amd.search import choice_alternatives, greedy_schedule
+    seeds = [greedy_schedule(g, tz.Platform(4), {"hs_launches": "hs_separate",
+                                                 "*": ["allfused", "fused", "accum", "w16"]},
+                             stream_for=lambda n: 1 if n.startswith("he_") else 0)]
+    # one rank: the horizontally fused launch (move and SpMV in one kernel) as a second seed
+    if "hs_onelaunch_i4" in choice_alternatives(g, "hs_launches"):
+        seeds.append(greedy_schedule(g, tz.Platform(4), {"hs_launches": "hs_onelaunch_i4"}))
     hv, sv = _halo_verify(tz, rt, ctrl, h), spmv_verify(rt, s)
 
     def both(seq):
@@ -1033,8 +1037,9 @@ def _baseline_configs(tz, args, ctrl, device, branch):
         b = hv(seq)
         return b + sv(None)
     rec = search_record(tz, ctrl, rt, g, 4, both, steps, warmup, mcts_iters=60, search_unroll=8,
-                        seed=args.seed, seeds=[seed])
+                        seed=args.seed, seeds=seeds)
     names = rec.get("schedule_gpu_ops", [])
+    rec["one_launch"] = next((n for n in names if n.startswith("hs_onelaunch")), None)
     rec["config"] = {"halo": f"{args.n}^3 x 3q ghost 3, 26 neighbours, qxyz", "spmv_m": 150_000,
                      "streams": 4, "baseline_ms": 0.0544 if world == 1 else None,
                      "rank_grid": list(h.rank_grid()),

@@ -27,7 +27,7 @@ ARCH = os.environ.get("TZ_OFFLOAD_ARCH", "gfx950")
 
 CORE = ["json", "numeric", "ops", "graph", "state", "serdes", "ctrl", "ctrl_mpi", "benchmark", "solve", "health"]
 HIP_HOST = ["hip_runtime", "rccl_comm", "comm_ops", "rocsparse_spmv"]
-WORKLOADS = ["halo", "halo_ipc", "halo_relay", "halo_hostsplit", "halo_graph", "halo_stencil", "spmv", "workloads_common", "link_matrix"]
+WORKLOADS = ["halo", "halo_ipc", "halo_relay", "halo_hostsplit", "halo_graph", "halo_stencil", "spmv", "workloads_common", "link_matrix", "fused_ops"]
 KERNELS = ["halo_kernels", "spmv_kernels", "stencil_kernels"]
 
 

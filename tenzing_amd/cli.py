@@ -53,7 +53,7 @@ def _build_workload(a, ctrl, device, setup):
         s, g = build_spmv(sc, ctrl, device, setup)
         return g, {"spmv": s}
     if a.workload == "fused":
-        h, s, g = build_fused(hc, sc, ctrl, device, setup)
+        h, s, g = build_fused(hc, sc, ctrl, device, setup, horizontal=a.horizontal == "on")
         return g, {"halo": h, "spmv": s}
     if a.workload == "noop":
         # reference test/test_noop_graph.cpp: Start -> op1 -> Finish (here: `--noop-width`
@@ -209,7 +209,7 @@ def cmd_search(a) -> int:
 _WORKLOAD_KEYS = ("workload", "noop_width", "streams", "halo_n", "nq", "ghost", "neighbors",
                   "order", "fuse", "transport", "relay", "relay_fracs", "hostsplit",
                   "hostsplit_fracs", "hostsplit_chunks", "wide_puts", "wide_put_blocks",
-                  "ipc_grid", "copy_puts", "copy_engines", "move_pairs",
+                  "ipc_grid", "copy_puts", "copy_engines", "move_pairs", "horizontal",
                   "stencil", "rank_grid",
                   "spmv_m", "spmv_matrix", "spmv_form", "spmv_transport", "spmv_library",
                   "spmv_distribute",
@@ -487,6 +487,8 @@ def _parser() -> argparse.ArgumentParser:
                    help="halo: copy-engine puts of one group over this many streams")
     s.add_argument("--move-pairs", default="on", choices=["on", "off"],
                    help="halo, xyzq: x self-wrap moves as row pairs")
+    s.add_argument("--horizontal", default="on", choices=["on", "off"],
+                   help="fused, one rank: offer the halo move and the SpMV as one kernel launch")
     s.add_argument("--stencil", action="store_true",
                    help="halo: add the 7-point stencil (interior beside / shell after the exchange)")
     s.add_argument("--rank-grid", default="", help="halo rank grid PXxPYxPZ (default: prime factors)")

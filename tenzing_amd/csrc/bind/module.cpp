@@ -1133,6 +1133,13 @@ PYBIND11_MODULE(_tz, m) {
       .def("op_graph", [](DistSpmv &s) { return std::const_pointer_cast<Graph>(s.op_graph()); })
       .def("check", [](DistSpmv &s, uintptr_t st) { return s.check(P(st)); }, py::arg("stream") = 0)
       .def("reset_y", [](DistSpmv &s, uintptr_t st) { s.reset_y(P(st)); }, py::arg("stream") = 0);
+  m.def("move_spmv_op", [](std::shared_ptr<HaloExchange> h, std::vector<int> dirs, std::shared_ptr<DistSpmv> s,
+                           std::string name, int lanes, bool intoY) {
+    return make_move_spmv_op(h, std::move(dirs), s, std::move(name), lanes, intoY);
+  }, py::arg("halo"), py::arg("dirs"), py::arg("spmv"), py::arg("name"), py::arg("lanes") = kern::kSpmvIlp + 4,
+     py::arg("into_y") = true,
+     "one GPU op running the halo's self moves `dirs` and the SpMV's local product in one kernel "
+     "(horizontal fusion; the SpMV's workgroups interleaved among the move's)");
   m.def("random_band_matrix", [](int64_t n, int64_t bw, int64_t nnz, uint64_t seed) {
     CsrHost a = random_band_matrix(n, bw, nnz, seed);
     return py::make_tuple(a.rowPtr, a.colInd, a.val);
@@ -1231,6 +1238,43 @@ PYBIND11_MODULE(_tz, m) {
     kern::iota_f64(n, base, scale, reinterpret_cast<double *>(a), P(s));
   }, py::arg("n"), py::arg("base"), py::arg("scale"), py::arg("a"), py::arg("stream") = 0);
   k.def("empty", [](uintptr_t s) { kern::empty(P(s)); }, py::arg("stream") = 0);
+  auto moves_from = [](const std::vector<py::dict> &ds) {
+    std::vector<kern::MoveDesc> ms;
+    for (auto &d : ds) {
+      kern::MoveDesc m;
+      m.src = reinterpret_cast<const double *>(d["src"].cast<uintptr_t>());
+      m.dst = reinterpret_cast<double *>(d["dst"].cast<uintptr_t>());
+      m.src_off = d["src_off"].cast<int64_t>();
+      m.dst_off = d["dst_off"].cast<int64_t>();
+      m.s1 = d.contains("s1") ? d["s1"].cast<int64_t>() : 0;
+      m.s2 = d.contains("s2") ? d["s2"].cast<int64_t>() : 0;
+      m.s3 = d.contains("s3") ? d["s3"].cast<int64_t>() : 0;
+      m.len = d["len"].cast<int32_t>();
+      m.n1 = d.contains("n1") ? d["n1"].cast<int32_t>() : 1;
+      m.n2 = d.contains("n2") ? d["n2"].cast<int32_t>() : 1;
+      m.n3 = d.contains("n3") ? d["n3"].cast<int32_t>() : 1;
+      m.pair = d.contains("pair") && d["pair"].cast<bool>();
+      ms.push_back(m);
+    }
+    return ms;
+  };
+  k.def("box_move_spmv", [moves_from](std::vector<py::dict> ds, int n, uintptr_t rp, uintptr_t ci, uintptr_t v,
+                                      uintptr_t x, uintptr_t y, int lanes, bool acc, uintptr_t s) {
+    const std::vector<kern::MoveDesc> ms = moves_from(ds);
+    kern::SpmvJob j;
+    j.nRows = n;
+    j.rowPtr = reinterpret_cast<const int32_t *>(rp);
+    j.colInd = reinterpret_cast<const int32_t *>(ci);
+    j.val = reinterpret_cast<const float *>(v);
+    j.x = reinterpret_cast<const float *>(x);
+    j.y = reinterpret_cast<float *>(y);
+    j.lanes = lanes;
+    j.accumulate = acc;
+    kern::box_move_spmv(ms.data(), int(ms.size()), j, P(s));
+  }, py::arg("moves"), py::arg("n_rows"), py::arg("row_ptr"), py::arg("col_ind"), py::arg("val"),
+     py::arg("x"), py::arg("y"), py::arg("lanes") = kern::kSpmvIlp + 4, py::arg("accumulate") = false,
+     py::arg("stream") = 0,
+     "the direct moves (as box_move_many) and one ILP CSR SpMV in one launch, workgroups interleaved");
   k.def("box_move_many", [](std::vector<py::dict> ds, uintptr_t s) {
     std::vector<kern::MoveDesc> ms;
     for (auto &d : ds) {

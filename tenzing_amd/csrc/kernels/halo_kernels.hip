@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
+#include "spmv_device.hpp"
 
 #include <algorithm>
 #include <cstdio>
@@ -362,10 +363,9 @@ __device__ __forceinline__ void pair_body(const DevDesc &d, uint32_t tid, uint32
   }
 }
 
+// one logical block `lb` of a batch of moves (box_move_many_k, box_move_spmv_k)
 template <int U, bool NT, bool NTS>
-__global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap r) {
-  const uint32_t lb = logical_block(r);
-  if (lb >= r.total) return; // padding of the remapped launch (no barriers in this kernel)
+__device__ __forceinline__ void move_block(const DevBatch &b, const DevRemap &r, uint32_t lb) {
   int box = 0;
   while (box + 1 < b.n && lb >= b.block_start[box + 1]) ++box;
   const DevDesc &d = b.d[box];
@@ -382,6 +382,40 @@ __global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap
   else if (d.vec < 0) pair_body<U, NTS>(d, tid, nth);
   else if (d.vec >= 3) peel_body<NT, NTS>(d, tid, nth);
   else move_body<1, U, NT, NTS>(d, tid, nth);
+}
+
+template <int U, bool NT, bool NTS>
+__global__ __launch_bounds__(kThreads) void box_move_many_k(DevBatch b, DevRemap r) {
+  const uint32_t lb = logical_block(r);
+  if (lb >= r.total) return; // padding of the remapped launch (no barriers in this kernel)
+  move_block<U, NT, NTS>(b, r, lb);
+}
+
+// the SpMV half of box_move_spmv_k (kernel arguments: device pointers and sizes)
+struct SpmvDev {
+  const int32_t *rowPtr, *colInd;
+  const float *val, *x;
+  float *y;
+  int32_t nRows, accumulate;
+  uint32_t nBlocks, stride; // SpMV workgroups; one every `stride` workgroups of the launch
+};
+
+// horizontal fusion: workgroup b is SpMV workgroup b / stride when b % stride == 0 (and that
+// index < nBlocks), else move workgroup b - (SpMV workgroups at or before b). Both kinds are
+// dispatched side by side from the first wave on. No barriers: a workgroup returns as soon as
+// its part is done.
+template <int U, bool NT, bool NTS, int W, int K>
+__global__ __launch_bounds__(kThreads) void box_move_spmv_k(DevBatch b, SpmvDev sp) {
+  const uint32_t bid = blockIdx.x;
+  const uint32_t k = bid / sp.stride;
+  if (bid % sp.stride == 0 && k < sp.nBlocks) {
+    dev::csr_spmv_ilp_row<W, K>(int(k) * kThreads + int(threadIdx.x), sp.nRows, sp.rowPtr, sp.colInd,
+                                sp.val, sp.x, sp.y, sp.accumulate);
+    return;
+  }
+  const uint32_t before = min(sp.nBlocks, k + 1);
+  DevRemap r{};
+  move_block<U, NT, NTS>(b, r, bid - before);
 }
 
 // shape-matched roof (line_roof): whole lines, 16-B accesses; d.vec carries the mode. U items
@@ -796,6 +830,54 @@ void box_move_many(const MoveDesc *moves, int n, void *stream) {
   if (U == 1) launch_move<1>(g, s, b, r, t.nt_move, t.nt_move_store);
   else if (U == 2) launch_move<2>(g, s, b, r, t.nt_move, t.nt_move_store);
   else launch_move<4>(g, s, b, r, t.nt_move, t.nt_move_store);
+  TZ_HIP_LAUNCH_CHECK();
+}
+
+namespace {
+template <int W, int K>
+void launch_move_spmv(const dim3 &g, hipStream_t s, const DevBatch &b, const SpmvDev &sp, bool ntl,
+                      bool nts) {
+  // one item in flight per lane, as the tuned move (BoxTuning::move_unroll 1)
+  if (ntl && nts) hipLaunchKernelGGL((box_move_spmv_k<1, true, true, W, K>), g, dim3(kThreads), 0, s, b, sp);
+  else if (ntl) hipLaunchKernelGGL((box_move_spmv_k<1, true, false, W, K>), g, dim3(kThreads), 0, s, b, sp);
+  else if (nts) hipLaunchKernelGGL((box_move_spmv_k<1, false, true, W, K>), g, dim3(kThreads), 0, s, b, sp);
+  else hipLaunchKernelGGL((box_move_spmv_k<1, false, false, W, K>), g, dim3(kThreads), 0, s, b, sp);
+}
+static_assert(sizeof(DevBatch) + sizeof(SpmvDev) <= 4096, "box_move_spmv_k kernargs over 4 KB");
+} // namespace
+
+void box_move_spmv(const MoveDesc *moves, int n, const SpmvJob &job, void *stream) {
+  if (n > kMaxBoxes) throw std::runtime_error("box_move_spmv: too many boxes");
+  if (job.nRows < 0 || (job.nRows > 0 && (!job.rowPtr || !job.y)))
+    throw std::runtime_error("box_move_spmv: bad SpMV job");
+  const int W = job.lanes - kSpmvIlp;
+  if (W != 1 && W != 2 && W != 4) throw std::runtime_error("box_move_spmv: lanes must be kSpmvIlp + 1, 2 or 4");
+  uint32_t total = 0;
+  std::vector<int> keep;
+  const int items = std::max(1, box_tuning().move_items);
+  const DevBatch b = n > 0 ? make_move_batch(moves, n, total, keep, 0, items) : DevBatch{};
+  SpmvDev sp{};
+  sp.rowPtr = job.rowPtr;
+  sp.colInd = job.colInd;
+  sp.val = job.val;
+  sp.x = job.x;
+  sp.y = job.y;
+  sp.nRows = job.nRows;
+  sp.accumulate = job.accumulate ? 1 : 0;
+  sp.nBlocks = uint32_t((int64_t(job.nRows) * W + kThreads - 1) / kThreads);
+  const uint64_t all = uint64_t(total) + sp.nBlocks;
+  if (all == 0) return;
+  if (all >= (uint64_t(1) << 31)) throw std::runtime_error("box_move_spmv: grid too large");
+  // an odd stride: the dispatcher deals workgroup b to XCD b % 8, so an even stride would put
+  // every SpMV workgroup on the same XCD (a stride of 8: all on XCD 0, 61 instead of 50 us)
+  sp.stride = sp.nBlocks ? uint32_t(all / sp.nBlocks) : uint32_t(all + 1);
+  if (sp.nBlocks && sp.stride % 2 == 0) sp.stride -= 1;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 g{unsigned(all)};
+  const BoxTuning &t = box_tuning();
+  if (W == 1) launch_move_spmv<1, 16>(g, s, b, sp, t.nt_move, t.nt_move_store);
+  else if (W == 2) launch_move_spmv<2, 8>(g, s, b, sp, t.nt_move, t.nt_move_store);
+  else launch_move_spmv<4, 4>(g, s, b, sp, t.nt_move, t.nt_move_store);
   TZ_HIP_LAUNCH_CHECK();
 }
 

@@ -65,6 +65,7 @@ void usage() {
          "  [--hostsplit auto|off|force] [--hostsplit-fracs F1,F2,...] [--hostsplit-chunks N]\n"
          "  [--wide-puts auto|on|off] [--wide-put-blocks N]\n"
          "  [--ipc-grid auto|0|1] [--copy-puts on|off] [--copy-engines N] [--move-pairs on|off]\n"
+         "  [--horizontal on|off]   halo+spmv on one rank: offer the move + SpMV as one launch\n"
          "  [--ctrl auto|tcp|mpi|self] [--mpi-lib PATH] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
          "  [--checkpoint PATH] [--resume PATH] [--seed-schedule PATH] [--watchdog S]\n"
@@ -298,6 +299,26 @@ int main(int argc, char **argv) {
       spmv = std::make_shared<DistSpmv>(s, ctrl.get());
       if (!sim) spmv->setup(ctrl.get());
       spmv->add_to_graph(*g);
+    }
+    if (workload == "halo+spmv") {
+      // horizontal fusion, as the Python builder (tenzing_amd/models/fused.py): on one rank with
+      // every halo direction a self move, a top-level choice between the two workloads' own ops
+      // and one launch running the move and the SpMV's local product together
+      const std::string hz = opt("horizontal", "on");
+      TZ_CHECK(hz == "on" || hz == "off", "--horizontal must be on or off");
+      std::vector<int> direct;
+      for (int i = 0; i < halo->ndirs(); ++i)
+        if (halo->is_direct(i)) direct.push_back(i);
+      if (hz == "on" && size == 1 && int(direct.size()) == halo->ndirs() && !halo->args().stencil) {
+        std::vector<OpPtr> alts = {std::make_shared<StaticCompoundOp>("hs_separate", g)};
+        for (int w : {4, 2})
+          alts.push_back(make_move_spmv_op(halo, direct, spmv, "hs_onelaunch_i" + std::to_string(w),
+                                           kern::kSpmvIlp + w, true));
+        auto top = std::make_shared<StaticChoiceOp>("hs_launches", alts);
+        g = std::make_shared<Graph>();
+        g->start_then(top);
+        g->then_finish(top);
+      }
     }
     if (workload == "diamond") {
       auto k1 = std::make_shared<BusyKernelOp>("k1", 20), k2 = std::make_shared<BusyKernelOp>("k2", 100),

@@ -672,6 +672,20 @@ void DistSpmv::spmv_local(int lanes, void *stream, bool intoY) const {
                  lanes > 0 ? lanes : lanes_, false, stream);
 }
 
+kern::SpmvJob DistSpmv::local_job(int lanes, bool intoY) const {
+  TZ_CHECK(ready(), "spmv not set up");
+  kern::SpmvJob j;
+  j.nRows = int(local_rows());
+  j.rowPtr = dLocalRow_.as<int32_t>();
+  j.colInd = dLocalCol_.as<int32_t>();
+  j.val = dLocalVal_.as<float>();
+  j.x = dX_.as<float>();
+  j.y = (intoY ? dY_ : dYl_).as<float>();
+  j.lanes = lanes;
+  j.accumulate = false;
+  return j;
+}
+
 void DistSpmv::spmv_remote(void *stream, bool accumulate) const {
   // an empty remote block leaves y_r at the zeros set up once (split form) and adds nothing
   // (accumulate form)

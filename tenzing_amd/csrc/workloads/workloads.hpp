@@ -691,6 +691,9 @@ public:
   static constexpr int kLibrary = -2;
   /// local block product into the partial y_l (or straight into y when `into_y`)
   void spmv_local(int lanes, void *stream, bool into_y = false) const;
+  /// the local product as a kernel job (y_l, or y itself with `into_y`), for kernels that run
+  /// it inside another launch (kern::box_move_spmv)
+  kern::SpmvJob local_job(int lanes, bool into_y) const;
   /// remote block product into the partial y_r (or y += ... when `accumulate`); no launch
   /// when the remote block is empty
   void spmv_remote(void *stream, bool accumulate = false) const;
@@ -753,5 +756,12 @@ private:
   std::shared_ptr<Graph> form_graph(bool accum, const std::string &p);
   OpPtr local_op(bool accum, const std::string &p);
 };
+
+/// Horizontal fusion (fused_ops.cpp): the halo's self moves `dirs` and the SpMV's local product
+/// (into y with `into_y`, else y_l) in ONE kernel launch (kern::box_move_spmv); `lanes`: the ILP
+/// SpMV kernel, kern::kSpmvIlp + 1, 2 or 4 lanes per row
+std::shared_ptr<GpuOp> make_move_spmv_op(std::shared_ptr<const HaloExchange> h, std::vector<int> dirs,
+                                         std::shared_ptr<const DistSpmv> s, std::string name, int lanes,
+                                         bool into_y);
 
 } // namespace tz

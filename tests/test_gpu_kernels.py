@@ -309,3 +309,57 @@ def test_widened_unpack_matches_torch(tz, gpu, order, neighbors, align):
     ghosts = _mask(n, ub, False)
     assert torch.equal(g3[ghosts], exp_all[ghosts])
     assert torch.equal(g3[~allowed], grid[~allowed])
+
+
+@pytest.mark.parametrize("lanes", [1004, 1002, 1001])
+@pytest.mark.parametrize("order", ["qxyz", "xyzq"])
+def test_box_move_spmv_matches_torch(tz, gpu, order, lanes):
+    """horizontal fusion: the 26-direction move and a CSR SpMV in one launch (their workgroups
+    interleaved) give exactly the move's ghosts (torch strided copy) and the SpMV's y (torch
+    fp64 product), with rows that need several passes of the ILP kernel; then accumulate"""
+    a = tz.HaloArgs()
+    a.nx, a.ny, a.nz, a.ghost, a.nq = 40, 24, 18, 3, 3
+    a.neighbors, a.order = 26, order
+    h = tz.HaloExchange(a)
+    grid = torch.randn(h.grid_elems(), dtype=torch.float64, device="cuda")
+    out, exp = grid.clone(), grid.clone()
+    moves = []
+    for i in range(h.ndirs()):
+        s, d = h.pack_box(i), h.unpack_box(h.opposite(i))
+        moves.append(dict(src=out.data_ptr(), dst=out.data_ptr(), src_off=s["grid_off"],
+                          dst_off=d["grid_off"], s1=s["s1"], s2=s["s2"], s3=s["s3"],
+                          len=s["len"], n1=s["n1"], n2=s["n2"], n3=s["n3"]))
+        for i3 in range(s["n3"]):
+            for i2 in range(s["n2"]):
+                so = s["grid_off"] + i2 * s["s2"] + i3 * s["s3"]
+                do = d["grid_off"] + i2 * s["s2"] + i3 * s["s3"]
+                exp.as_strided((s["n1"], s["len"]), (s["s1"], 1), do).copy_(
+                    grid.as_strided((s["n1"], s["len"]), (s["s1"], 1), so))
+    n = 30_000
+    rp, ci, val = tz._tz.random_band_matrix(n, 500, 40 * n, 11)  # 40 per row: several passes
+    rp_t = torch.tensor(rp, dtype=torch.int32, device="cuda")
+    ci_t = torch.tensor(ci, dtype=torch.int32, device="cuda")
+    v_t = torch.tensor(val, dtype=torch.float32, device="cuda")
+    x = torch.randn(n, dtype=torch.float32, device="cuda")
+    y = torch.full((n,), 7.0, dtype=torch.float32, device="cuda")
+    A = torch.sparse_csr_tensor(rp_t.long().cpu(), ci_t.long().cpu(), v_t.cpu(), size=(n, n)).to_dense()
+    ref = A.double() @ x.double().cpu()
+    args = (n, rp_t.data_ptr(), ci_t.data_ptr(), v_t.data_ptr(), x.data_ptr(), y.data_ptr(), lanes)
+    tz._tz.kernels.box_move_spmv(moves, *args, False, _stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, exp)
+    assert torch.allclose(y.double().cpu(), ref, rtol=1e-4, atol=1e-4)
+    tz._tz.kernels.box_move_spmv(moves, *args, True, _stream())  # y += A x; the move again
+    torch.cuda.synchronize()
+    assert torch.equal(out, exp)
+    assert torch.allclose(y.double().cpu(), 2 * ref, rtol=1e-4, atol=2e-4)
+    # SpMV only / move only: the same launcher with an empty half
+    y.zero_()
+    tz._tz.kernels.box_move_spmv([], *args, False, _stream())
+    out2 = grid.clone()
+    for m in moves:
+        m["src"] = m["dst"] = out2.data_ptr()
+    tz._tz.kernels.box_move_spmv(moves, 0, 0, 0, 0, 0, 0, lanes, False, _stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(y.double().cpu(), ref, rtol=1e-4, atol=1e-4)
+    assert torch.equal(out2, exp)

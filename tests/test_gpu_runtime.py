@@ -631,3 +631,31 @@ def test_bench_save_best_then_run(tz, gpu, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["correct"] and j["halo_bad_cells"] == 0 and j["ms_per_iter"] > 0
+
+
+@pytest.mark.parametrize("alt", ["hs_onelaunch_i4", "hs_onelaunch_i2", "hs_separate"])
+def test_config5_one_launch_schedule_is_exact(tz, gpu, alt):
+    """BASELINE config 5 on one GPU: each hs_launches alternative, eager and compiled to a
+    hipGraph, leaves every ghost cell exact and y = A x (the workloads' own checks), from two grid
+    generations"""
+    from tenzing_amd.models import HaloConfig, SpmvConfig, build_fused
+    from tenzing_amd.search import greedy_schedule
+
+    h, s, g = build_fused(HaloConfig(n=48, neighbors=26, order="qxyz", fuse="choice"),
+                          SpmvConfig(m=20_000), tz.SelfCtrl(), 0)
+    seq = greedy_schedule(g, tz.Platform(4), {"hs_launches": alt, "*": ["allfused", "accum"]},
+                          stream_for=lambda n: 1 if n.startswith("he_") else 0)
+    names = [o.name for o in seq.ops() if isinstance(o, tz._tz.BoundGpuOp)]
+    assert (names == [alt]) == alt.startswith("hs_onelaunch"), names
+    for mode in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+        rt = tz.HipRuntime(device=0, n_streams=4, mode=mode, graph_unroll=3)
+        for gen in (1, 2):
+            h.init_grid(gen=gen)
+            s.reset_y()
+            rt.device_sync()
+            rt.prepare(seq)
+            rt.run(1)
+            rt.device_sync()
+            assert h.check_grid() == 0, (alt, mode, gen)
+            assert s.check() < 1e-4, (alt, mode, gen)
+        del rt
