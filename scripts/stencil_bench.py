@@ -24,6 +24,10 @@ def main():
     ap.add_argument("--zcs", default="32,64", help="z-chunk lengths to sweep (16, 32, 64)")
     ap.add_argument("--pfs", default="1,2")
     ap.add_argument("--dbs", default="1,0")
+    ap.add_argument("--xcds", default="0", help="tile orders: 0 hardware, 1 XCD-contiguous")
+    ap.add_argument("--rounds", type=int, default=1,
+                    help="time every configuration this many times, interleaved (one line each)")
+    ap.add_argument("--no-direct", action="store_true", help="skip the non-LDS kernel")
     a = ap.parse_args()
     n, nq, g = a.n, 3, 3
     st = torch.cuda.current_stream().cuda_stream
@@ -42,9 +46,12 @@ def main():
         O = torch.empty_like(G)
         base = g * sz + g * sy + x0
         nbytes = 2 * 8 * n ** 3 * nq
-        configs = [(True, ty, int(zc), int(pf), db == "1") for ty in (8, 16)
-                   for zc in a.zcs.split(",") for pf in a.pfs.split(",") for db in a.dbs.split(",")]
-        configs += [(False, 8, 32, 1, False)]
+        configs = [(True, ty, int(zc), int(pf), db == "1", x == "1") for ty in (8, 16)
+                   for zc in a.zcs.split(",") for pf in a.pfs.split(",") for db in a.dbs.split(",")
+                   for x in a.xcds.split(",")]
+        if not a.no_direct:
+            configs += [(False, 8, 32, 1, False, False)]
+        configs = configs * max(1, a.rounds)
         # roof: torch's contiguous copy of the whole padded grid (read + write every element)
         for _ in range(3):
             O.copy_(G)
@@ -59,8 +66,9 @@ def main():
         us = statistics.median(ts)
         print(json.dumps({"order": order, "copy_roof": True, "us": round(us, 1),
                           "TBps": round(2 * 8 * G.numel() / us / 1e6, 2)}), flush=True)
-        for lds, ty, zc, pf, db in configs:
+        for lds, ty, zc, pf, db, xcd in configs:
             tz._tz.kernels.set_stencil_tuning(ty, zc, pf, db)
+            tz._tz.kernels.set_stencil_xcd_tiles(xcd)
 
             def fn():
                 tz._tz.kernels.stencil7(G.data_ptr(), O.data_ptr(), base, row, n, n, nouter, sy, sz,
@@ -76,7 +84,8 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1e3)
             us = statistics.median(ts)
-            print(json.dumps({"order": order, "lds": lds, "ty": ty, "zc": zc, "pf": pf, "db": db, "us": round(us, 1),
+            print(json.dumps({"order": order, "lds": lds, "ty": ty, "zc": zc, "pf": pf, "db": db,
+                              "xcd_tiles": xcd, "us": round(us, 1),
                               "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
         del G, O
         torch.cuda.empty_cache()

@@ -1216,13 +1216,17 @@ PYBIND11_MODULE(_tz, m) {
      py::arg("c0") = 0.4, py::arg("c1") = 0.1, py::arg("lds") = true, py::arg("stream") = 0);
   k.def("set_stencil_tuning", [](int ty, int zc, int pf, bool db) {
     TZ_CHECK(ty == 8 || ty == 16, "stencil ty must be 8 or 16");
-    TZ_CHECK(zc == 16 || zc == 32 || zc == 64, "stencil zc must be 16, 32 or 64");
+    TZ_CHECK(zc == 16 || zc == 32 || zc == 64 || zc == 128, "stencil zc must be 16, 32, 64 or 128");
+    TZ_CHECK(zc != 128 || pf == 1, "stencil zc 128 takes pf 1");
     TZ_CHECK(pf == 1 || pf == 2, "stencil pf must be 1 or 2");
     kern::stencil_tuning().ty = ty;
     kern::stencil_tuning().zc = zc;
     kern::stencil_tuning().pf = pf;
     kern::stencil_tuning().db = db;
-  }, py::arg("ty") = 16, py::arg("zc") = 16, py::arg("pf") = 1, py::arg("db") = true);
+  }, py::arg("ty") = 16, py::arg("zc") = 64, py::arg("pf") = 1, py::arg("db") = true);
+  k.def("set_stencil_xcd_tiles", [](bool on) { kern::stencil_tuning().xcd_tiles = on; }, py::arg("on"),
+        "stencil tiles in XCD-contiguous order (each XCD a contiguous range of tiles)");
+  k.def("get_stencil_xcd_tiles", []() { return kern::stencil_tuning().xcd_tiles; });
   k.def("gather_f32", [](int n, uintptr_t src, uintptr_t idx, uintptr_t dst, uintptr_t s) {
     kern::gather_f32(n, reinterpret_cast<const float *>(src), reinterpret_cast<const int32_t *>(idx),
                      reinterpret_cast<float *>(dst), P(s));

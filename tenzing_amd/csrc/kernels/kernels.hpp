@@ -251,11 +251,17 @@ struct StencilBox {
 /// stencil launch shape: rows per workgroup tile (4, 8, 16) and planes per z chunk (32, 64)
 struct StencilTuning {
   int ty = 16; // 64 x 16 tiles (scripts/stencil_bench.py)
-  // 16-plane chunks: 4x the workgroups of 64-plane chunks for two extra planes read per chunk;
-  // 1580 vs 1620 us at 512^3 x 3 (profiles/archive/r2_move_shape/stencil_zc.jsonl)
-  int zc = 16;
+  // 64-plane chunks with the tiles in XCD-contiguous order (below): 512^3 x 3, interleaved
+  // A/B in one process, QXYZ 1538 us / XYZQ 1483 us, against 1569-1573 / 1566 us for the best
+  // hardware-order tiling (16-plane chunks, whose 4x the workgroups had beaten 64-plane ones in
+  // the hardware order) and 1605 / 1589 us for torch's copy of the padded grid
+  // (profiles/r6_stencil/)
+  int zc = 64;
   int pf = 1;  // planes in flight beyond z + 1 (1 or 2)
   bool db = true; // double-buffered LDS tile (one barrier per plane instead of two)
+  // tiles in XCD-contiguous order (each XCD a contiguous range of tiles, so a tile's row aprons
+  // come from its own L2; FETCH_SIZE -8 %) instead of the hardware's round-robin over the 8 XCDs
+  bool xcd_tiles = true;
 };
 StencilTuning &stencil_tuning();
 /// out = c0 * in + c1 * (sum of the 6 face neighbours) over the box; `lds`: 2.5-D LDS-tiled

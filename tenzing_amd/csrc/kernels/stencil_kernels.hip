@@ -56,19 +56,36 @@ template <> struct VT<2> {
 
 // PF: planes prefetched ahead of the z + 1 plane (1: z + 2; 2: z + 2 and z + 3), i.e. the
 // loads each lane keeps in flight; the tile is double-buffered, one barrier per plane
+// Tile order of the launch: per = 0, the hardware order (blockIdx.x / y / z = x tile, row tile,
+// z chunk, so consecutive workgroups -- dealt round-robin to the 8 XCDs -- sit on different XCDs
+// and a tile's row apron comes from another XCD's L2 or from memory); per > 0, a 1-D launch of
+// 8 * per workgroups where XCD k runs tiles [k * per, (k + 1) * per) in (x, row, z-chunk) order,
+// so the tiles above and below a tile run on its own XCD at about the same time
+struct TileGrid {
+  uint32_t gx, gy, gz, per;
+};
+
 template <bool LDS, int VX, int TY, int ZC, int PF, bool DB>
-__global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
+__global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b, TileGrid tg) {
+  uint32_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (tg.per) {
+    const uint32_t l = (blockIdx.x % 8u) * tg.per + blockIdx.x / 8u;
+    if (l >= tg.gx * tg.gy * tg.gz) return; // launch padding: the whole workgroup, before any barrier
+    bx = l % tg.gx;
+    by = (l / tg.gx) % tg.gy;
+    bz = l / (tg.gx * tg.gy);
+  }
   using V = VT<VX>;
   using T = typename V::T;
   constexpr int W = TX * VX;              // elements per tile row
   constexpr int LW = W + 2 * XS_MAX;      // LDS row width
   __shared__ double tiles[LDS && DB ? 2 : 1][TY + 2][LW];
   const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
-  const int r = blockIdx.x * W + tx * VX; // first element of this thread within the row
-  const int y = blockIdx.y * TY + ty;     // row
+  const int r = int(bx) * W + tx * VX; // first element of this thread within the row
+  const int y = int(by) * TY + ty;     // row
   const int zChunks = (b.nz + ZC - 1) / ZC;
-  const int outer = blockIdx.z / zChunks; // XYZQ: quantity
-  const int z0 = (blockIdx.z % zChunks) * ZC;
+  const int outer = int(bz) / zChunks; // XYZQ: quantity
+  const int z0 = (int(bz) % zChunks) * ZC;
   const int z1 = min(z0 + ZC, b.nz);
   // VX = 2 launches only when row is even: a thread's two elements are both in or both out
   // output elements of the box (m0 / m1 masked at the row ends); VX = 2 pairs straddling a
@@ -105,8 +122,8 @@ __global__ __launch_bounds__(TX *TY) void stencil7_k(StencilBox b) {
     }
     alr[a] = lr;
     alc[a] = lc;
-    agr[a] = blockIdx.x * W + lc - XS_MAX;
-    agy[a] = blockIdx.y * TY + lr - 1;
+    agr[a] = int(bx) * W + lc - XS_MAX;
+    agy[a] = int(by) * TY + lr - 1;
     // apron cells outside [-xs, row + xs) x [-1, ny] feed no stored output: never loaded
     aok[a] = LDS && k < NAPRON && agr[a] >= llo && agr[a] < lhi && agy[a] >= -1 && agy[a] <= b.ny;
   }
@@ -264,9 +281,15 @@ template <bool LDS, int VX, int TY, int ZC, int PF, bool DB>
 void launch_stencil_db(const StencilBox &b, hipStream_t s) {
   const int W = TX * VX;
   const int zChunks = (b.nz + ZC - 1) / ZC;
-  const dim3 g(unsigned((b.row + W - 1) / W), unsigned((b.ny + TY - 1) / TY),
-               unsigned(zChunks * b.nouter));
-  hipLaunchKernelGGL((stencil7_k<LDS, VX, TY, ZC, PF, DB>), g, dim3(TX * TY), 0, s, b);
+  TileGrid tg{unsigned((b.row + W - 1) / W), unsigned((b.ny + TY - 1) / TY), unsigned(zChunks * b.nouter), 0};
+  dim3 g(tg.gx, tg.gy, tg.gz);
+  if (stencil_tuning().xcd_tiles) {
+    const uint64_t total = uint64_t(tg.gx) * tg.gy * tg.gz;
+    if (total >= (uint64_t(1) << 31)) throw std::runtime_error("stencil7: too many tiles");
+    tg.per = unsigned((total + 7) / 8);
+    g = dim3(tg.per * 8);
+  }
+  hipLaunchKernelGGL((stencil7_k<LDS, VX, TY, ZC, PF, DB>), g, dim3(TX * TY), 0, s, b, tg);
 }
 
 template <bool LDS, int VX, int TY, int ZC, int PF>
@@ -281,6 +304,8 @@ void launch_zc(const StencilBox &b, hipStream_t s) {
   if (t.zc == 64) {
     if (t.pf >= 2) launch_stencil<LDS, VX, TY, 64, 2>(b, s);
     else launch_stencil<LDS, VX, TY, 64, 1>(b, s);
+  } else if (t.zc == 128) {
+    launch_stencil<LDS, VX, TY, 128, 1>(b, s);
   } else if (t.zc == 16) {
     if (t.pf >= 2) launch_stencil<LDS, VX, TY, 16, 2>(b, s);
     else launch_stencil<LDS, VX, TY, 16, 1>(b, s);

@@ -160,12 +160,17 @@ def test_vector_kernels(tz, gpu):
     assert torch.equal(io, 3.0 + 0.5 * torch.arange(1000, dtype=torch.float64, device="cuda"))
 
 
-@pytest.fixture(params=[(16, 16, 1), (16, 64, 1), (8, 32, 2), (16, 16, 2)], ids=lambda t: "ty%d-zc%d-pf%d" % t)
+@pytest.fixture(params=[(16, 16, 1, 0), (16, 64, 1, 0), (8, 32, 2, 0), (16, 16, 2, 0), (16, 16, 1, 1),
+                        (8, 64, 1, 1)], ids=lambda t: "ty%d-zc%d-pf%d-xcd%d" % t)
 def stencil_tuning(tz, request):
-    """kernel tilings (rows per tile, planes per chunk, planes in flight); restores the default"""
-    tz._tz.kernels.set_stencil_tuning(*request.param)
+    """kernel tilings (rows per tile, planes per chunk, planes in flight, XCD-contiguous tile
+    order); restores the default"""
+    prev = tz._tz.kernels.get_stencil_xcd_tiles()
+    tz._tz.kernels.set_stencil_tuning(*request.param[:3])
+    tz._tz.kernels.set_stencil_xcd_tiles(bool(request.param[3]))
     yield request.param
     tz._tz.kernels.set_stencil_tuning()
+    tz._tz.kernels.set_stencil_xcd_tiles(prev)
 
 
 @pytest.mark.parametrize("nx", [100, 99, 1])  # even rows: 2 per thread; odd: 1; 1: thin box
