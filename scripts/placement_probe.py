@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--spacer-mb", default="0",
                     help="hold this much device memory before each grid (other placements); a "
                          "comma list gives one size per grid")
+    ap.add_argument("--xcd-remaps", default="0",
+                    help="comma list of the move's block orders to time per grid (0, 1, 2)")
     ap.add_argument("--dispatches", default="", help="summarize a counter CSV instead")
     a = ap.parse_args()
     if a.dispatches:
@@ -77,11 +79,18 @@ def main():
         h, _ = build_halo(HaloConfig(n=a.n, neighbors=26, order=order, ghost_align=int(align),
                                      transport="direct", pitch_pad=pad), tz.SelfCtrl(), 0)
         halos.append(h)
+    k = tz._tz.kernels
+    prev = k.get_xcd_remap()
     for g, h in enumerate(halos):
-        us = [_time_move(h, a.iters) for _ in range(2)]
         va = h.grid_ptr()
-        print(json.dumps({"grid": g, "layout": a.layout, "spacer_mb": sp[g], "grid_va": hex(va),
-                          "grid_va_mod_1GB_MB": (va % (1 << 30)) >> 20, "move_us": us}), flush=True)
+        rec = {"grid": g, "layout": a.layout, "spacer_mb": sp[g], "grid_va": hex(va),
+               "grid_va_mod_1GB_MB": (va % (1 << 30)) >> 20}
+        for mode in (int(v) for v in a.xcd_remaps.split(",")):
+            k.set_xcd_remap(mode)
+            us = [_time_move(h, a.iters) for _ in range(2)]
+            rec["move_us" if mode == 0 else f"move_us_remap{mode}"] = us
+        k.set_xcd_remap(prev)
+        print(json.dumps(rec), flush=True)
     st = torch.cuda.current_stream().cuda_stream
     for h in halos:
         for _ in range(a.reps):
