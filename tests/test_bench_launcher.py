@@ -53,3 +53,35 @@ def test_self_spawned_ranks_rendezvous_and_the_failure_is_relayed():
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["partial"] is True and j["launcher"] == "bench.py"
     assert "[2, 2]" in j["error"]
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("tz_bench", BENCH)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_spmv_transport_of_a_schedule():
+    b = _bench_module()
+    assert b.spmv_via(["a_Pack", "a_yl_i4", "a_exchange", "a_yr"]) == "rccl"
+    assert b.spmv_via(["spmv_i_put", "spmv_i_wait", "spmv_yl_w8", "he_put_dx1_dy0_dz0"]) == "ipc"
+    # halo puts are not the SpMV's transport
+    assert b.spmv_via(["spmv_yl_w8", "he_put_dx1_dy0_dz0"]) == "local"
+
+
+def test_launcher_world_from_each_launcher(monkeypatch):
+    b = _bench_module()
+    for k in _LAUNCH + ("SLURM_NTASKS",):
+        monkeypatch.delenv(k, raising=False)
+    assert b.launched_world() is None
+    monkeypatch.setenv("PMI_RANK", "0")
+    assert b.launched_world() == 1  # srun without a task count: one rank
+    monkeypatch.setenv("SLURM_NTASKS", "4")
+    assert b.launched_world() == 4
+    monkeypatch.setenv("OMPI_COMM_WORLD_SIZE", "3")
+    assert b.launched_world() == 3
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    assert b.launched_world() == 8  # torchrun's variables win
