@@ -80,7 +80,7 @@ HipRuntime::HipRuntime(const HipRuntimeOpts &opts)
     }
     streams_.push_back(s);
   }
-  // spare streams (never used) up to TZ_PAD_STREAMS in all: HIP deals its hardware queues to
+  // spare streams (never used) up to pad_streams in all: HIP deals its hardware queues to
   // streams round-robin, and hipGraph launches run their parallel branches on streams of HIP's
   // own; with 3 schedule streams one of those landed on the launch stream's queue (three
   // independent 200 us kernels: 447 us per launch; with 4-8 streams owned: 241-244 us; a host

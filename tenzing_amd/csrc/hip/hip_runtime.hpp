@@ -159,7 +159,7 @@ private:
   int device_ = 0;
   ExecMode mode_;
   std::vector<void *> streams_;
-  std::vector<void *> spare_;    // never used: hardware-queue padding (TZ_PAD_STREAMS)
+  std::vector<void *> spare_;    // never used: hardware-queue padding (pad_streams)
   int pad_ = 0;                  // streams owned at least (schedule streams + spares)
   std::vector<void *> events_;   // schedule events
   std::vector<void *> internal_; // StreamWait helpers

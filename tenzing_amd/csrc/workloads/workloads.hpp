@@ -538,7 +538,7 @@ private:
   /// their own; a failure drops only that variant
   void wide_put_preflight(Ctrl *ctrl);
   // copy-engine puts can spread every copy over this many streams (one SDMA engine each; env
-  // TZ_COPY_ENGINES). One engine moves ~60 GB/s, and independent copies on 2 / 4 streams reach
+  // HaloArgs::copy_engines). One engine moves ~60 GB/s, and independent copies on 2 / 4 streams reach
   // 120 / 235 GB/s. Forking the chunks from the op's stream and joining them back through events
   // costs more than it gains (19 MB: 58 GB/s on one stream, 33 on two, 15 on four;
   // scripts/sdma_probe.hip, profiles/archive/r2_sdma/), so the default keeps one stream per op and
