@@ -1014,6 +1014,12 @@ PYBIND11_MODULE(_tz, m) {
              d["x_offset_cells"] = g.xoff;   // padding before x = 0 (the first ghost cell)
              d["row_pitch_elems"] = g.sy;    // doubles per pitched row
              d["grid_bytes"] = double(h.grid_elems()) * 8.0;
+             // element strides of the logical (q, z, y, x) index, x counted from the first
+             // ghost cell at element offset x_offset_cells * stride x
+             const bool q = g.order == 1;
+             d["strides_qzyx"] = py::make_tuple(q ? 1 : g.sq, g.sz, g.sy, q ? int64_t(g.nq) : 1);
+             d["shape_qzyx"] = py::make_tuple(g.nq, g.nz + 2 * g.g, g.ny + 2 * g.g, g.nx + 2 * g.g);
+             d["ghost"] = g.g;
              return d;
            }, "storage layout: order, x padding before the first ghost cell, row pitch")
       .def("exchange_bytes", &HaloExchange::exchange_bytes)
@@ -1022,6 +1028,10 @@ PYBIND11_MODULE(_tz, m) {
       .def("ready", &HaloExchange::ready)
       .def("add_to_graph", &HaloExchange::add_to_graph)
       .def("grid_ptr", [](const HaloExchange &h) { return reinterpret_cast<uintptr_t>(h.grid()); })
+      .def("read_grid", [](HaloExchange &h, uintptr_t dst, uintptr_t s) { h.copy_grid(P(dst), false, P(s)); },
+           py::arg("dst"), py::arg("stream") = 0, "copy grid_elems() doubles of storage to dst")
+      .def("write_grid", [](HaloExchange &h, uintptr_t src, uintptr_t s) { h.copy_grid(P(src), true, P(s)); },
+           py::arg("src"), py::arg("stream") = 0, "overwrite the grid storage from src")
       .def("init_grid", [](HaloExchange &h, uintptr_t s, int gen) { h.init_grid(P(s), gen); },
            py::arg("stream") = 0, py::arg("gen") = 0)
       .def("check_grid", [](HaloExchange &h, uintptr_t s) { return h.check_grid(P(s)); }, py::arg("stream") = 0)

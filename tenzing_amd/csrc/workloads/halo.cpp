@@ -784,6 +784,16 @@ uint64_t HaloExchange::check_grid(void *stream) {
   return n;
 }
 
+void HaloExchange::copy_grid(void *ptr, bool toGrid, void *stream) {
+  TZ_CHECK(ready(), "halo not set up");
+  TZ_CHECK(ptr, "copy_grid: null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t bytes = gridElems_ * sizeof(double);
+  if (toGrid) TZ_HIP(hipMemcpyAsync(grid(), ptr, bytes, hipMemcpyDefault, s));
+  else TZ_HIP(hipMemcpyAsync(ptr, grid(), bytes, hipMemcpyDefault, s));
+  TZ_HIP(hipStreamSynchronize(s));
+}
+
 void HaloExchange::check_pipelined(int i) const {
   TZ_CHECK(i >= 0 && i < ndirs(), "direction " << i << " out of range");
   TZ_CHECK(!direct_[i], "direction " << dirs_[i].name()

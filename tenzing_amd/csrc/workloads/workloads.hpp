@@ -301,6 +301,10 @@ public:
   void init_grid(void *stream = nullptr, int gen = 0);
   /// number of wrong elements after an exchange (0 = all ghosts correct, interior untouched)
   uint64_t check_grid(void *stream = nullptr);
+  /// copy the whole grid storage (grid_elems() doubles) to `ptr` (toGrid false) or from it
+  /// (toGrid true); any device or host pointer; synchronous. Lets a test check an exchange
+  /// against an independent model of the layout instead of check_grid's own formula
+  void copy_grid(void *ptr, bool toGrid, void *stream = nullptr);
   /// stencil mode: number of output cells that differ from the stencil of the initialized grid
   uint64_t check_stencil(void *stream = nullptr);
   /// stencil mode: apply the stencil to an interior region: 0 = ghost-free interior

@@ -1,0 +1,119 @@
+"""An independent model of a completed halo exchange, in plain torch.
+
+`HaloExchange.check_grid` counts wrong cells with a device kernel whose expected values come
+from the same geometry code as the exchange itself (`csrc/kernels/halo_kernels.hip`,
+`halo_expect`). The reference has no halo output or fixture to compare against (its halo driver
+does not build at HEAD: `include/tenzing/graph.hpp:62-65` vs
+`src/halo_exchange/ops_halo_exchange.cu:50`), so this module pins the exchange to a model that
+shares nothing with the native code:
+
+- the global field is random (not an encoded coordinate), generated on the host by torch from a
+  seed, the same on every rank;
+- the expected local block is a slice of the field padded periodically by ``torch.nn.functional
+  .pad(mode="circular")``;
+- the grid is read back through the storage strides the workload reports
+  (``HaloExchange.layout()``), so the layout itself is checked as well.
+
+The semantics are those of the reference's exchange (`src/halo_exchange/ops_halo_exchange.cu`):
+periodic boundaries over the rank grid, ghost width ``g`` on every side, 6 neighbours fill the
+face ghosts only, 26 fill faces, edges and corners.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def global_field(nq: int, extent_zyx, seed: int) -> torch.Tensor:
+    """random fp64 field (nq, GZ, GY, GX), identical on every rank for one seed"""
+    gen = torch.Generator().manual_seed(int(seed))
+    return torch.rand((nq, *extent_zyx), generator=gen, dtype=torch.float64)
+
+
+def ghost_class(n_zyx, g: int) -> torch.Tensor:
+    """number of ghost axes (0 interior, 1 face, 2 edge, 3 corner) of every padded cell (z, y, x)"""
+    out = None
+    for axis, n in enumerate(n_zyx):
+        i = torch.arange(n + 2 * g)
+        ghost = ((i < g) | (i >= n + g)).to(torch.int8)
+        shape = [1, 1, 1]
+        shape[axis] = n + 2 * g
+        ghost = ghost.view(shape)
+        out = ghost if out is None else out + ghost
+    return out
+
+
+def expected_block(field: torch.Tensor, coords_zyx, n_zyx, g: int, neighbors: int,
+                   before: torch.Tensor) -> torch.Tensor:
+    """the padded local block (nq, nz+2g, ny+2g, nx+2g) of the rank at `coords_zyx` after a
+    complete exchange; cells the exchange does not fill keep their `before` values"""
+    padded = F.pad(field.unsqueeze(0), (g, g, g, g, g, g), mode="circular")[0]
+    sl = [slice(None)]
+    for c, n in zip(coords_zyx, n_zyx):
+        sl.append(slice(c * n, c * n + n + 2 * g))
+    block = padded[tuple(sl)].clone()
+    if neighbors == 6:
+        keep = (ghost_class(n_zyx, g) >= 2).to(block.device).expand_as(block)
+        block[keep] = before[keep]
+    return block
+
+
+def logical_view(storage: torch.Tensor, layout: dict) -> torch.Tensor:
+    """(q, z, y, x) view of a flat copy of the grid storage, x counted from the first ghost cell"""
+    st = tuple(int(s) for s in layout["strides_qzyx"])
+    shape = tuple(int(s) for s in layout["shape_qzyx"])
+    off = int(layout["x_offset_cells"]) * st[3]
+    return torch.as_strided(storage, shape, st, off)
+
+
+class ExchangeCheck:
+    """load a random field into a halo workload's grid and check an exchange against the model.
+
+    The field is drawn on the host (the same on every rank); the copies of the grid and the
+    model live on `device` ("cpu", or "cuda:N" for large grids)."""
+
+    def __init__(self, halo, seed: int = 0, sentinel: float = -2.5, device="cpu"):
+        self.halo = halo
+        self.device = torch.device(device)
+        self.layout = halo.layout()
+        self.g = int(self.layout["ghost"])
+        nq, Z, Y, X = (int(s) for s in self.layout["shape_qzyx"])
+        self.nq = nq
+        self.n_zyx = (Z - 2 * self.g, Y - 2 * self.g, X - 2 * self.g)
+        cx, cy, cz = halo.coords()
+        px, py, pz = halo.rank_grid()
+        self.coords_zyx = (cz, cy, cx)
+        extent = tuple(c * n for c, n in zip((pz, py, px), self.n_zyx))
+        self.field = global_field(nq, extent, seed).to(self.device)
+        self.sentinel = sentinel
+        self.neighbors = int(halo.args.neighbors)
+
+    def load(self):
+        """interior = this rank's slice of the field, every ghost cell = sentinel"""
+        storage = torch.zeros(self.halo.grid_elems(), dtype=torch.float64, device=self.device)
+        self._sync()
+        self.halo.read_grid(storage.data_ptr())
+        view = logical_view(storage, self.layout)
+        view.fill_(self.sentinel)
+        g = self.g
+        sl = [slice(None)] + [slice(c * n, (c + 1) * n) for c, n in zip(self.coords_zyx, self.n_zyx)]
+        view[:, g:-g, g:-g, g:-g] = self.field[tuple(sl)]
+        self.before = view.clone()
+        self._sync()  # torch's writes land before the copy (the copy runs on the null stream)
+        self.halo.write_grid(storage.data_ptr())
+
+    def mismatches(self) -> dict:
+        """cells that differ from the model, by ghost class (0 interior ... 3 corner)"""
+        storage = torch.empty(self.halo.grid_elems(), dtype=torch.float64, device=self.device)
+        self._sync()
+        self.halo.read_grid(storage.data_ptr())
+        got = logical_view(storage, self.layout)
+        want = expected_block(self.field, self.coords_zyx, self.n_zyx, self.g, self.neighbors,
+                              self.before)
+        bad = got != want
+        cls = ghost_class(self.n_zyx, self.g).to(self.device).expand_as(bad)
+        return {k: int(bad[cls == k].sum()) for k in range(4)}
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)

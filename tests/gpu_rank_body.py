@@ -319,6 +319,49 @@ def main():
         from tenzing_amd.utils.env import runtime_libraries
         out["runtime"] = runtime_libraries()
         del rt
+    elif case == "parity":
+        # every transport between real ranks against the independent torch model
+        # (tenzing_amd/utils/halo_ref.py): each rank loads its slice of one random global field
+        # and checks its whole padded block after the exchange
+        from tenzing_amd.utils.halo_ref import ExchangeCheck
+
+        n = int(os.environ.get("TZ_TEST_N", "24"))
+        transport = os.environ.get("TZ_TEST_TRANSPORT", "ipc")
+        res = []
+        for order in os.environ.get("TZ_TEST_ORDERS", "qxyz,xyzq").split(","):
+            for neighbors in (6, 26):
+                halo, g = build_halo(HaloConfig(n=n, neighbors=neighbors, order=order,
+                                                transport=transport, fuse="choice",
+                                                hostsplit="off"), ctrl, dev)
+                rt = tz.HipRuntime(device=dev, n_streams=3, watchdog_s=60.0)
+                for mode in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+                    rt.set_mode(mode)
+                    for seed in range(int(os.environ.get("TZ_TEST_SEEDS", "2"))):
+                        msg = ""
+                        if ctrl.rank == 0:
+                            msg = tz.random_rollout(tz.State(g, tz.Platform(3)), seed).json(True)
+                        seq = tz.OpIndex(g).sequence_from_json(ctrl.bcast(msg, 0).decode())
+                        chk = ExchangeCheck(halo, seed=17 * seed + neighbors)
+                        chk.load()
+                        ctrl.barrier()
+                        rt.prepare(seq)
+                        rt.run(1)
+                        rt.device_sync()
+                        ctrl.barrier()
+                        m1 = chk.mismatches()
+                        ctrl.barrier()
+                        rt.run(3)
+                        rt.device_sync()
+                        ctrl.barrier()
+                        m2 = chk.mismatches()
+                        say(order, neighbors, str(mode), seed, m1, m2)
+                        res.append(dict(order=order, neighbors=neighbors, mode=str(mode),
+                                        seed=seed, bad1=sum(m1.values()), bad2=sum(m2.values()),
+                                        by_class=m1, transport=halo.transport(),
+                                        coords=list(halo.coords())))
+                        ctrl.barrier()
+                del rt, halo
+        out["runs"] = res
     elif case == "ipc_abort":
         # a candidate that hangs on rank 0 (a spinning kernel ahead of its puts): the watchdogs
         # abort it on every rank, the benchmarker fails it collectively, the recovery hooks reset

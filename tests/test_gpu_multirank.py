@@ -654,3 +654,33 @@ def test_bench_self_launched_two_ranks_with_subrecords_loopback(gpu):
         assert rec["config"]["spmv_transport"] in ("ipc", "rccl"), rec["config"]
     assert sp["config"]["rccl_nranks"] is None  # (loopback: RCCL refused)
     assert fu["config"]["halo_transport"] not in (None, "direct"), fu["config"]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_exchange_matches_independent_torch_model_loopback(gpu, world):
+    """IPC puts between real ranks against the torch model of the exchange (random field,
+    circular padding, strides as reported): 2 ranks (1x1x2, x and y wrap onto the rank itself)
+    and 8 ranks (2x2x2, the driver's node, every direction remote), both orders, 6 and 26
+    neighbours, eager and as hipGraphs"""
+    res = _launch("parity", world, timeout=170,
+                  extra_env={"TZ_TEST_ORDERS": "qxyz,xyzq" if world == 2 else "qxyz",
+                             "TZ_TEST_SEEDS": "2" if world == 2 else "1"})
+    coords = set()
+    for r in res:
+        assert r["runs"], r
+        for run in r["runs"]:
+            assert run["bad1"] == run["bad2"] == 0, run
+            assert run["transport"] == ("ipc" if world == 8 else "direct+ipc"), run
+        coords.add(tuple(r["runs"][0]["coords"]))
+    assert len(coords) == world
+
+
+@rccl_loopback
+def test_rccl_exchange_matches_independent_torch_model_loopback(gpu):
+    """the RCCL transport between 2 real ranks against the same model"""
+    res = _launch("parity", 2, timeout=170,
+                  extra_env={"TZ_RCCL_LOOPBACK": "1", "TZ_TEST_TRANSPORT": "rccl",
+                             "TZ_TEST_ORDERS": "qxyz", "TZ_TEST_SEEDS": "1"})
+    for r in res:
+        for run in r["runs"]:
+            assert run["bad1"] == run["bad2"] == 0 and run["transport"] == "rccl", run
