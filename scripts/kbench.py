@@ -1,6 +1,7 @@
 """Isolated kernel bandwidth microbenchmarks for the halo / copy kernels (MI355X).
 
-python scripts/kbench.py [--n 512] [--neighbors 26] [--reps 50]
+python scripts/kbench.py [--n 512] [--neighbors 26] [--reps 50] [--order xyzq]
+                         [--ghost-align -2] [--widen-ab]
 Prints one JSON line per measurement: op, bytes moved (read+write), us, GB/s.
 Interleaves variants in one process (methodology rule: A/B in one process).
 """
@@ -35,14 +36,29 @@ def main():
     ap.add_argument("--neighbors", type=int, default=26)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--order", default="xyzq")
+    ap.add_argument("--ghost-align", type=int, default=-2,
+                    help="HaloConfig.ghost_align: -2 auto (16), -1 x = 0 at the row start, 8, 16")
+    ap.add_argument("--widen-ab", action="store_true",
+                    help="only the 26-box unpack with the widened rows off / on, interleaved")
     args = ap.parse_args()
     torch.zeros(1, device="cuda")
-    h, _ = build_halo(HaloConfig(n=args.n, neighbors=args.neighbors, order=args.order,
-                                 transport="copy"), tz.SelfCtrl(), device=0)
-    hd, _ = build_halo(HaloConfig(n=args.n, neighbors=args.neighbors, order=args.order,
-                                  transport="direct"), tz.SelfCtrl(), device=0)
-    print(json.dumps({"order": args.order, "grid_bytes": h.grid_elems() * 8}), flush=True)
+    cfg = dict(n=args.n, neighbors=args.neighbors, order=args.order, ghost_align=args.ghost_align)
+    h, _ = build_halo(HaloConfig(transport="copy", **cfg), tz.SelfCtrl(), device=0)
+    print(json.dumps({"order": args.order, "grid_bytes": h.grid_elems() * 8,
+                      "layout": h.layout()}), flush=True)
     st = torch.cuda.current_stream().cuda_stream
+    if args.widen_ab:
+        K = tz._tz.kernels
+        tot = h.exchange_bytes()
+        for rnd in range(3):
+            for widen in (False, True):
+                K.set_widen_unpack(widen)
+                us = timeit(lambda: h.unpack_all(st), max(5, args.reps // 5))
+                print(json.dumps(dict(op="unpack_all", widen=widen, round=rnd, us=round(us, 3),
+                                      GBps=round(2 * tot / us / 1e3, 1))), flush=True)
+        K.set_widen_unpack(True)
+        return
+    hd, _ = build_halo(HaloConfig(transport="direct", **cfg), tz.SelfCtrl(), device=0)
     out = []
 
     def rec(op, nbytes, us, **kw):
