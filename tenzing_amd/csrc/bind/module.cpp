@@ -1056,6 +1056,15 @@ PYBIND11_MODULE(_tz, m) {
                d["n"] = py::make_tuple(m.n1, m.n2, m.n3);
                d["s"] = py::make_tuple(m.s1, m.s2, m.s3);
                d["pair"] = m.pair;
+               // the keys kernels.box_move_many / move_kinds read (pointers 0 before setup)
+               d["src"] = reinterpret_cast<uintptr_t>(m.src);
+               d["dst"] = reinterpret_cast<uintptr_t>(m.dst);
+               d["s1"] = m.s1;
+               d["s2"] = m.s2;
+               d["s3"] = m.s3;
+               d["n1"] = m.n1;
+               d["n2"] = m.n2;
+               d["n3"] = m.n3;
                l.append(d);
              }
              return l;
@@ -1289,23 +1298,12 @@ PYBIND11_MODULE(_tz, m) {
      py::arg("x"), py::arg("y"), py::arg("lanes") = kern::kSpmvIlp + 4, py::arg("accumulate") = false,
      py::arg("stream") = 0,
      "the direct moves (as box_move_many) and one ILP CSR SpMV in one launch, workgroups interleaved");
-  k.def("box_move_many", [](std::vector<py::dict> ds, uintptr_t s) {
-    std::vector<kern::MoveDesc> ms;
-    for (auto &d : ds) {
-      kern::MoveDesc m;
-      m.src = reinterpret_cast<const double *>(d["src"].cast<uintptr_t>());
-      m.dst = reinterpret_cast<double *>(d["dst"].cast<uintptr_t>());
-      m.src_off = d["src_off"].cast<int64_t>();
-      m.dst_off = d["dst_off"].cast<int64_t>();
-      m.s1 = d.contains("s1") ? d["s1"].cast<int64_t>() : 0;
-      m.s2 = d.contains("s2") ? d["s2"].cast<int64_t>() : 0;
-      m.s3 = d.contains("s3") ? d["s3"].cast<int64_t>() : 0;
-      m.len = d["len"].cast<int32_t>();
-      m.n1 = d.contains("n1") ? d["n1"].cast<int32_t>() : 1;
-      m.n2 = d.contains("n2") ? d["n2"].cast<int32_t>() : 1;
-      m.n3 = d.contains("n3") ? d["n3"].cast<int32_t>() : 1;
-      ms.push_back(m);
-    }
+  k.def("move_kinds", [moves_from](std::vector<py::dict> ds) {
+    const std::vector<kern::MoveDesc> ms = moves_from(ds);
+    return kern::move_kinds(ms.data(), int(ms.size()));
+  }, py::arg("moves"), "how box_move_many would move each box (no GPU needed)");
+  k.def("box_move_many", [moves_from](std::vector<py::dict> ds, uintptr_t s) {
+    const std::vector<kern::MoveDesc> ms = moves_from(ds);
     kern::box_move_many(ms.data(), int(ms.size()), P(s));
   }, py::arg("moves"), py::arg("stream") = 0);
   k.def("set_box_tuning", [](int unroll, bool ntPack, bool ntUnpack, int maxBlocks, bool ntMove) {

@@ -1047,6 +1047,20 @@ DevBatch make_move_batch(const MoveDesc *moves, int n, uint32_t &total, std::vec
 }
 } // namespace
 
+std::vector<std::string> move_kinds(const MoveDesc *moves, int n) {
+  if (n <= 0) return {};
+  if (n > kMaxBoxes) throw std::runtime_error("move_kinds: too many boxes");
+  uint32_t total = 0;
+  std::vector<int> keep;
+  const DevBatch b = make_move_batch(moves, n, total, keep);
+  std::vector<std::string> out(size_t(n), "empty");
+  for (int k = 0; k < b.n; ++k) {
+    const int v = b.d[k].vec;
+    out[size_t(keep[size_t(k)])] = v < 0 ? "pair" : v >= 3 ? "peeled" : v == 2 ? "vec16" : "vec8";
+  }
+  return out;
+}
+
 std::vector<LineBox> line_boxes(const MoveDesc *moves, int n, bool copies) {
   std::vector<LineBox> reads, writes, moved;
   auto add = [](std::vector<LineBox> &v, const MoveDesc &m, double *base, int64_t off) {

@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <vector>
+#include <string>
 
 namespace tz {
 namespace kern {
@@ -122,6 +123,9 @@ void line_roof(const LineBox *boxes, int n, void *stream, int variant = 0);
 /// shape); otherwise reads and writes are separate boxes. Lines read and written by the same
 /// rows become mode-2 boxes.
 std::vector<LineBox> line_boxes(const MoveDesc *moves, int n, bool copies = true);
+/// how box_move_many would move each box (no launch): "vec16", "vec8", "peeled", "pair" or
+/// "empty"
+std::vector<std::string> move_kinds(const MoveDesc *moves, int n);
 
 /// Completion signal of a move whose destination is another rank's memory (IPC peer put):
 /// when the last block of box i has stored its part, it makes every store of the box visible

@@ -368,3 +368,27 @@ def test_box_move_spmv_matches_torch(tz, gpu, order, lanes):
     torch.cuda.synchronize()
     assert torch.allclose(y.double().cpu(), ref, rtol=1e-4, atol=1e-4)
     assert torch.equal(out2, exp)
+
+
+@pytest.mark.parametrize("nx,g", [(24, 3), (16, 4), (20, 3)])
+def test_row_pair_moves_match_torch(tz, gpu, nx, g):
+    """the x self-wrap of the reference's XYZQ layout (x = 0 at the row start) as one row pair
+    against the two plain moves in torch; the whole grid is compared"""
+    from test_move_kinds import _pair_moves
+
+    h, m = _pair_moves(tz, nx, g, base=1)  # geometry only; pointers below
+    grid = torch.randn(h.grid_elems(), dtype=torch.float64, device="cuda")
+    out, exp = grid.clone(), grid.clone()
+    m = dict(m, src=out.data_ptr(), dst=out.data_ptr())
+    assert tz._tz.kernels.move_kinds([m]) == ["pair"]
+    delta, L = m["dst_off"] - m["src_off"], m["len"]
+    runs = [(m["src_off"], m["dst_off"]), (m["src_off"] + L + delta, m["src_off"] + L)]
+    for i3 in range(m["n3"]):
+        for i2 in range(m["n2"]):
+            for so, do in runs:
+                o = i2 * m["s2"] + i3 * m["s3"]
+                exp.as_strided((m["n1"], L), (m["s1"], 1), do + o).copy_(
+                    grid.as_strided((m["n1"], L), (m["s1"], 1), so + o))
+    tz._tz.kernels.box_move_many([m], _stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, exp)

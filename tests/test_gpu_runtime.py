@@ -666,16 +666,18 @@ def test_config5_one_launch_schedule_is_exact(tz, gpu, alt):
 @pytest.mark.parametrize("transport", ["copy", "direct"])
 @pytest.mark.parametrize("neighbors", [6, 26])
 @pytest.mark.parametrize("order", ["xyzq", "qxyz"])
-def test_exchange_matches_independent_torch_model(tz, gpu, order, neighbors, transport,
+@pytest.mark.parametrize("n", [20, 24])
+def test_exchange_matches_independent_torch_model(tz, gpu, n, order, neighbors, transport,
                                                   ghost_align, mode):
     """the exchange against a model that shares no code with it (tenzing_amd/utils/halo_ref.py):
     a random field, torch's circular padding, the grid read back through the reported strides.
     Every ghost cell the exchange fills must equal the model, every other cell must be untouched,
-    over random schedules of the search's choice graph and repeated exchanges."""
+    over random schedules of the search's choice graph and repeated exchanges. n = 24 puts the
+    high x ghost run of the row-start layout on a 64-B boundary, n = 20 does not."""
     from tenzing_amd.models import HaloConfig, build_halo
     from tenzing_amd.utils.halo_ref import ExchangeCheck
 
-    cfg = HaloConfig(n=20, neighbors=neighbors, order=order, transport=transport, fuse="choice",
+    cfg = HaloConfig(n=n, neighbors=neighbors, order=order, transport=transport, fuse="choice",
                      ghost_align=ghost_align)
     halo, g = build_halo(cfg, tz.SelfCtrl(), device=0)
     rt = tz.HipRuntime(device=0, n_streams=3,
