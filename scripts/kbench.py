@@ -40,9 +40,33 @@ def main():
                     help="HaloConfig.ghost_align: -2 auto (16), -1 x = 0 at the row start, 8, 16")
     ap.add_argument("--widen-ab", action="store_true",
                     help="only the 26-box unpack with the widened rows off / on, interleaved")
+    ap.add_argument("--grid-memory-ab", action="store_true",
+                    help="only the 26-direction move, pack and unpack on a coarse- and a "
+                         "fine-grained grid, interleaved")
     args = ap.parse_args()
     torch.zeros(1, device="cuda")
     cfg = dict(n=args.n, neighbors=args.neighbors, order=args.order, ghost_align=args.ghost_align)
+    if args.grid_memory_ab:
+        st = torch.cuda.current_stream().cuda_stream
+        hs = {}
+        for mem in (0, 1):
+            c, _ = build_halo(HaloConfig(transport="copy", grid_memory=mem, **cfg), tz.SelfCtrl(), device=0)
+            d, _ = build_halo(HaloConfig(transport="direct", grid_memory=mem, **cfg), tz.SelfCtrl(), device=0)
+            hs[c.grid_memory()] = (c, d)
+        dirs = list(range(hs["fine"][1].ndirs()))
+        for rnd in range(3):
+            for mem, (c, d) in hs.items():
+                r = dict(op="grid_memory_ab", grid_memory=mem, round=rnd)
+                r["direct_all_us"] = round(timeit(lambda: d.direct_group(dirs, st), max(5, args.reps // 5)), 3)
+                r["pack_all_us"] = round(timeit(lambda: c.pack_all(st), max(5, args.reps // 5)), 3)
+                r["unpack_all_us"] = round(timeit(lambda: c.unpack_all(st), max(5, args.reps // 5)), 3)
+                print(json.dumps(r), flush=True)
+        for mem, (c, d) in hs.items():
+            d.init_grid()
+            d.direct_group(dirs, st)
+            torch.cuda.synchronize()
+            print(json.dumps(dict(grid_memory=mem, check_grid=int(d.check_grid()))), flush=True)
+        return
     h, _ = build_halo(HaloConfig(transport="copy", **cfg), tz.SelfCtrl(), device=0)
     print(json.dumps({"order": args.order, "grid_bytes": h.grid_elems() * 8,
                       "layout": h.layout()}), flush=True)

@@ -983,6 +983,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("copy_puts", &HaloArgs::copy_puts)
       .def_readwrite("copy_engines", &HaloArgs::copy_engines)
       .def_readwrite("move_pairs", &HaloArgs::move_pairs)
+      .def_readwrite("grid_memory", &HaloArgs::grid_memory)
       .def_readwrite("device", &HaloArgs::device)
       .def("json", [](const HaloArgs &a) { return a.json().dump(); });
   py::class_<HaloExchange, std::shared_ptr<HaloExchange>>(m, "HaloExchange")
@@ -1007,6 +1008,7 @@ PYBIND11_MODULE(_tz, m) {
                   },
                   py::arg("box"), py::arg("parts"))
       .def("grid_elems", &HaloExchange::grid_elems)
+      .def("grid_memory", &HaloExchange::grid_memory, "fine or coarse (HaloArgs.grid_memory)")
       .def("layout", [](const HaloExchange &h) {
              const kern::HaloGeom g = h.geom();
              py::dict d;

@@ -50,6 +50,7 @@ Json HaloArgs::json() const {
   j["copy_puts"] = copy_puts;
   j["copy_engines"] = copy_engines;
   j["move_pairs"] = move_pairs;
+  j["grid_memory"] = grid_memory;
   return j;
 }
 
@@ -359,7 +360,11 @@ void HaloExchange::setup(Ctrl *ctrl) {
   if (ready()) return;
   ctrl_ = ctrl;
   if (a_.device >= 0) TZ_HIP(hipSetDevice(a_.device));
-  grid_ = DeviceBuffer(gridElems_ * sizeof(double));
+  TZ_CHECK(a_.grid_memory >= -1 && a_.grid_memory <= 1, "grid_memory must be -1 (auto), 0 or 1");
+  // IPC grid mode: the neighbours' puts store into this grid's ghost cells, as into receive
+  // buffers in buffers mode (DeviceBuffer's peerWritten note)
+  gridFine_ = a_.grid_memory < 0 ? useIpc_ && ipcGrid_ : a_.grid_memory != 0;
+  grid_ = DeviceBuffer(gridElems_ * sizeof(double), gridFine_);
   // staging buffers only for pipelined directions (locality is symmetric: direct_[i] ==
   // direct_[opp(i)], so a pipelined shift(i) never touches a direct direction's buffers)
   send_.resize(ndirs());

@@ -224,6 +224,10 @@ struct HaloArgs {
   // XYZQ self-wrap moves of the x axis as row pairs (one lane moves a row's +x and -x runs,
   // which share lines in the row-start layout); false: separate moves (A/B)
   bool move_pairs = true;
+  // grid memory: -1 auto (fine-grained when peers store into it, i.e. IPC "grid" mode; else
+  // coarse-grained), 0 coarse-grained, 1 fine-grained. A peer's stores over xGMI bypass this
+  // GPU's L2, so a coarse-grained grid may keep stale or dirty lines of the ghost cells
+  int grid_memory = -1;
   // also run a 7-point stencil over the interior after the exchange (into a second grid): the
   // search may update the ghost-free interior while ghosts are in flight and the one-cell
   // boundary shell afterwards, or the whole domain after the exchange (a ChoiceOp)
@@ -391,6 +395,8 @@ public:
   /// returns each credit right after the arrival, so ghosts stay valid only until the peer's
   /// next put: stencil mode (which reads them after the exchange) always uses "buffers".
   std::string ipc_mode() const { return useIpc_ ? (ipcGrid_ ? "grid" : "buffers") : ""; }
+  /// "fine" or "coarse": the grid's memory (set up)
+  std::string grid_memory() const { return gridFine_ ? "fine" : "coarse"; }
   /// relay routing (see HaloArgs::relay) is available: rank grid 2x2x2, ipc buffers mode
   bool uses_relay() const { return relay_ && useIpc_ && (relayReady_ || !ready()); }
   /// relay routing, direct link: put the first (1 - f) share of every face of `faces` and the
@@ -598,6 +604,7 @@ private:
   void ghost_widening(int ghostDx, int64_t dstOff, int32_t len, int32_t &lead, int32_t &trail) const;
   static constexpr int kDefaultComms = 4;
   bool ipcGrid_ = true;
+  bool gridFine_ = false; // the grid is fine-grained memory (HaloArgs::grid_memory)
   std::vector<void *> peerGrid_, peerFlags_; // per rank (nullptr: not a neighbour / self)
   std::vector<void *> peerRecv_;             // per direction: the receiver's buffer ("buffers")
   std::vector<void *> opened_;               // IPC mappings to close

@@ -71,6 +71,9 @@ class HaloConfig:
     copy_puts: bool = True   # copy-engine puts offered (receive buffers only)
     copy_engines: int = 1    # copy-engine puts of one group spread over this many streams
     move_pairs: bool = True  # XYZQ x self-wrap moves as row pairs
+    # grid memory: -1 auto (fine-grained in IPC grid mode, where peers store into it), 0 coarse,
+    # 1 fine-grained
+    grid_memory: int = -1
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":
         a = _tz.HaloArgs()
@@ -96,6 +99,7 @@ class HaloConfig:
         a.copy_puts = bool(self.copy_puts)
         a.copy_engines = int(self.copy_engines)
         a.move_pairs = bool(self.move_pairs)
+        a.grid_memory = int(self.grid_memory)
         if self.rank_grid:
             a.px, a.py, a.pz = (int(v) for v in self.rank_grid)
         a.rank, a.size, a.device = rank, size, device

@@ -51,6 +51,7 @@ def main():
             out["relay_ready"] = halo.uses_relay()
             out["transports"] = halo.transport_report()
             out["rccl_nranks"] = halo.rccl_nranks()
+            out["grid_memory"] = halo.grid_memory()
             from tenzing_amd.search import choice_alternatives
             out["graph_ops"] = choice_alternatives(g, "he_remote")
             out["hostsplit_ready"] = halo.uses_hostsplit()

@@ -464,3 +464,8 @@ def test_runtime_options_flip_both_ways_in_one_process(tz):
     for pairs_on in (True, False):
         a = HaloConfig(n=16, order="xyzq", move_pairs=pairs_on).args(0, 1, -1)
         assert a.move_pairs is pairs_on and '"move_pairs":%s' % str(pairs_on).lower() in a.json().replace(" ", "")
+    for mem in (-1, 0, 1):
+        a = HaloConfig(n=16, grid_memory=mem).args(0, 1, -1)
+        assert a.grid_memory == mem and '"grid_memory":%d' % mem in a.json().replace(" ", "")
+    with pytest.raises(Exception, match="grid_memory"):
+        tz._tz.HaloExchange(HaloConfig(n=16, grid_memory=2).args(0, 1, -1)).setup(None)

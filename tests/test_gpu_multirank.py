@@ -128,6 +128,8 @@ def test_ipc_halo_loopback(gpu, world, mode):
             # 2 ranks: grid 1x1x2 (x, y self-neighbours move directly); 4 ranks: 1x2x2;
             # 8 ranks: 2x2x2, every direction remote
             assert run["transport"] == ("ipc" if world == 8 else "direct+ipc")
+        # peers store into the grid itself in grid mode: fine-grained memory there
+        assert r["grid_memory"] == ("fine" if mode == "grid" else "coarse"), r["grid_memory"]
         # buffers mode also offers copy-engine (SDMA) puts: some schedules must have used them
         used = any(run["copyput"] for run in r["runs"])
         if mode == "grid" or world < 8:  # (8 ranks sample too few schedules to insist)
