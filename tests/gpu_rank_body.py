@@ -26,6 +26,8 @@ def main():
 
     say("start", case)
 
+    import gc
+
     ctrl, dev = init(timeout_s=120)
     say("init done")
     out = {"rank": ctrl.rank, "size": ctrl.size}
@@ -109,18 +111,22 @@ def main():
                                     hostsplit=any(o.name.startswith("he_hs") for o in seq.ops()),
                                     mixed=any(o.name == "he_copyput_mx" for o in seq.ops()),
                                     wide=any(o.name.startswith("he_putw_") for o in seq.ops())))
-            if os.environ.get("TZ_TEST_NO_MCTS"):
-                continue
-            # a short collective search over ipc schedules
-            bench = tz.EmpiricalBenchmarker(rt, ctrl)
-            o = tz.MctsOpts()
-            o.n_iters = 4
-            o.bench = tz.BenchOpts(n_iters=3, max_retries=1, target_secs=0.001)
-            rt.set_mode(tz.ExecMode.Eager)
-            r = tz.mcts_explore(g, tz.Platform(3), bench, ctrl, o)
-            out.setdefault("mcts", []).append(len(r.sims))
-            out.setdefault("mcts_err", []).append(halo.ipc_errors())
-            del rt, halo
+            if not os.environ.get("TZ_TEST_NO_MCTS"):
+                # a short collective search over ipc schedules
+                bench = tz.EmpiricalBenchmarker(rt, ctrl)
+                o = tz.MctsOpts()
+                o.n_iters = 4
+                o.bench = tz.BenchOpts(n_iters=3, max_retries=1, target_secs=0.001)
+                rt.set_mode(tz.ExecMode.Eager)
+                r = tz.mcts_explore(g, tz.Platform(3), bench, ctrl, o)
+                out.setdefault("mcts", []).append(len(r.sims))
+                out.setdefault("mcts_err", []).append(halo.ipc_errors())
+                del bench, r
+            # release this build on every rank before the next one sets up (see "parity")
+            seq = cand = None  # (rank 0's drawn candidates hold the ops too)
+            del rt, halo, g
+            gc.collect()
+            ctrl.barrier()
         out["runs"] = res
     elif case in ("spmv", "fused"):
         from tenzing_amd.models import SpmvConfig, build_fused, build_spmv
@@ -361,7 +367,14 @@ def main():
                                         by_class=m1, transport=halo.transport(),
                                         coords=list(halo.coords())))
                         ctrl.barrier()
-                del rt, halo
+                # release this build (its RCCL communicators, IPC mappings) on every rank before
+                # the next one sets up: the check and the graph hold the workload too, and a
+                # communicator torn down by whichever reference went last, while the next
+                # build's communicators were already in use, failed a send in RCCL's loopback
+                # transport ("internal error")
+                del rt, halo, g, chk, seq
+                gc.collect()
+                ctrl.barrier()
         out["runs"] = res
     elif case == "ipc_abort":
         # a candidate that hangs on rank 0 (a spinning kernel ahead of its puts): the watchdogs
