@@ -43,7 +43,8 @@ def _build_workload(a, ctrl, device, setup):
                     wide_puts=a.wide_puts, wide_put_blocks=a.wide_put_blocks,
                     ipc_grid=None if a.ipc_grid == "auto" else int(a.ipc_grid),
                     copy_puts=a.copy_puts == "on", copy_engines=a.copy_engines,
-                    move_pairs=a.move_pairs == "on")
+                    move_pairs=a.move_pairs == "on",
+                    grid_memory={"auto": -1, "coarse": 0, "fine": 1}[a.grid_memory])
     sc = SpmvConfig(m=a.spmv_m, form=a.spmv_form, transport=a.spmv_transport,
                     matrix=a.spmv_matrix, library=a.spmv_library, distribute=a.spmv_distribute)
     if a.workload == "halo":
@@ -487,6 +488,9 @@ def _parser() -> argparse.ArgumentParser:
                    help="halo: copy-engine puts of one group over this many streams")
     s.add_argument("--move-pairs", default="on", choices=["on", "off"],
                    help="halo, xyzq: x self-wrap moves as row pairs")
+    s.add_argument("--grid-memory", default="auto", choices=["auto", "coarse", "fine"],
+                   help="halo: grid memory (auto: fine-grained where peers store into it, ipc "
+                        "grid mode)")
     s.add_argument("--horizontal", default="on", choices=["on", "off"],
                    help="fused, one rank: offer the halo move and the SpMV as one kernel launch")
     s.add_argument("--stencil", action="store_true",

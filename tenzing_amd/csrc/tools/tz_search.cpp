@@ -65,6 +65,7 @@ void usage() {
          "  [--hostsplit auto|off|force] [--hostsplit-fracs F1,F2,...] [--hostsplit-chunks N]\n"
          "  [--wide-puts auto|on|off] [--wide-put-blocks N]\n"
          "  [--ipc-grid auto|0|1] [--copy-puts on|off] [--copy-engines N] [--move-pairs on|off]\n"
+         "  [--grid-memory auto|coarse|fine]\n"
          "  [--horizontal on|off]   halo+spmv on one rank: offer the move + SpMV as one launch\n"
          "  [--ctrl auto|tcp|mpi|self] [--mpi-lib PATH] [--rdzv-file PATH]\n"
          "  [--master-addr HOST] [--csv PATH] [--jsonl PATH] [--dump-graph PATH] [--dump-tree]\n"
@@ -272,6 +273,9 @@ int main(int argc, char **argv) {
         const std::string mp = opt("move-pairs", "on");
         TZ_CHECK(mp == "on" || mp == "off", "--move-pairs must be on or off");
         h.move_pairs = mp == "on";
+        const std::string gm = opt("grid-memory", "auto");
+        TZ_CHECK(gm == "auto" || gm == "coarse" || gm == "fine", "--grid-memory must be auto, coarse or fine");
+        h.grid_memory = gm == "auto" ? -1 : gm == "fine" ? 1 : 0;
       }
       TZ_CHECK(h.order == "xyzq" || h.order == "qxyz", "--order must be xyzq or qxyz");
       h.rank = rank;

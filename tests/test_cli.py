@@ -293,3 +293,18 @@ def test_bench_names_the_transport_of_a_schedule():
     assert bench.remote_via(["he_hs30_putd", "he_hs30_puth"]) == "hostsplit30"
     assert bench.remote_via(["he_direct_all"]) is None
     assert bench.schedule_via(["he_direct_a", "he_putw_x"]) == ["direct", "ipc_wide"]
+
+
+def test_grid_memory_option_in_both_clis():
+    """both CLIs take --grid-memory, and the native one refuses a bad value"""
+    out = _py("search", "--workload", "halo", "--sim", "--streams", "2", "--iters", "4",
+              "--halo-n", "16", "--bench-iters", "2", "--grid-memory", "fine")
+    assert json.loads(out.strip().splitlines()[-1])["candidates"] == 4
+    exe = os.path.join(ROOT, "tenzing_amd", "bin", "tz-search")
+    ok = subprocess.run([exe, "--sim", "--workload", "halo", "--halo-n", "16", "--streams", "2",
+                         "--iters", "4", "--bench-iters", "2", "--grid-memory", "coarse"],
+                        capture_output=True, text=True, timeout=300)
+    assert ok.returncode == 0, ok.stderr[-2000:]
+    bad = subprocess.run([exe, "--sim", "--workload", "halo", "--halo-n", "16", "--iters", "2",
+                          "--grid-memory", "bogus"], capture_output=True, text=True, timeout=300)
+    assert bad.returncode != 0 and "--grid-memory" in bad.stderr
