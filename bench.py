@@ -1011,7 +1011,13 @@ def _baseline_configs(tz, args, ctrl, device, branch):
     rec["config"] = {"m": sc.m, "streams": 2, "dtype": "fp32",
                      "baseline_ms": 0.0094 if world == 1 else None, **spmv_facts(s, rec)}
     recs["spmv_c2"] = rec
+    # release config 2's workload (its communicators and IPC mappings) on every rank before
+    # config 5 sets up its own
     del rt, s, g
+    import gc
+
+    gc.collect()
+    ctrl.barrier()
 
     grid = tuple(int(v) for v in args.rank_grid.lower().split("x")) if args.rank_grid else ()
     hc = HaloConfig(n=args.n, neighbors=26, order="qxyz", fuse="choice", transport=args.transport,
