@@ -103,7 +103,9 @@ class ExchangeCheck:
         self.halo.write_grid(storage.data_ptr())
 
     def mismatches(self) -> dict:
-        """cells that differ from the model, by ghost class (0 interior ... 3 corner)"""
+        """cells that differ from the model, by ghost class (0 interior ... 3 corner). Call it
+        once the exchange has completed on the device (`HipRuntime.device_sync()`): the copy runs
+        on the null stream, which does not wait for the runtime's non-blocking streams"""
         storage = torch.empty(self.halo.grid_elems(), dtype=torch.float64, device=self.device)
         self._sync()
         self.halo.read_grid(storage.data_ptr())
