@@ -46,10 +46,16 @@ def local_cpus(device: int) -> list[int]:
 
 
 def bind_local_cpus(device: int) -> list[int]:
-    """Pin this process to the GPU-local CPUs (no-op if unknown). Returns the CPU list used."""
+    """Pin this process to the GPU-local CPUs (no-op if unknown). Returns the CPU list used.
+
+    Only the local CPUs this process may run on count. When fewer than 4 of them remain (a
+    cpuset that holds other CPUs than the GPU's), the process stays unpinned: the HIP runtime's
+    and RCCL's helper threads would otherwise share one or two CPUs with the search."""
     cpus = local_cpus(device)
     allowed = os.sched_getaffinity(0)
     cpus = [c for c in cpus if c in allowed]
+    if len(cpus) < min(4, len(allowed)):
+        return []
     if cpus:
         os.sched_setaffinity(0, cpus)
     return cpus

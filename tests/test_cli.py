@@ -96,12 +96,18 @@ def test_cpulist_parsing_and_binding(monkeypatch):
     assert env.parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
     assert env.parse_cpulist("") == []
     allowed = sorted(os.sched_getaffinity(0))
-    monkeypatch.setattr(env, "local_cpus", lambda dev: [allowed[0], 10 ** 6])
+    mine = allowed[:4]
+    monkeypatch.setattr(env, "local_cpus", lambda dev: mine + [10 ** 6])
     try:
-        assert env.bind_local_cpus(0) == [allowed[0]]
-        assert os.sched_getaffinity(0) == {allowed[0]}
+        assert env.bind_local_cpus(0) == mine
+        assert os.sched_getaffinity(0) == set(mine)
     finally:
         os.sched_setaffinity(0, allowed)
+    if len(allowed) >= 4:
+        # one usable local CPU out of several allowed: too few to pin the process to
+        monkeypatch.setattr(env, "local_cpus", lambda dev: [allowed[0], 10 ** 6])
+        assert env.bind_local_cpus(0) == []
+        assert sorted(os.sched_getaffinity(0)) == allowed
     monkeypatch.setattr(env, "local_cpus", lambda dev: [])
     assert env.bind_local_cpus(0) == []
     assert sorted(os.sched_getaffinity(0)) == allowed
