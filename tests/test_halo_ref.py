@@ -38,14 +38,16 @@ def test_field_is_the_same_for_one_seed():
     assert not torch.equal(a, halo_ref.global_field(3, (4, 4, 4), seed=2))
 
 
+@pytest.mark.parametrize("pitch_pad", [0, 16])
 @pytest.mark.parametrize("order", ["xyzq", "qxyz"])
 @pytest.mark.parametrize("ghost_align", [-1, 0, 8, 16])
-def test_reported_strides_address_the_grid(tz, order, ghost_align):
+def test_reported_strides_address_the_grid(tz, order, ghost_align, pitch_pad):
     """every logical cell has its own storage element inside the grid, and x runs along the
     fastest axis of its layout (checked without a GPU: the workload is not set up)"""
     from tenzing_amd.models import HaloConfig, build_halo
 
-    cfg = HaloConfig(n=6, neighbors=26, order=order, ghost_align=ghost_align, transport="direct")
+    cfg = HaloConfig(n=6, neighbors=26, order=order, ghost_align=ghost_align, transport="direct",
+                     pitch_pad=pitch_pad)
     h, _ = build_halo(cfg, tz.SelfCtrl(), setup=False)
     lay = h.layout()
     st, shape = lay["strides_qzyx"], lay["shape_qzyx"]
@@ -55,6 +57,7 @@ def test_reported_strides_address_the_grid(tz, order, ghost_align):
     view += 1  # every logical cell once
     assert int(storage.sum()) == 3 * 12 ** 3 and int(storage.max()) == 1
     assert st[3] == (1 if order == "xyzq" else 3)
+    assert lay["row_pitch_elems"] == st[2] and st[2] % 16 == 0
     if ghost_align == -1:
         assert lay["x_offset_cells"] == 0
     if ghost_align in (8, 16) and order == "xyzq":
