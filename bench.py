@@ -331,6 +331,10 @@ def main() -> int:
                     help="x ghost runs aligned to 16 (line) / 8 (sector) elements, 0 = interior "
                          "rows sector-aligned, -1 = x=0 at the pitched row start (reference), "
                          "-2 = auto (16, line-aligned, in both orders)")
+    ap.add_argument("--torch-model", default="on", choices=["on", "off"],
+                    help="after the headline: one more exchange of the timed schedule from a "
+                         "hashed field, checked against an independent torch model "
+                         "(`torch_model_check`)")
     ap.add_argument("--subrecords", default="auto", choices=["auto", "on", "off"],
                     help="after the headline: BASELINE configs 2 (SpMV, band m / ranks) and 5 "
                          "(SpMV + halo), each searched briefly over this run's transports, "
@@ -818,6 +822,12 @@ def main() -> int:
                          0 if bad == 0 else 3)
 
     stuck = False
+    if args.torch_model == "on":
+        # the timed schedule once more against a model that shares no code with the exchange
+        # (tenzing_amd/utils/halo_ref.py): every rank loads its block of a hashed global field,
+        # runs one exchange and compares its whole padded block with torch's periodic model
+        post_phase("torch_model")
+        post_done("torch_model", torch_model_check=_torch_model_check(tz, rt, ctrl, halo, device))
     # per-link bandwidth of each transport (context for the multi-GPU number: an exchange can
     # not beat the bytes its busiest link carries divided by what one link moves)
     if world > 1 and args.link_probe_iters > 0:
@@ -899,6 +909,41 @@ def main() -> int:
         sys.stdout.flush()
         os._exit(0 if bad == 0 else 3)
     return 0 if bad == 0 else 3
+
+
+def _torch_model_check(tz, rt, ctrl, halo, device):
+    """one exchange of the prepared (timed) schedule from a hashed field, every cell of every
+    rank's padded block compared with tenzing_amd.utils.halo_ref's model; bad cells summed over
+    ranks by ghost class (interior, face, edge, corner). The grid is re-initialized afterwards."""
+    t0 = time.time()
+    try:
+        import torch
+
+        from tenzing_amd.utils.halo_ref import ExchangeCheck
+
+        torch.cuda.set_device(device)
+        rt.device_sync()
+        ctrl.barrier()
+        chk = ExchangeCheck(halo, seed=20261, device=f"cuda:{device}", field="hashed")
+        chk.load()
+        ctrl.barrier()  # every rank's field is in place before any peer's puts land
+        rt.run(1)
+        rt.device_sync()
+        ctrl.barrier()
+        m = chk.mismatches()
+        del chk
+        torch.cuda.empty_cache()
+        by = [int(v) for v in ctrl.allreduce_sum([float(m[k]) for k in range(4)])]
+        val = {"bad_cells": sum(by), "by_ghost_class": by, "field": "hashed"}
+    except Exception as e:  # noqa: BLE001 (a diagnostic after the headline)
+        val = {"error": f"{type(e).__name__}: {e}"}
+    try:
+        halo.init_grid()
+        rt.device_sync()
+    except Exception as e:  # noqa: BLE001
+        val["restore_error"] = f"{type(e).__name__}: {e}"
+    val["s"] = round(time.time() - t0, 2)
+    return val
 
 
 def _sub_runtime(tz, args, device, branch, n_streams):

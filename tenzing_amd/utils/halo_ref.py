@@ -7,8 +7,9 @@ does not build at HEAD: `include/tenzing/graph.hpp:62-65` vs
 `src/halo_exchange/ops_halo_exchange.cu:50`), so this module pins the exchange to a model that
 shares nothing with the native code:
 
-- the global field is random (not an encoded coordinate), generated on the host by torch from a
-  seed, the same on every rank;
+- the global field is random (not an encoded coordinate): drawn by a torch generator from a
+  seed, the same on every rank, or (any size) a multiplicative hash of each cell's global index
+  that each rank evaluates for its own block only;
 - the expected local block is a slice of the field padded periodically by ``torch.nn.functional
   .pad(mode="circular")``;
 - the grid is read back through the storage strides the workload reports
@@ -28,6 +29,39 @@ def global_field(nq: int, extent_zyx, seed: int) -> torch.Tensor:
     """random fp64 field (nq, GZ, GY, GX), identical on every rank for one seed"""
     gen = torch.Generator().manual_seed(int(seed))
     return torch.rand((nq, *extent_zyx), generator=gen, dtype=torch.float64)
+
+
+_P = 2147483647  # 2^31 - 1
+_A = 48271
+
+
+def hashed_values(q: int, gz, gy, gx, extent_zyx, seed: int) -> torch.Tensor:
+    """a pseudo-random value in [0, 1) for every global cell (q, gz, gy, gx) (broadcastable int64
+    tensors of wrapped coordinates): two multiplicative rounds modulo 2^31 - 1 of the cell's
+    linear index. Any rank computes any cell's value without the global field, so the model
+    scales to any rank count; cells closer than 2^31 - 1 in the linear index never share a value"""
+    GZ, GY, GX = (int(e) for e in extent_zyx)
+    idx = ((q * GZ + gz) * GY + gy) * GX + gx
+    h = ((idx % _P) * _A + (int(seed) % 65536) * 16807 + 12345) % _P
+    h = (h * _A) % _P
+    return h.to(torch.float64) / _P
+
+
+def hashed_block(nq: int, coords_zyx, n_zyx, extent_zyx, g: int, seed: int,
+                 device="cpu") -> torch.Tensor:
+    """the padded block (nq, nz+2g, ny+2g, nx+2g) of the rank at `coords_zyx` in the periodic
+    hashed field: its interior is what the rank holds, all of it what a 26-neighbour exchange
+    leaves"""
+    ax = []
+    for k, (c, n, e) in enumerate(zip(coords_zyx, n_zyx, extent_zyx)):
+        i = (torch.arange(n + 2 * g, device=device, dtype=torch.int64) + (c * n - g)) % int(e)
+        shape = [1, 1, 1]
+        shape[k] = n + 2 * g
+        ax.append(i.view(shape))
+    out = torch.empty((nq, *(n + 2 * g for n in n_zyx)), dtype=torch.float64, device=device)
+    for q in range(nq):
+        out[q] = hashed_values(q, ax[0], ax[1], ax[2], extent_zyx, seed)
+    return out
 
 
 def ghost_class(n_zyx, g: int) -> torch.Tensor:
@@ -69,12 +103,19 @@ def logical_view(storage: torch.Tensor, layout: dict) -> torch.Tensor:
 class ExchangeCheck:
     """load a random field into a halo workload's grid and check an exchange against the model.
 
-    The field is drawn on the host (the same on every rank); the copies of the grid and the
-    model live on `device` ("cpu", or "cuda:N" for large grids)."""
+    field "random": drawn on the host by a torch generator, the whole global field on every
+    rank (small grids); "hashed": `hashed_values`, each rank computes only its own block (any
+    size, any rank count). The copies of the grid and the model live on `device` ("cpu", or
+    "cuda:N" for large grids)."""
 
-    def __init__(self, halo, seed: int = 0, sentinel: float = -2.5, device="cpu"):
+    def __init__(self, halo, seed: int = 0, sentinel: float = -2.5, device="cpu",
+                 field: str = "random"):
+        if field not in ("random", "hashed"):
+            raise ValueError(f"field must be random or hashed (got {field!r})")
         self.halo = halo
         self.device = torch.device(device)
+        self.kind = field
+        self.seed = seed
         self.layout = halo.layout()
         self.g = int(self.layout["ghost"])
         nq, Z, Y, X = (int(s) for s in self.layout["shape_qzyx"])
@@ -83,8 +124,9 @@ class ExchangeCheck:
         cx, cy, cz = halo.coords()
         px, py, pz = halo.rank_grid()
         self.coords_zyx = (cz, cy, cx)
-        extent = tuple(c * n for c, n in zip((pz, py, px), self.n_zyx))
-        self.field = global_field(nq, extent, seed).to(self.device)
+        self.extent = tuple(c * n for c, n in zip((pz, py, px), self.n_zyx))
+        self.field = (global_field(nq, self.extent, seed).to(self.device) if field == "random"
+                      else None)
         self.sentinel = sentinel
         self.neighbors = int(halo.args.neighbors)
 
@@ -96,8 +138,12 @@ class ExchangeCheck:
         view = logical_view(storage, self.layout)
         view.fill_(self.sentinel)
         g = self.g
-        sl = [slice(None)] + [slice(c * n, (c + 1) * n) for c, n in zip(self.coords_zyx, self.n_zyx)]
-        view[:, g:-g, g:-g, g:-g] = self.field[tuple(sl)]
+        if self.field is not None:
+            sl = [slice(None)] + [slice(c * n, (c + 1) * n)
+                                  for c, n in zip(self.coords_zyx, self.n_zyx)]
+            view[:, g:-g, g:-g, g:-g] = self.field[tuple(sl)]
+        else:
+            view[:, g:-g, g:-g, g:-g] = self._hashed()[:, g:-g, g:-g, g:-g]
         self.before = view.clone()
         self._sync()  # torch's writes land before the copy (the copy runs on the null stream)
         self.halo.write_grid(storage.data_ptr())
@@ -110,11 +156,21 @@ class ExchangeCheck:
         self._sync()
         self.halo.read_grid(storage.data_ptr())
         got = logical_view(storage, self.layout)
-        want = expected_block(self.field, self.coords_zyx, self.n_zyx, self.g, self.neighbors,
-                              self.before)
+        if self.field is not None:
+            want = expected_block(self.field, self.coords_zyx, self.n_zyx, self.g,
+                                  self.neighbors, self.before)
+        else:
+            want = self._hashed()
+            if self.neighbors == 6:
+                keep = (ghost_class(self.n_zyx, self.g) >= 2).to(self.device).expand_as(want)
+                want[keep] = self.before[keep]
         bad = got != want
         cls = ghost_class(self.n_zyx, self.g).to(self.device).expand_as(bad)
         return {k: int(bad[cls == k].sum()) for k in range(4)}
+
+    def _hashed(self) -> torch.Tensor:
+        return hashed_block(self.nq, self.coords_zyx, self.n_zyx, self.extent, self.g, self.seed,
+                            self.device)
 
     def _sync(self):
         if self.device.type == "cuda":

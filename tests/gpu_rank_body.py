@@ -348,7 +348,8 @@ def main():
                         if ctrl.rank == 0:
                             msg = tz.random_rollout(tz.State(g, tz.Platform(3)), seed).json(True)
                         seq = tz.OpIndex(g).sequence_from_json(ctrl.bcast(msg, 0).decode())
-                        chk = ExchangeCheck(halo, seed=17 * seed + neighbors)
+                        chk = ExchangeCheck(halo, seed=17 * seed + neighbors,
+                                            field=os.environ.get("TZ_TEST_FIELD", "random"))
                         chk.load()
                         ctrl.barrier()
                         rt.prepare(seq)

@@ -34,7 +34,8 @@ def test_bench_one_rank_subrecords(gpu):
     assert bp["tried"] and bp["tried"][0]["probe"]["ratio"] > 0, bp
     assert bp["tried"][0]["probe"]["unrolled"]["ratio"] > 0, bp
     assert j["pad_streams"] == bp["pad_streams"]
-    assert j["post_timing"]["done"] == ["move_roof", "reference_layout", "baseline_configs"]
+    assert j["post_timing"]["done"] == ["torch_model", "move_roof", "reference_layout", "baseline_configs"]
+    assert j["torch_model_check"]["bad_cells"] == 0, j["torch_model_check"]
     for roof in (j["move_roof"], j["reference_layout"]["move_roof"]):
         assert roof["move_us"] > 0 and roof["roof_us"] > 0 and roof["read_lines_MB"] > 0, roof
     ref = j["reference_layout"]

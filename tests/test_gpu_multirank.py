@@ -250,6 +250,9 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     assert j["transport"] == "direct+ipc" and j["config"]["rank_grid"] == [1, 1, 2]
     assert j["value"] > 0 and j["higher_is_better"] is False
     assert j["ipc_mode"] == mode
+    # the timed schedule once more against the independent torch model, every rank's block
+    tm = j["torch_model_check"]
+    assert tm.get("bad_cells") == 0 and sum(tm["by_ghost_class"]) == 0, tm
     # self-describing multi-GPU record: RCCL refused (two ranks on one device), its reason
     # recorded, no communicator size; IPC passed its preflight
     assert j["partial"] is False and j["phase"] == "done"
@@ -304,7 +307,7 @@ def test_bench_two_ranks_loopback(gpu, tmp_path, mode):
     assert (p["pair_GBps"]["sdma"] is not None) == (p["pair_GBps"]["mixed"] is not None) == (mode == "buffers")
     assert p["busiest_link_MB"] > p["face_MB"] > 0 and p["busiest_link_at_probe_rate_ms"] > 0
     # the model calibrated on these rates, beside the measured per-transport seeds
-    assert j["post_timing"]["done"] == ["link_probe", "link_matrix", "topology", "model_check"]
+    assert j["post_timing"]["done"] == ["torch_model", "link_probe", "link_matrix", "topology", "model_check"]
     mc = j["model_check"]
     assert "error" not in mc, mc
     seeded = {r["transport"]: r for r in mc["seeds"] if r["measured_us"] is not None}
@@ -643,6 +646,7 @@ def test_bench_self_launched_two_ranks_with_subrecords_loopback(gpu):
     assert j["n_gpus"] == 2 and j["launcher"] == "bench.py" and j["config"]["rank_grid"] == [1, 1, 2]
     assert j["partial"] is False and j["verified_bad_cells"] == 0
     assert j["verified_bad_cells_after_timing"] == 0
+    assert j["torch_model_check"].get("bad_cells") == 0, j["torch_model_check"]
     assert "baseline_configs" in j["post_timing"]["done"], j["post_timing"]
     assert "reference_layout" not in j  # one-rank only
     bc = j["baseline_configs"]
@@ -666,7 +670,9 @@ def test_exchange_matches_independent_torch_model_loopback(gpu, world):
     neighbours, eager and as hipGraphs"""
     res = _launch("parity", world, timeout=170,
                   extra_env={"TZ_TEST_ORDERS": "qxyz,xyzq" if world == 2 else "qxyz",
-                             "TZ_TEST_SEEDS": "2" if world == 2 else "1"})
+                             "TZ_TEST_SEEDS": "2" if world == 2 else "1",
+                             # 8 ranks: the hashed field, each rank evaluating its own block
+                             "TZ_TEST_FIELD": "random" if world == 2 else "hashed"})
     coords = set()
     for r in res:
         assert r["runs"], r

@@ -624,6 +624,8 @@ def test_bench_save_best_then_run(tz, gpu, tmp_path):
                         "--subrecords", "off", "--save-best", str(path)], cwd=root, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
+    tm = json.loads(r.stdout.strip().splitlines()[-1])["torch_model_check"]
+    assert tm.get("bad_cells") == 0 and tm["field"] == "hashed", tm
     doc = json.loads(path.read_text())
     assert doc["ranks"] == 1 and doc["args"]["halo_n"] == 64 and doc["args"]["neighbors"] == 26
     r = subprocess.run([sys.executable, "-m", "tenzing_amd", "run", str(path), "--iters", "50",
@@ -666,14 +668,15 @@ def test_config5_one_launch_schedule_is_exact(tz, gpu, alt):
 @pytest.mark.parametrize("transport", ["copy", "direct"])
 @pytest.mark.parametrize("neighbors", [6, 26])
 @pytest.mark.parametrize("order", ["xyzq", "qxyz"])
-@pytest.mark.parametrize("n", [20, 24])
-def test_exchange_matches_independent_torch_model(tz, gpu, n, order, neighbors, transport,
+@pytest.mark.parametrize("n,field", [(20, "random"), (24, "hashed")])
+def test_exchange_matches_independent_torch_model(tz, gpu, n, field, order, neighbors, transport,
                                                   ghost_align, mode):
     """the exchange against a model that shares no code with it (tenzing_amd/utils/halo_ref.py):
     a random field, torch's circular padding, the grid read back through the reported strides.
     Every ghost cell the exchange fills must equal the model, every other cell must be untouched,
     over random schedules of the search's choice graph and repeated exchanges. n = 24 puts the
-    high x ghost run of the row-start layout on a 64-B boundary, n = 20 does not."""
+    high x ghost run of the row-start layout on a 64-B boundary, n = 20 does not; n = 24 also
+    uses the hashed field (each rank's block computed on its own)."""
     from tenzing_amd.models import HaloConfig, build_halo
     from tenzing_amd.utils.halo_ref import ExchangeCheck
 
@@ -684,7 +687,7 @@ def test_exchange_matches_independent_torch_model(tz, gpu, n, order, neighbors, 
                        mode=tz.ExecMode.Graph if mode == "graph" else tz.ExecMode.Eager)
     for seed in range(2):
         seq = tz.random_rollout(tz.State(g, tz.Platform(3)), seed)
-        chk = ExchangeCheck(halo, seed=seed)
+        chk = ExchangeCheck(halo, seed=seed, field=field)
         chk.load()
         before = chk.mismatches()
         assert before[0] == 0 and before[1] > 0  # interior loaded, ghosts not yet filled
@@ -713,7 +716,7 @@ def test_headline_exchange_matches_independent_torch_model(tz, gpu):
     ctrl = tz.SelfCtrl()
     res = tz.mcts_explore(g, tz.Platform(4), tz.EmpiricalBenchmarker(rt, ctrl), ctrl, o)
     best = res.sims[res.best()].seq
-    chk = ExchangeCheck(halo, seed=7, device="cuda:0")
+    chk = ExchangeCheck(halo, seed=7, device="cuda:0", field="hashed")
     chk.load()
     rt.prepare(best)
     rt.run(2)

@@ -63,3 +63,18 @@ def test_reported_strides_address_the_grid(tz, order, ghost_align, pitch_pad):
     if ghost_align in (8, 16) and order == "xyzq":
         # the first interior cell (x = ghost) starts an aligned run
         assert (lay["x_offset_cells"] + 3) % ghost_align == 0
+
+
+@pytest.mark.parametrize("coords", [(0, 0, 0), (1, 0, 1), (1, 1, 1)])
+def test_hashed_block_is_the_padded_global_field(coords):
+    """the per-rank hashed block equals circular padding of the materialized hashed field"""
+    n, g, grid, nq = (3, 4, 5), 2, (2, 2, 2), 2
+    ext = tuple(p * k for p, k in zip(grid, n))
+    iz, iy, ix = (torch.arange(e).view(s) for e, s in zip(ext, ((-1, 1, 1), (1, -1, 1), (1, 1, -1))))
+    field = torch.stack([halo_ref.hashed_values(q, iz, iy, ix, ext, 7) for q in range(nq)])
+    assert 0 <= float(field.min()) and float(field.max()) < 1
+    assert field.unique().numel() == field.numel()
+    before = torch.full((nq, *(k + 2 * g for k in n)), -2.5, dtype=torch.float64)
+    want = halo_ref.expected_block(field, coords, n, g, 26, before)
+    assert torch.equal(halo_ref.hashed_block(nq, coords, n, ext, g, 7), want)
+    assert not torch.equal(halo_ref.hashed_block(nq, coords, n, ext, g, 8), want)
