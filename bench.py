@@ -1056,13 +1056,11 @@ def _baseline_configs(tz, args, ctrl, device, branch):
     rec["config"] = {"m": sc.m, "streams": 2, "dtype": "fp32",
                      "baseline_ms": 0.0094 if world == 1 else None, **spmv_facts(s, rec)}
     recs["spmv_c2"] = rec
-    # release config 2's workload (its communicators and IPC mappings) on every rank before
-    # config 5 sets up its own
-    del rt, s, g
-    import gc
-
-    gc.collect()
-    ctrl.barrier()
+    # config 2's workload stays alive until both sub-records are done: its RCCL communicators
+    # are destroyed after the last RCCL operation of the run, never between two workloads'
+    # (tests/gpu_rank_body.py: a teardown there hung or failed the next workload's first send)
+    keep = (s, g)
+    del rt
 
     grid = tuple(int(v) for v in args.rank_grid.lower().split("x")) if args.rank_grid else ()
     hc = HaloConfig(n=args.n, neighbors=26, order="qxyz", fuse="choice", transport=args.transport,
@@ -1098,7 +1096,7 @@ def _baseline_configs(tz, args, ctrl, device, branch):
                      "halo_rccl_nranks": h.rccl_nranks() or None,
                      **spmv_facts(s, rec)}
     recs["fused_c5"] = rec
-    del rt
+    del rt, keep
     return recs
 
 

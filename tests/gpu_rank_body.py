@@ -26,9 +26,8 @@ def main():
 
     say("start", case)
 
-    import gc
-
     ctrl, dev = init(timeout_s=120)
+    keep = []  # workloads built by this rank, kept until exit
     say("init done")
     out = {"rank": ctrl.rank, "size": ctrl.size}
     if case == "ipc_halo":
@@ -123,10 +122,12 @@ def main():
                 out.setdefault("mcts_err", []).append(halo.ipc_errors())
                 del bench, r
             # release this build on every rank before the next one sets up (see "parity")
-            seq = cand = None  # (rank 0's drawn candidates hold the ops too)
-            del rt, halo, g
-            gc.collect()
-            ctrl.barrier()
+            # every workload stays alive until the process ends: RCCL communicators destroyed
+            # between two workloads (in use just before, or just after) hung or failed the next
+            # workload's first send in RCCL's loopback transport, whichever side of the next
+            # setup the teardown fell on
+            keep.append((halo, g))
+            del rt
         out["runs"] = res
     elif case in ("spmv", "fused"):
         from tenzing_amd.models import SpmvConfig, build_fused, build_spmv
@@ -368,14 +369,9 @@ def main():
                                         by_class=m1, transport=halo.transport(),
                                         coords=list(halo.coords())))
                         ctrl.barrier()
-                # release this build (its RCCL communicators, IPC mappings) on every rank before
-                # the next one sets up: the check and the graph hold the workload too, and a
-                # communicator torn down by whichever reference went last, while the next
-                # build's communicators were already in use, failed a send in RCCL's loopback
-                # transport ("internal error")
-                del rt, halo, g, chk, seq
-                gc.collect()
-                ctrl.barrier()
+                # (every workload stays alive until the process ends: see "ipc_halo")
+                keep.append((halo, g))
+                del rt
         out["runs"] = res
     elif case == "ipc_abort":
         # a candidate that hangs on rank 0 (a spinning kernel ahead of its puts): the watchdogs
