@@ -339,6 +339,8 @@ def main():
         for order in os.environ.get("TZ_TEST_ORDERS", "qxyz,xyzq").split(","):
             for neighbors in (6, 26):
                 halo, g = build_halo(HaloConfig(n=n, neighbors=neighbors, order=order,
+                                                nq=int(os.environ.get("TZ_TEST_NQ", "3")),
+                                                ghost=int(os.environ.get("TZ_TEST_GHOST", "3")),
                                                 transport=transport, fuse="choice",
                                                 hostsplit="off"), ctrl, dev)
                 rt = tz.HipRuntime(device=dev, n_streams=3, watchdog_s=60.0)

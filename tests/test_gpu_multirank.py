@@ -692,3 +692,16 @@ def test_rccl_exchange_matches_independent_torch_model_loopback(gpu):
     for r in res:
         for run in r["runs"]:
             assert run["bad1"] == run["bad2"] == 0 and run["transport"] == "rccl", run
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_odd_shape_exchange_matches_independent_torch_model_loopback(gpu, world):
+    """odd interior size, 2 quantities, ghost 2, both orders, IPC puts between real ranks
+    (1x1x2 and 1x2x2), against the torch model's hashed field"""
+    res = _launch("parity", world, timeout=170,
+                  extra_env={"TZ_TEST_N": "17", "TZ_TEST_NQ": "2", "TZ_TEST_GHOST": "2",
+                             "TZ_TEST_SEEDS": "1", "TZ_TEST_FIELD": "hashed"})
+    for r in res:
+        assert r["runs"], r
+        for run in r["runs"]:
+            assert run["bad1"] == run["bad2"] == 0, run

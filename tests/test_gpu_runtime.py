@@ -722,3 +722,28 @@ def test_headline_exchange_matches_independent_torch_model(tz, gpu):
     rt.run(2)
     rt.device_sync()
     assert chk.mismatches() == {0: 0, 1: 0, 2: 0, 3: 0}, best.desc()
+
+
+@pytest.mark.parametrize("shape", [(17, 1, 1), (16, 5, 2), (13, 2, 4), (9, 3, 3), (30, 4, 5)])
+@pytest.mark.parametrize("ghost_align", [-1, -2])
+@pytest.mark.parametrize("transport", ["copy", "direct"])
+@pytest.mark.parametrize("order", ["xyzq", "qxyz"])
+def test_odd_shapes_match_independent_torch_model(tz, gpu, shape, ghost_align, transport, order):
+    """interior sizes, quantity counts and ghost widths away from the headline's (odd n, one
+    quantity, ghost 1 to 5) against the torch model, 26 neighbours, eager and as hipGraphs"""
+    from tenzing_amd.models import HaloConfig, build_halo
+    from tenzing_amd.utils.halo_ref import ExchangeCheck
+
+    n, nq, ghost = shape
+    cfg = HaloConfig(n=n, nq=nq, ghost=ghost, neighbors=26, order=order, transport=transport,
+                     fuse="choice", ghost_align=ghost_align)
+    halo, g = build_halo(cfg, tz.SelfCtrl(), device=0)
+    for mode in (tz.ExecMode.Eager, tz.ExecMode.Graph):
+        rt = tz.HipRuntime(device=0, n_streams=3, mode=mode)
+        seq = tz.random_rollout(tz.State(g, tz.Platform(3)), n + nq + ghost)
+        chk = ExchangeCheck(halo, seed=n * 7 + ghost, field="hashed")
+        chk.load()
+        rt.prepare(seq)
+        rt.run(2)
+        rt.device_sync()
+        assert chk.mismatches() == {0: 0, 1: 0, 2: 0, 3: 0}, (shape, str(mode), seq.desc())
