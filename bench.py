@@ -917,24 +917,9 @@ def _torch_model_check(tz, rt, ctrl, halo, device):
     ranks by ghost class (interior, face, edge, corner). The grid is re-initialized afterwards."""
     t0 = time.time()
     try:
-        import torch
+        from tenzing_amd.utils.halo_ref import check_prepared
 
-        from tenzing_amd.utils.halo_ref import ExchangeCheck
-
-        torch.cuda.set_device(device)
-        rt.device_sync()
-        ctrl.barrier()
-        chk = ExchangeCheck(halo, seed=20261, device=f"cuda:{device}", field="hashed")
-        chk.load()
-        ctrl.barrier()  # every rank's field is in place before any peer's puts land
-        rt.run(1)
-        rt.device_sync()
-        ctrl.barrier()
-        m = chk.mismatches()
-        del chk
-        torch.cuda.empty_cache()
-        by = [int(v) for v in ctrl.allreduce_sum([float(m[k]) for k in range(4)])]
-        val = {"bad_cells": sum(by), "by_ghost_class": by, "field": "hashed"}
+        val = check_prepared(halo, rt, ctrl, device)
     except Exception as e:  # noqa: BLE001 (a diagnostic after the headline)
         val = {"error": f"{type(e).__name__}: {e}"}
     try:

@@ -309,6 +309,12 @@ def cmd_run(a) -> int:
     if "halo" in wl:
         out["halo_bad_cells"] = int(ctrl.allreduce_sum([float(wl["halo"].check_grid())])[0])
         ok &= out["halo_bad_cells"] == 0
+        if a.torch_model == "on":
+            # once more against the independent torch model (tenzing_amd/utils/halo_ref.py)
+            from tenzing_amd.utils.halo_ref import check_prepared
+
+            out["torch_model_check"] = check_prepared(wl["halo"], rt, ctrl, device)
+            ok &= out["torch_model_check"]["bad_cells"] == 0
     if "spmv" in wl:
         out["spmv_max_rel_err"] = ctrl.allreduce_max([wl["spmv"].check()])[0]
         ok &= out["spmv_max_rel_err"] < 1e-4
@@ -528,6 +534,9 @@ def _parser() -> argparse.ArgumentParser:
     u.add_argument("--graph-unroll", type=int, default=20)
     u.add_argument("--watchdog", type=float, default=30.0,
                    help="watchdog floor (s) per run, plus 50 x n x the expected iteration time")
+    u.add_argument("--torch-model", default="on", choices=["on", "off"],
+                   help="halo workloads: also check one exchange against the independent torch "
+                        "model (`torch_model_check`)")
     u.set_defaults(fn=cmd_run)
     return ap
 

@@ -175,3 +175,24 @@ class ExchangeCheck:
     def _sync(self):
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+
+
+def check_prepared(halo, rt, ctrl, device: int, seed: int = 20261) -> dict:
+    """One exchange of the schedule prepared on `rt`, from a hashed field, every cell of every
+    rank's padded block compared with the model on `device`; bad cells summed over ranks by
+    ghost class (interior, face, edge, corner). Collective: every rank calls it together. The
+    grid holds the hashed field afterwards (re-initialize it before a device-side check)."""
+    torch.cuda.set_device(device)
+    rt.device_sync()
+    ctrl.barrier()
+    chk = ExchangeCheck(halo, seed=seed, device=f"cuda:{device}", field="hashed")
+    chk.load()
+    ctrl.barrier()  # every rank's field is in place before any peer's puts land
+    rt.run(1)
+    rt.device_sync()
+    ctrl.barrier()
+    m = chk.mismatches()
+    del chk
+    torch.cuda.empty_cache()
+    by = [int(v) for v in ctrl.allreduce_sum([float(m[k]) for k in range(4)])]
+    return {"bad_cells": sum(by), "by_ghost_class": by, "field": "hashed"}

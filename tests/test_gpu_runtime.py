@@ -559,6 +559,7 @@ def test_search_save_best_then_run(tz, gpu, tmp_path, workload):
     assert path.exists() and s["best_pct10_ms"] > 0
     r = cli("run", str(path), "--iters", "200", "--warmup", "10")
     assert r["correct"] and r["mode"] == "graph" and r["ms_per_iter"] > 0
+    assert r["torch_model_check"]["bad_cells"] == 0, r["torch_model_check"]
     if workload == "halo":
         assert r["halo_bad_cells"] == 0
     else:
@@ -633,6 +634,7 @@ def test_bench_save_best_then_run(tz, gpu, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["correct"] and j["halo_bad_cells"] == 0 and j["ms_per_iter"] > 0
+    assert j["torch_model_check"]["bad_cells"] == 0, j["torch_model_check"]
 
 
 @pytest.mark.parametrize("alt", ["hs_onelaunch_i4", "hs_onelaunch_i2", "hs_separate"])
