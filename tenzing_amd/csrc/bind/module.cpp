@@ -984,6 +984,7 @@ PYBIND11_MODULE(_tz, m) {
       .def_readwrite("copy_engines", &HaloArgs::copy_engines)
       .def_readwrite("move_pairs", &HaloArgs::move_pairs)
       .def_readwrite("grid_memory", &HaloArgs::grid_memory)
+      .def_readwrite("node_tag", &HaloArgs::node_tag)
       .def_readwrite("device", &HaloArgs::device)
       .def("json", [](const HaloArgs &a) { return a.json().dump(); });
   py::class_<HaloExchange, std::shared_ptr<HaloExchange>>(m, "HaloExchange")
@@ -1009,6 +1010,8 @@ PYBIND11_MODULE(_tz, m) {
                   py::arg("box"), py::arg("parts"))
       .def("grid_elems", &HaloExchange::grid_elems)
       .def("grid_memory", &HaloExchange::grid_memory, "fine or coarse (HaloArgs.grid_memory)")
+      .def("off_node_dirs", &HaloExchange::off_node_dirs,
+           "remote directions whose neighbour runs on another node (RCCL only)")
       .def("layout", [](const HaloExchange &h) {
              const kern::HaloGeom g = h.geom();
              py::dict d;

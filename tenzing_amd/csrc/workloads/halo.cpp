@@ -51,6 +51,7 @@ Json HaloArgs::json() const {
   j["copy_engines"] = copy_engines;
   j["move_pairs"] = move_pairs;
   j["grid_memory"] = grid_memory;
+  j["node_tag"] = node_tag;
   return j;
 }
 
@@ -361,6 +362,38 @@ void HaloExchange::setup(Ctrl *ctrl) {
   ctrl_ = ctrl;
   if (a_.device >= 0) TZ_HIP(hipSetDevice(a_.device));
   TZ_CHECK(a_.grid_memory >= -1 && a_.grid_memory <= 1, "grid_memory must be -1 (auto), 0 or 1");
+  if (useIpc_ && ctrl && ctrl->size() > 1) {
+    // IPC needs the neighbour on this node. A direction whose neighbour runs on another node on
+    // ANY rank goes over RCCL on every rank (a shift pairs my send in direction d with my
+    // receive from the opposite side: both ends must use one transport), the other remote
+    // directions keep the IPC transports. One node: nothing changes.
+    const std::vector<std::string> ids = ctrl->allgather(node_identity() + a_.node_tag);
+    TZ_CHECK(int(ids.size()) == a_.size, "allgather returned " << ids.size() << " entries");
+    std::vector<double> off(size_t(ndirs()), 0.0);
+    for (int i = 0; i < ndirs(); ++i)
+      if (ipc_[i] && ids[size_t(nbr_[i])] != ids[size_t(a_.rank)]) off[size_t(i)] = 1.0;
+    ctrl->allreduce_max(off.data(), int(off.size()));
+    offNode_.assign(size_t(ndirs()), 0);
+    int n = 0;
+    for (int i = 0; i < ndirs(); ++i)
+      if (off[size_t(i)] != 0.0) {
+        offNode_[size_t(i)] = 1;
+        ipc_[i] = false;
+        ++n;
+      }
+    if (n > 0) {
+      TZ_CHECK(a_.transport == "auto", "transport " << a_.transport << ": " << n
+                   << " directions have a neighbour on another node, which IPC cannot reach "
+                      "(transport auto sends them over RCCL)");
+      useIpc_ = std::any_of(ipc_.begin(), ipc_.end(), [](bool b) { return b; });
+      // relay routing and the host split assume every face is an IPC put
+      relay_ = false;
+      hsOffered_ = false;
+      useCopy_ = useIpc_ && a_.copy_puts;
+      TZ_LOG(Info, "halo: " << n << " directions cross nodes (RCCL), "
+                            << std::count(ipc_.begin(), ipc_.end(), true) << " stay on IPC");
+    }
+  }
   // IPC grid mode: the neighbours' puts store into this grid's ghost cells, as into receive
   // buffers in buffers mode (DeviceBuffer's peerWritten note)
   gridFine_ = a_.grid_memory < 0 ? useIpc_ && ipcGrid_ : a_.grid_memory != 0;
@@ -495,6 +528,12 @@ void HaloExchange::setup(Ctrl *ctrl) {
   bool piped = false;
   for (int i = 0; i < ndirs(); ++i) piped = piped || pipe_[i];
   if (piped && !useRccl_ && a_.transport != "copy" && !useHost_) {
+    if (!off_node_dirs().empty() && useIpc_ && ipcReady_) {
+      // off-node directions have no IPC path: the host-staged transport carries every remote
+      // direction (one mechanism, agreed by every rank through RCCL's failure agreement)
+      ipcReady_ = false;
+      ipcWhy_ = "RCCL unavailable for the directions that cross nodes: host-staged transport";
+    }
     if (useIpc_ && ipcReady_) {
       for (int i = 0; i < ndirs(); ++i) {
         if (pipe_[i]) {

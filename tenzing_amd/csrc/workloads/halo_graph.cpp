@@ -551,7 +551,7 @@ void HaloExchange::add_fused(Graph &g, const std::vector<int> &dirs, const std::
 }
 
 void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via,
-                                 const std::string &pre) {
+                                 const std::string &pre, const std::string &tagPre) {
   auto self = std::const_pointer_cast<const HaloExchange>(shared_from_this());
   const std::string &f = a_.fuse;
   const bool singleStage = direct_[dirs.front()] || via != kViaPipe;
@@ -565,11 +565,11 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via
     add_chains(g, dirs, via);
   } else if (f == "all" || (f == "pack" && singleStage)) {
     // (direct moves and puts have no pack stage: "pack" degenerates to one fused op)
-    add_fused(g, dirs, "all", via);
+    add_fused(g, dirs, tagPre + "all", via);
   } else if (f == "pack") {
     // fused pack / unpack kernels, per-direction transfers
-    auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, "all");
-    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, dirs, "all");
+    auto p = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Pack, dirs, tagPre + "all");
+    auto u = std::make_shared<HaloStageGroup>(self, HaloStageGroup::Unpack, dirs, tagPre + "all");
     g.start_then(p);
     g.then_finish(u);
     for (int i : dirs) {
@@ -587,7 +587,7 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via
              {"faces", subset(group_dirs(1))}, {"small", subset(group_dirs(0))}})
       if (!gr.second.empty()) groups.push_back(gr);
     if (f == "groups") {
-      for (auto &gr : groups) add_fused(g, gr.second, gr.first, via);
+      for (auto &gr : groups) add_fused(g, gr.second, tagPre + gr.first, via);
       return;
     }
     // per group: split chains vs one fused chain
@@ -596,7 +596,7 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via
       auto split = std::make_shared<Graph>();
       add_chains(*split, gr.second, via);
       auto fused = std::make_shared<Graph>();
-      add_fused(*fused, gr.second, gr.first, via);
+      add_fused(*fused, gr.second, tagPre + gr.first, via);
       std::vector<OpPtr> alts = {
           std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_split", split),
           std::make_shared<StaticCompoundOp>(pre + "he_" + gr.first + "_fused", fused)};
@@ -613,7 +613,7 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via
     // two groups: additionally one chain for every direction (a single launch per stage
     // avoids the two groups' kernels competing for CUs)
     auto all = std::make_shared<Graph>();
-    add_fused(*all, dirs, "all", via);
+    add_fused(*all, dirs, tagPre + "all", via);
     std::vector<OpPtr> top = {std::make_shared<StaticCompoundOp>(pre + "he_grouped", grouped),
                               std::make_shared<StaticCompoundOp>(pre + "he_allfused", all)};
     // remote directions to several peers: one chain per peer as well. Each peer is one xGMI
@@ -630,7 +630,8 @@ void HaloExchange::add_structure(Graph &g, const std::vector<int> &dirs, int via
       for (const auto &kv : byPeer) groupsByPeer.push_back(kv.second);
       std::sort(groupsByPeer.begin(), groupsByPeer.end());
       auto peers = std::make_shared<Graph>();
-      for (const auto &grp : groupsByPeer) add_fused(*peers, grp, "p" + dirs_[grp.front()].name(), via);
+      for (const auto &grp : groupsByPeer)
+        add_fused(*peers, grp, tagPre + "p" + dirs_[grp.front()].name(), via);
       top.push_back(std::make_shared<StaticCompoundOp>(pre + "he_bypeer", peers));
     }
     auto choice = std::make_shared<StaticChoiceOp>(pre + "he_exchange", top);
@@ -727,6 +728,17 @@ void HaloExchange::add_exchange(Graph &g) {
     return;
   }
   TZ_CHECK(ipc || pipe, "no transport available for the remote directions");
+  // directions that cross nodes: RCCL only, a structure of their own (names prefixed "far_");
+  // the IPC alternatives below cover the rest
+  if (pipe && ipc) {
+    std::vector<int> near, far;
+    for (int i : remote) (offNode_.empty() || !offNode_[size_t(i)] ? near : far).push_back(i);
+    if (!far.empty()) {
+      add_structure(g, far, kViaPipe, "far_", "far_");
+      if (near.empty()) return;
+      remote = near;
+    }
+  }
   // the copy-engine variant needs receive buffers ("buffers" mode)
   const bool copy = ipc && useCopy_ && !ipcGrid_;
   std::vector<OpPtr> alts;

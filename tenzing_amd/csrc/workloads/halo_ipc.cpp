@@ -6,6 +6,18 @@
 
 namespace tz {
 
+void HaloExchange::off_node_exchange(void *stream) const {
+  // the directions that cross nodes, over RCCL (pack, shift, unpack; every rank issues the same
+  // shifts in the same order): the IPC preflights run them beside their puts, so that the check
+  // after an exchange covers every ghost cell
+  const std::vector<int> far = off_node_dirs();
+  if (far.empty()) return;
+  TZ_CHECK(useRccl_, "directions that cross nodes need the RCCL transport");
+  for (int i : far) pack(i, stream);
+  for (int i : far) shift(i, stream);
+  for (int i : far) unpack(opp_[i], stream);
+}
+
 void HaloExchange::ipc_preflight(Ctrl *ctrl) {
   // Complete exchanges through IPC before the search may use it: every ghost must arrive
   // (no wait timeout) and be right on every rank. A mapping that "works" but does not deliver
@@ -30,6 +42,7 @@ void HaloExchange::ipc_preflight(Ctrl *ctrl) {
     }
     try {
       if (!local.empty()) direct_group(local, nullptr);
+      off_node_exchange(nullptr); // (directions that cross nodes: RCCL, so the check is whole)
       put_group(remote, nullptr);
       wait_group(remote, nullptr);
       if (!ipcGrid_) ipc_unpack_group(remote, nullptr);
@@ -89,6 +102,7 @@ void HaloExchange::copy_preflight(Ctrl *ctrl) {
     ctrl->barrier();
     try {
       if (!local.empty()) direct_group(local, nullptr);
+      off_node_exchange(nullptr);
       copy_put_group(remote, nullptr, /*sdma=*/k == 1);
       wait_group(remote, nullptr);
       ipc_unpack_group(remote, nullptr);
@@ -180,6 +194,7 @@ void HaloExchange::wide_put_preflight(Ctrl *ctrl) {
   ctrl->barrier();
   try {
     if (!local.empty()) direct_group(local, nullptr);
+    off_node_exchange(nullptr);
     put_group(remote, nullptr, a_.wide_put_blocks);
     wait_group(remote, nullptr);
     if (!ipcGrid_) ipc_unpack_group(remote, nullptr);

@@ -228,6 +228,9 @@ struct HaloArgs {
   // coarse-grained), 0 coarse-grained, 1 fine-grained. A peer's stores over xGMI bypass this
   // GPU's L2, so a coarse-grained grid may keep stale or dirty lines of the ghost cells
   int grid_memory = -1;
+  // appended to this process's node identity (tests: ranks on one node posing as several
+  // nodes). Directions whose neighbour is on another node go over RCCL (see HaloExchange)
+  std::string node_tag;
   // also run a 7-point stencil over the interior after the exchange (into a second grid): the
   // search may update the ghost-free interior while ghosts are in flight and the one-cell
   // boundary shell afterwards, or the whole domain after the exchange (a ChoiceOp)
@@ -399,6 +402,16 @@ public:
   std::string grid_memory() const { return gridFine_ ? "fine" : "coarse"; }
   /// relay routing (see HaloArgs::relay) is available: rank grid 2x2x2, ipc buffers mode
   bool uses_relay() const { return relay_ && useIpc_ && (relayReady_ || !ready()); }
+  /// remote directions whose neighbour runs on another node (on some rank: the split is the
+  /// same on every rank); they go over RCCL while the others keep the IPC transports
+  /// the off-node directions' exchange over RCCL (pack, shift, unpack), collective
+  void off_node_exchange(void *stream) const;
+  std::vector<int> off_node_dirs() const {
+    std::vector<int> v;
+    for (int i = 0; i < int(offNode_.size()); ++i)
+      if (offNode_[size_t(i)]) v.push_back(i);
+    return v;
+  }
   /// relay routing, direct link: put the first (1 - f) share of every face of `faces` and the
   /// whole box of every other direction of `dirs` into the neighbours' receive buffers
   void relay_put_direct(const std::vector<int> &dirs, double frac, void *stream) const;
@@ -484,7 +497,7 @@ private:
   void add_chains(Graph &g, const std::vector<int> &dirs, int via);
   void add_fused(Graph &g, const std::vector<int> &dirs, const std::string &tag, int via);
   void add_structure(Graph &g, const std::vector<int> &dirs, int via,
-                     const std::string &pre); // fuse mode over `dirs`
+                     const std::string &pre, const std::string &tagPre = ""); // fuse mode over `dirs`
   void add_ipc_part(Graph &g, const std::vector<int> &remote, int via);
   void add_relay_part(Graph &g, const std::vector<int> &remote, double frac);
   /// buffers mode: the two faces of every axis go to their peers by different engines at once
@@ -605,6 +618,9 @@ private:
   static constexpr int kDefaultComms = 4;
   bool ipcGrid_ = true;
   bool gridFine_ = false; // the grid is fine-grained memory (HaloArgs::grid_memory)
+  // directions whose neighbour (on some rank) runs on another node: RCCL only, beside IPC for
+  // the rest (set up by node identity; empty on one node)
+  std::vector<char> offNode_;
   std::vector<void *> peerGrid_, peerFlags_; // per rank (nullptr: not a neighbour / self)
   std::vector<void *> peerRecv_;             // per direction: the receiver's buffer ("buffers")
   std::vector<void *> opened_;               // IPC mappings to close

@@ -74,6 +74,9 @@ class HaloConfig:
     # grid memory: -1 auto (fine-grained in IPC grid mode, where peers store into it), 0 coarse,
     # 1 fine-grained
     grid_memory: int = -1
+    # appended to the node identity: ranks of one node posing as several (tests); directions
+    # whose neighbour is on another node go over RCCL, the rest keep IPC
+    node_tag: str = ""
 
     def args(self, rank: int = 0, size: int = 1, device: int = -1) -> "_tz.HaloArgs":
         a = _tz.HaloArgs()
@@ -100,6 +103,7 @@ class HaloConfig:
         a.copy_engines = int(self.copy_engines)
         a.move_pairs = bool(self.move_pairs)
         a.grid_memory = int(self.grid_memory)
+        a.node_tag = str(self.node_tag)
         if self.rank_grid:
             a.px, a.py, a.pz = (int(v) for v in self.rank_grid)
         a.rank, a.size, a.device = rank, size, device

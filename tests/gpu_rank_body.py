@@ -335,6 +335,9 @@ def main():
 
         n = int(os.environ.get("TZ_TEST_N", "24"))
         transport = os.environ.get("TZ_TEST_TRANSPORT", "ipc")
+        # ranks posing as several nodes: TZ_TEST_NODE_TAGS=a,a,b,b gives rank r the r-th tag
+        tags = [t for t in os.environ.get("TZ_TEST_NODE_TAGS", "").split(",") if t]
+        node_tag = tags[ctrl.rank] if tags else ""
         res = []
         for order in os.environ.get("TZ_TEST_ORDERS", "qxyz,xyzq").split(","):
             for neighbors in (6, 26):
@@ -342,7 +345,7 @@ def main():
                                                 nq=int(os.environ.get("TZ_TEST_NQ", "3")),
                                                 ghost=int(os.environ.get("TZ_TEST_GHOST", "3")),
                                                 transport=transport, fuse="choice",
-                                                hostsplit="off"), ctrl, dev)
+                                                hostsplit="off", node_tag=node_tag), ctrl, dev)
                 rt = tz.HipRuntime(device=dev, n_streams=3, watchdog_s=60.0)
                 for mode in (tz.ExecMode.Eager, tz.ExecMode.Graph):
                     rt.set_mode(mode)
@@ -369,7 +372,10 @@ def main():
                         res.append(dict(order=order, neighbors=neighbors, mode=str(mode),
                                         seed=seed, bad1=sum(m1.values()), bad2=sum(m2.values()),
                                         by_class=m1, transport=halo.transport(),
-                                        coords=list(halo.coords())))
+                                        coords=list(halo.coords()),
+                                        off_node=len(halo.off_node_dirs()),
+                                        schedule_via=sorted({o.name.split("_")[1] for o in seq.ops()
+                                                             if o.name.startswith("he_")})))
                         ctrl.barrier()
                 # (every workload stays alive until the process ends: see "ipc_halo")
                 keep.append((halo, g))

@@ -705,3 +705,22 @@ def test_odd_shape_exchange_matches_independent_torch_model_loopback(gpu, world)
         assert r["runs"], r
         for run in r["runs"]:
             assert run["bad1"] == run["bad2"] == 0, run
+
+
+@rccl_loopback
+def test_cross_node_directions_over_rccl_beside_ipc_loopback(gpu):
+    """4 ranks posing as 2 nodes (node tags a, a, b, b; 1x2x2 grid): the z directions cross
+    "nodes" and go over RCCL on every rank, the y directions stay on IPC puts, in one schedule;
+    every rank's whole block against the torch model, eager and as hipGraphs"""
+    res = _launch("parity", 4, timeout=170,
+                  extra_env={"TZ_RCCL_LOOPBACK": "1", "TZ_TEST_TRANSPORT": "auto",
+                             "TZ_TEST_NODE_TAGS": "a,a,b,b", "TZ_TEST_ORDERS": "qxyz",
+                             "TZ_TEST_SEEDS": "1", "TZ_TEST_FIELD": "hashed"})
+    for r in res:
+        assert r["runs"], r
+        for run in r["runs"]:
+            assert run["bad1"] == run["bad2"] == 0, run
+            assert run["transport"] == "direct+rccl+ipc", run
+            # 26 neighbours: the 9 directions with dz = +1 or -1 ... all 18 with dz != 0;
+            # 6 neighbours: the two z faces
+            assert run["off_node"] == (18 if run["neighbors"] == 26 else 2), run
