@@ -721,6 +721,5 @@ def test_cross_node_directions_over_rccl_beside_ipc_loopback(gpu):
         for run in r["runs"]:
             assert run["bad1"] == run["bad2"] == 0, run
             assert run["transport"] == "direct+rccl+ipc", run
-            # 26 neighbours: the 9 directions with dz = +1 or -1 ... all 18 with dz != 0;
-            # 6 neighbours: the two z faces
+            # off-node: every direction with dz != 0 (18 of 26; with 6 neighbours the two z faces)
             assert run["off_node"] == (18 if run["neighbors"] == 26 else 2), run
